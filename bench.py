@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X exclusive-topology placement engine.
+
+Metric (BASELINE.json): exclusive-topology placements/sec at 15k nodes; p99
+recovery placement latency. Workload (`value`): config 2 — a 15,000-node /
+1,000-rack post-delete snapshot and a full-JobSet recovery of 990 jobs x 15
+pods — resident in HBM; one step = one placement of all 990
+jobs (tally kernel + feasibility-bitmap kernel + assignment kernel) from the
+resident snapshot and job list to assign[] in HBM.
+
+`--gpus N` (torchrun, one rank per GPU): config 2 has ~0.4 MB of rows and does
+not shard usefully, so ranks run independent replicas (weak scaling, no
+data-path collective, SURVEY.md §8e "replicas only"); value = all ranks'
+placements / max-over-ranks time. The sharded path of config 4 (1M nodes,
+node dimension split over the ranks, per-leaf tallies SUM-all-reduced by RCCL)
+is reported beside it under "cfg4_1M".
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+
+
+def tally_bytes(p) -> int:
+    """Algorithmic bytes of one tally launch: every node row read once
+    (labels 8W + taints 4 + free 4R + excl 4 B), leaf offsets and block table
+    read, per-(class, leaf) capacities and per-leaf occupancy written once."""
+    n = p.nodes
+    row = 8 * n.n_label_words + 4 + 4 * n.n_res + 4
+    L = n.n_leaves
+    return n.n_nodes * row + 4 * (L + 1) + 4 * len(p.classes) * L + 4 * L
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--no-cfg4", action="store_true", help="skip the 1M-node sharded leg")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from jobset_amd import synth
+    from jobset_amd.distributed import ShardedPlacement, barrier, max_over_ranks
+    from jobset_amd.engine import Engine
+
+    stream = torch.cuda.current_stream().cuda_stream
+    eng = Engine(local)
+
+    # ------------------------------------------------ config 2 (value)
+    p = synth.config2()
+    eng.load(p)
+    J = p.n_jobs
+    jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+    out = torch.empty(J, dtype=torch.int32, device="cuda")
+
+    def step():
+        eng.place_device(jc.data_ptr(), J, out.data_ptr(), stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    placed = int((out.cpu().numpy() >= 0).sum())
+    total_placements = placed * args.steps * world
+    value = total_placements / elapsed
+
+    # kernel durations by HIP events on the launch stream (same steps again)
+    eng.set_timing(True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    tm = eng.timing(reset=True)
+    eng.set_timing(False)
+    tally_us = tm.tally_ms * 1e3 / max(tm.calls, 1)
+    feas_us = tm.feas_ms * 1e3 / max(tm.calls, 1)
+    assign_us = tm.assign_ms * 1e3 / max(tm.calls, 1)
+    tb = tally_bytes(p)
+    achieved = tb / (tally_us * 1e-6) / 1e9
+
+    # ------------------------------------------------ p99 recovery latency (host API, trial snapshots)
+    lat = []
+    if rank == 0 and args.trials > 0:
+        for t in range(args.trials):
+            pt = synth.config2(trial=t)
+            eng.upload_snapshot(pt.nodes)           # post-delete snapshot ready (untimed)
+            r = eng.place(pt.job_class)             # restart triggered -> assign[] returned
+            lat.append(r.wall_us)
+        eng.upload_snapshot(p.nodes)
+    lat_sorted = sorted(lat)
+
+    def pct(q):
+        return lat_sorted[min(len(lat_sorted) - 1, int(q * len(lat_sorted)))] if lat_sorted else None
+
+    # ------------------------------------------------ CPU baseline (rank 0, N=1 only)
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        from oracle import oracle as O
+        pk = O.PackedProblem(p)
+        O.place_c(p, pk)
+        n, t0c = 0, time.perf_counter()
+        while time.perf_counter() - t0c < args.cpu_seconds:
+            a, _, _ = O.place_c(p, pk)
+            n += 1
+        dt = time.perf_counter() - t0c
+        cpu = {"value": round(int((a >= 0).sum()) * n / dt, 1), "unit": "placements/s", "cores": 1,
+               "kind": "port",
+               "sample": f"config 2 placed {n} times in {dt:.1f} s by oracle/cpu_ref.c (1 thread, -O2), "
+                         f"same snapshot and rules"}
+
+    # ------------------------------------------------ config 4: 1M nodes, sharded over the ranks
+    cfg4 = None
+    if not args.no_cfg4:
+        p4 = synth.config4()
+        sp = ShardedPlacement(Engine(local) if world > 1 else eng, p4, rank, world, stream)
+        for _ in range(max(2, args.warmup // 4)):
+            sp.step()
+        torch.cuda.synchronize()
+        barrier(world)
+        steps4 = max(10, args.steps // 4)
+        t0 = time.perf_counter()
+        for _ in range(steps4):
+            sp.step()
+        torch.cuda.synchronize()
+        barrier(world)
+        el4 = max_over_ranks(time.perf_counter() - t0, world)
+        placed4 = sp.placed()
+        sp.engine.set_timing(True)
+        for _ in range(steps4):
+            sp.step()
+        torch.cuda.synchronize()
+        t4 = sp.engine.timing(reset=True)
+        sp.engine.set_timing(False)
+        t4_us = t4.tally_ms * 1e3 / max(t4.calls, 1)
+        tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
+        cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
+                "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
+                "placed": placed4, "tally_us": round(t4_us, 2),
+                "tally_gbs": round(tb4 / (t4_us * 1e-6) / 1e9, 1),
+                "tally_frac": round(tb4 / (t4_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "feas_us": round(t4.feas_ms * 1e3 / max(t4.calls, 1), 2),
+                "assign_us": round(t4.assign_ms * 1e3 / max(t4.calls, 1), 2),
+                "allreduce_us": sp.allreduce_us(), "shards": world}
+
+    if rank == 0:
+        line = {
+            "metric": "exclusive-topology placements/sec at 15k nodes; p99 recovery placement latency",
+            "value": round(value, 1),
+            "unit": "placements/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic",
+            "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery",
+                       "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J,
+                       "pods_per_job": p.classes[0].pods, "classes": len(p.classes),
+                       "parallelism": f"replicas{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                         "kernel": "tally_kernel", "bytes_per_launch": tb, "avg_us": round(tally_us, 3)},
+            "kernels_us": {"tally": round(tally_us, 3), "feas": round(feas_us, 3), "assign": round(assign_us, 3)},
+            "p50_recovery_us": round(pct(0.50), 1) if lat else None,
+            "p99_recovery_us": round(pct(0.99), 1) if lat else None,
+            "recovery_trials": len(lat),
+            "cpu_baseline": cpu,
+            "cfg4_1M": cfg4,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,183 @@
+/*
+ * jsplace.h — C ABI of the MI355X exclusive-topology placement engine.
+ *
+ * This is the drop-in boundary for JobSet's exclusive-placement path
+ * (SURVEY.md §8b). Every entry point takes plain pointers and sizes; no Go,
+ * torch or HIP types cross it (device pointers and streams are passed as
+ * void* / uintptr-sized handles). Return value: 0 on success, a negative
+ * JSP_E* code on failure; the message is available from jsp_last_error()
+ * (thread-local). Nothing aborts or throws across the ABI.
+ *
+ * Which reference interface each entry point replaces (file:line under the
+ * reference tree, danielvegamyhre/jobset @ 2024-10-08):
+ *
+ *  jsp_engine_create / jsp_engine_destroy
+ *      Constructed beside NewPodReconciler / NewPodWebhook in main.go:168,186
+ *      and injected into them (there is no engine in the reference: the domain
+ *      is chosen by kube-scheduler).
+ *  jsp_topology_upload / jsp_snapshot_upload / jsp_snapshot_patch
+ *      Replace the per-pod cached Node Get of topologyFromPod
+ *      (pkg/webhooks/pod_mutating_webhook.go:173-194) and leaderPodTopology
+ *      (pkg/controllers/pod_controller.go:242-263) with one resident snapshot
+ *      of the node informer cache (RBAC nodes get/list/watch,
+ *      config/components/rbac/role.yaml:16-23).
+ *  jsp_place / jsp_place_device (= jsp_tally_device + jsp_assign_device)
+ *      The placement decision that the leader's exclusive affinity terms
+ *      (setExclusiveAffinities, pod_mutating_webhook.go:95-135) delegate to
+ *      kube-scheduler, evaluated for every child Job of a JobSet at first
+ *      admission and at full recreate (failurePolicyRecreateAll,
+ *      pkg/controllers/failure_policy.go:155-175 -> reconcile,
+ *      pkg/controllers/jobset_controller.go:172-176, 523-551).
+ *      Job order = globalJobIndex (jobset_controller.go:1056-1065).
+ *  jsp_resolve_leader_domains
+ *      Batched form of setNodeSelector/topologyFromPod
+ *      (pod_mutating_webhook.go:137-194): leader node row -> domain id at the
+ *      job's topology level (the follower nodeSelector value).
+ *  jsp_audit_placements
+ *      Batched form of validatePodPlacements / leaderPodTopology /
+ *      followerPodTopology (pod_controller.go:172-277).
+ *
+ * Threading: one engine is not re-entrant; calls on one engine are
+ * serialised by an internal mutex (the Go wrapper also holds one).
+ */
+#ifndef JSPLACE_H
+#define JSPLACE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define JSP_ABI_VERSION 1
+
+#define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
+#define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
+#define JSP_MAX_RES 4         /* cpu-milli, memory-MiB, gpu, pods (any 4 the host chooses) */
+#define JSP_MAX_CLASSES 64
+
+/* error codes */
+#define JSP_OK 0
+#define JSP_EINVAL -1   /* bad argument / malformed snapshot */
+#define JSP_EHIP -2     /* HIP runtime error (includes: no GPU) */
+#define JSP_ENOMEM -3   /* device or host allocation failed */
+#define JSP_ESTATE -4   /* call order: no topology / snapshot / classes yet */
+#define JSP_ERANGE -5   /* problem exceeds an engine limit (message says which) */
+
+typedef struct jsp_engine jsp_engine;
+
+/* Global domain hierarchy; identical on every shard. Level K-1 domains are the
+ * "leaves". Domain ids at each level are dense 0..D_k-1 and ordered so that
+ * each domain covers a contiguous leaf range [first_leaf[k][d], first_leaf[k][d+1]).
+ * Nesting is required: every level-k boundary is also a level-(k+1) boundary. */
+typedef struct jsp_topology {
+    uint32_t n_levels;                           /* K, 1..JSP_MAX_LEVELS */
+    uint32_t n_domains[JSP_MAX_LEVELS];          /* D_k */
+    const uint32_t* first_leaf[JSP_MAX_LEVELS];  /* [D_k+1]; entry K-1 ignored (identity) */
+} jsp_topology;
+
+/* Node rows held by this engine (one shard), sorted by leaf domain.
+ * Column layout is SoA so every column streams coalesced from HBM. */
+typedef struct jsp_nodes {
+    uint32_t n_nodes;          /* N rows */
+    uint32_t leaf_begin;       /* global id of the first leaf held here */
+    uint32_t n_leaves;         /* leaves held here: [leaf_begin, leaf_begin+n_leaves) */
+    const uint32_t* leaf_start;/* [n_leaves+1] row offsets (0 .. N) */
+    uint32_t n_label_words;    /* W, 1..JSP_MAX_LABEL_WORDS */
+    const uint64_t* labels;    /* [W][N] interned (key,value) label bits */
+    const uint32_t* taints;    /* [N] interned NoSchedule/NoExecute taint bits */
+    uint32_t n_res;            /* R, 1..JSP_MAX_RES */
+    const uint32_t* free_res;  /* [R][N] allocatable minus requested */
+    const int32_t* excl_owner; /* [N] id of the exclusive job whose domain covers the
+                                  row (existing placements), -1 = none */
+} jsp_nodes;
+
+/* One requirement class: jobs are deduplicated into classes on the host. */
+typedef struct jsp_job_class {
+    uint64_t req_labels[JSP_MAX_LABEL_WORDS];    /* bits that must be set (nodeSelector) */
+    uint64_t forbid_labels[JSP_MAX_LABEL_WORDS]; /* bits that must be clear (NotIn/DoesNotExist) */
+    uint32_t tolerated_taints;                   /* taint bits this class tolerates */
+    uint32_t level;                              /* topology level of its exclusive-topology key */
+    uint32_t pods;                               /* pods per job (parallelism), >= 1 */
+    uint32_t req_res[JSP_MAX_RES];               /* per-pod request per resource, 0 = none */
+} jsp_job_class;
+
+typedef struct jsp_stats {
+    uint32_t jobs;             /* J */
+    uint32_t placed;           /* assign[j] != -1 */
+    uint32_t runs;             /* same-class job runs the assignment walked */
+    uint32_t reserved;
+    double wall_us;            /* host wall time of the call */
+} jsp_stats;
+
+typedef struct jsp_timing {
+    uint64_t calls;            /* timed jsp_*_device calls since last reset */
+    double tally_ms;           /* summed HIP-event time of the tally kernel */
+    double feas_ms;            /* summed HIP-event time of the feasibility-bitmap kernel */
+    double assign_ms;          /* summed HIP-event time of the assignment kernel */
+} jsp_timing;
+
+/* ---- lifecycle ---- */
+int jsp_abi_version(void);
+const char* jsp_last_error(void);
+int jsp_device_count(int* out);
+int jsp_engine_create(int device_id, jsp_engine** out);
+void jsp_engine_destroy(jsp_engine* e);
+
+/* ---- snapshot ---- */
+int jsp_topology_upload(jsp_engine* e, const jsp_topology* topo);
+int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nodes);
+/* Overwrite n rows (ids in `rows`, local to this shard) of the resident
+ * snapshot. delta columns are [W][n], [n], [R][n], [n]; structure (leaf
+ * ranges) is unchanged. */
+int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n,
+                       const uint64_t* labels, const uint32_t* taints,
+                       const uint32_t* free_res, const int32_t* excl_owner);
+int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t n_classes);
+
+/* ---- placement (host buffers; includes H2D of job_class and D2H of results) ----
+ * assign_out [J]: domain id at the job's class level, -1 = unplaceable.
+ * tally_out (nullable) [C][n_leaves_total]: per-(class, leaf) pod capacity.
+ * occ_out (nullable) [n_leaves_total]: rows covered by other exclusive jobs. */
+int jsp_place(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
+              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out,
+              jsp_stats* stats);
+
+/* ---- placement (device-resident buffers; stream = hipStream_t or NULL) ----
+ * d_cap [C][ld] and d_occ [ld] with ld >= total leaves; a shard writes only
+ * columns [leaf_begin, leaf_begin+n_leaves) so the caller can SUM-all-reduce
+ * zero-initialised buffers across shards before jsp_assign_device. */
+int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld,
+                     void* stream);
+int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ,
+                      uint32_t ld, const uint32_t* d_job_class, uint32_t n_jobs,
+                      int32_t* d_assign, void* stream);
+int jsp_place_device(jsp_engine* e, const uint32_t* d_job_class, uint32_t n_jobs,
+                     int32_t* d_assign, void* stream);
+
+/* ---- follower pinning and audit (batched webhook / PodReconciler work) ----
+ * jsp_resolve_leader_domains: for each job, the domain (at `levels[i]`) of
+ * the node row its leader is bound to; -1 when the row is -1 (leader not
+ * bound / node unknown). Host buffers.
+ * jsp_audit_placements: for each job i, followers [follower_off[i],
+ * follower_off[i+1]) carry the interned domain id their nodeSelector names
+ * (-1 = selector missing); bad_out[i] = number of followers whose domain
+ * differs from the domain of leader_rows[i] at levels[i], or 0xFFFFFFFF when
+ * the leader row is -1 (leader node unknown). */
+int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows,
+                               const uint32_t* levels, uint32_t n, int32_t* domain_out);
+int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels,
+                         const uint32_t* follower_off, const int32_t* follower_domains,
+                         uint32_t n_jobs, uint32_t* bad_out);
+
+/* ---- instrumentation ---- */
+int jsp_engine_set_timing(jsp_engine* e, int enable);
+int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
+void* jsp_engine_stream(jsp_engine* e);
+int jsp_engine_sync(jsp_engine* e);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* JSPLACE_H */

@@ -1,0 +1,636 @@
+// jsp_engine.cc — host side of the exclusive-topology placement engine:
+// the C ABI of include/jsplace.h over HIP device buffers and the kernels of
+// jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/jsplace.h"
+#include "jsp_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return set_err(JSP_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),  \
+                           __FILE__, __LINE__);                                              \
+    } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t reserve(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipMalloc(&p, n ? n : 16);
+        if (e == hipSuccess) bytes = n ? n : 16;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct EvPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int tag = 0;  // 0 tally, 1 feas, 2 assign
+};
+
+}  // namespace
+
+struct jsp_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+
+    // topology
+    bool have_topo = false;
+    uint32_t K = 0;
+    uint32_t D[JSP_MAX_LEVELS] = {0, 0, 0, 0};
+    uint32_t L_total = 0;
+    DevBuf fl[JSP_MAX_LEVELS], cs[JSP_MAX_LEVELS], par[JSP_MAX_LEVELS];
+    uint32_t t_off_h[JSP_MAX_LEVELS + 1] = {0, 0, 0, 0, 0};
+    DevBuf t_off;
+    jsp::TopoDev topo{};
+
+    // snapshot
+    bool have_snap = false;
+    uint32_t N = 0, npad = 0, W = 0, R = 0, leaf_begin = 0, n_leaves = 0, max_leaf_rows = 0;
+    DevBuf labels, taints, freer, excl, leaf_start, blk_leaf;
+    uint32_t n_blocks = 0;
+
+    // classes
+    bool have_cls = false;
+    uint32_t C = 0;
+    std::vector<jsp::DevClass> cls_h;
+    DevBuf cls, word_off, feas;
+    uint32_t feas_words = 0;
+
+    // scratch
+    DevBuf cap, occ, jobs, assign, stats, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+
+    // timing
+    bool timing = false;
+    std::vector<EvPair> ev;
+    size_t ev_used = 0;
+    jsp_timing acc{};
+
+    ~jsp_engine() {
+        (void)hipSetDevice(device);
+        for (auto& p : ev) {
+            if (p.a) (void)hipEventDestroy(p.a);
+            if (p.b) (void)hipEventDestroy(p.b);
+        }
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+constexpr uint32_t kTargetBlockRows = jsp::kChunkRows - 4;  // one chunk even when unaligned
+constexpr size_t kMaxEvents = 3 * 4096;
+
+int resolve_timing(jsp_engine* e) {
+    if (e->ev_used == 0) return JSP_OK;
+    HIP_TRY(hipEventSynchronize(e->ev[e->ev_used - 1].b));
+    for (size_t i = 0; i < e->ev_used; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e->ev[i].a, e->ev[i].b));
+        if (e->ev[i].tag == 0) e->acc.tally_ms += ms;
+        else if (e->ev[i].tag == 1) e->acc.feas_ms += ms;
+        else e->acc.assign_ms += ms;
+    }
+    e->ev_used = 0;
+    return JSP_OK;
+}
+
+// Returns the pair to bracket a launch with (nullptr when timing is off).
+EvPair* ev_begin(jsp_engine* e, int tag, hipStream_t s) {
+    if (!e->timing) return nullptr;
+    if (e->ev_used == kMaxEvents && resolve_timing(e) != JSP_OK) return nullptr;
+    if (e->ev_used == e->ev.size()) {
+        EvPair p;
+        if (hipEventCreate(&p.a) != hipSuccess || hipEventCreate(&p.b) != hipSuccess) return nullptr;
+        e->ev.push_back(p);
+    }
+    EvPair* p = &e->ev[e->ev_used++];
+    p->tag = tag;
+    if (tag == 0) e->acc.calls += 1;
+    (void)hipEventRecord(p->a, s);
+    return p;
+}
+
+void ev_end(EvPair* p, hipStream_t s) {
+    if (p) (void)hipEventRecord(p->b, s);
+}
+
+hipStream_t pick(jsp_engine* e, void* s) { return s ? static_cast<hipStream_t>(s) : e->stream; }
+
+int check_engine(jsp_engine* e) {
+    if (!e) return set_err(JSP_EINVAL, "engine is NULL");
+    if (hipSetDevice(e->device) != hipSuccess) return set_err(JSP_EHIP, "hipSetDevice(%d) failed", e->device);
+    return JSP_OK;
+}
+
+template <class T>
+hipError_t upload(DevBuf& b, const T* src, size_t n, hipStream_t s) {
+    hipError_t err = b.reserve(n * sizeof(T));
+    if (err != hipSuccess || n == 0) return err;
+    return hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s) {
+    jsp::TallyArgs a{};
+    a.labels = e->labels.as<uint64_t>();
+    a.taints = e->taints.as<uint32_t>();
+    a.freer = e->freer.as<uint32_t>();
+    a.excl = e->excl.as<int32_t>();
+    a.npad = e->npad;
+    a.leaf_start = e->leaf_start.as<uint32_t>();
+    a.blk_leaf = e->blk_leaf.as<uint32_t>();
+    a.n_blocks = e->n_blocks;
+    a.cls = e->cls.as<jsp::DevClass>();
+    a.cap_out = d_cap;
+    a.occ_out = d_occ;
+    a.ld = ld;
+    a.leaf_base = e->leaf_begin;
+    a.W = (int)e->W;
+    a.R = (int)e->R;
+    if (e->n_blocks == 0) return JSP_OK;
+    EvPair* p = ev_begin(e, 0, s);
+    uint32_t c0 = 0;
+    do {
+        a.c0 = c0;
+        a.nc = std::min<uint32_t>(e->C - c0, jsp::kTallyClasses);
+        a.do_occ = (c0 == 0);
+        HIP_TRY(jsp::launch_tally(a, s));
+        c0 += a.nc;
+    } while (c0 < e->C);
+    ev_end(p, s);
+    return JSP_OK;
+}
+
+int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
+                const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, hipStream_t s) {
+    EvPair* p = ev_begin(e, 1, s);
+    HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
+                             e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
+    ev_end(p, s);
+    p = ev_begin(e, 2, s);
+    HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
+                               e->C, e->topo, e->t_off.as<uint32_t>(), e->t_off_h[e->K], d_job_class, J, d_assign,
+                               e->stats.as<uint32_t>(), s));
+    ev_end(p, s);
+    return JSP_OK;
+}
+
+int ready(jsp_engine* e, bool need_cls) {
+    if (!e->have_topo) return set_err(JSP_ESTATE, "no topology uploaded");
+    if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
+    if (need_cls && !e->have_cls) return set_err(JSP_ESTATE, "no job classes uploaded");
+    return JSP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int jsp_abi_version(void) { return JSP_ABI_VERSION; }
+
+const char* jsp_last_error(void) { return g_err.c_str(); }
+
+int jsp_device_count(int* out) {
+    if (!out) return set_err(JSP_EINVAL, "out is NULL");
+    int n = 0;
+    hipError_t err = hipGetDeviceCount(&n);
+    if (err != hipSuccess) {
+        *out = 0;
+        return set_err(JSP_EHIP, "hipGetDeviceCount: %s", hipGetErrorString(err));
+    }
+    *out = n;
+    return JSP_OK;
+}
+
+int jsp_engine_create(int device_id, jsp_engine** out) {
+    if (!out) return set_err(JSP_EINVAL, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    hipError_t err = hipGetDeviceCount(&n);
+    if (err != hipSuccess || n == 0)
+        return set_err(JSP_EHIP, "no HIP device available (%s)", hipGetErrorString(err));
+    if (device_id < 0 || device_id >= n) return set_err(JSP_EINVAL, "device %d out of range [0,%d)", device_id, n);
+    HIP_TRY(hipSetDevice(device_id));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device_id));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return set_err(JSP_EHIP, "device %d is %s; this engine is built for gfx950 (MI355X) only", device_id,
+                       prop.gcnArchName);
+    auto* e = new (std::nothrow) jsp_engine();
+    if (!e) return set_err(JSP_ENOMEM, "engine allocation failed");
+    e->device = device_id;
+    err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
+    if (err != hipSuccess) {
+        delete e;
+        return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
+    }
+    if (e->stats.reserve(16) != hipSuccess) {
+        delete e;
+        return set_err(JSP_ENOMEM, "stats buffer");
+    }
+    *out = e;
+    return JSP_OK;
+}
+
+void jsp_engine_destroy(jsp_engine* e) {
+    if (!e) return;
+    {
+        std::lock_guard<std::mutex> g(e->mu);
+        (void)hipSetDevice(e->device);
+        if (e->stream) (void)hipStreamSynchronize(e->stream);
+    }
+    delete e;
+}
+
+int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!t) return set_err(JSP_EINVAL, "topology is NULL");
+    const uint32_t K = t->n_levels;
+    if (K < 1 || K > JSP_MAX_LEVELS) return set_err(JSP_EINVAL, "n_levels %u out of range [1,%d]", K, JSP_MAX_LEVELS);
+    const uint32_t L = t->n_domains[K - 1];
+    std::vector<std::vector<uint32_t>> fl(K);
+    for (uint32_t k = 0; k < K; ++k) {
+        const uint32_t D = t->n_domains[k];
+        fl[k].resize(D + 1);
+        if (k + 1 == K || t->first_leaf[k] == nullptr) {
+            if (k + 1 != K) return set_err(JSP_EINVAL, "first_leaf[%u] is NULL", k);
+            for (uint32_t d = 0; d <= D; ++d) fl[k][d] = d;
+        } else {
+            std::memcpy(fl[k].data(), t->first_leaf[k], sizeof(uint32_t) * (D + 1));
+        }
+        if (fl[k][0] != 0 || fl[k][D] != L) return set_err(JSP_EINVAL, "first_leaf[%u] must run 0..%u", k, L);
+        for (uint32_t d = 0; d < D; ++d)
+            if (fl[k][d] > fl[k][d + 1]) return set_err(JSP_EINVAL, "first_leaf[%u] not monotone at %u", k, d);
+    }
+    for (uint32_t k = 0; k + 1 < K; ++k)
+        for (uint32_t d = 0; d <= t->n_domains[k]; ++d)
+            if (!std::binary_search(fl[k + 1].begin(), fl[k + 1].end(), fl[k][d]))
+                return set_err(JSP_EINVAL, "level %u is not nested in level %u (boundary %u)", k, k + 1, fl[k][d]);
+    // taken-bitmap layout in LDS
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+        e->t_off_h[k] = off;
+        off += (t->n_domains[k] + 63) / 64;
+    }
+    e->t_off_h[K] = off;
+    if (off > jsp::kMaxTakenWords)
+        return set_err(JSP_ERANGE, "topology has %u bitmap words over all levels; engine limit is %u (%u domains)",
+                       off, jsp::kMaxTakenWords, jsp::kMaxTakenWords * 64);
+    hipStream_t s = e->stream;
+    jsp::TopoDev td{};
+    td.K = K;
+    for (uint32_t k = 0; k < K; ++k) {
+        td.D[k] = t->n_domains[k];
+        HIP_TRY(upload(e->fl[k], fl[k].data(), fl[k].size(), s));
+        td.fl[k] = e->fl[k].as<uint32_t>();
+        if (k + 1 < K) {  // child_start: level-(k+1) range of each level-k domain
+            std::vector<uint32_t> cs(t->n_domains[k] + 1);
+            for (uint32_t d = 0; d <= t->n_domains[k]; ++d)
+                cs[d] = (uint32_t)(std::lower_bound(fl[k + 1].begin(), fl[k + 1].end(), fl[k][d]) - fl[k + 1].begin());
+            HIP_TRY(upload(e->cs[k], cs.data(), cs.size(), s));
+            td.cs[k] = e->cs[k].as<uint32_t>();
+        }
+        if (k > 0) {  // parent at level k-1 of each level-k domain (by its first leaf)
+            std::vector<int32_t> par(std::max<uint32_t>(t->n_domains[k], 1));
+            for (uint32_t d = 0; d < t->n_domains[k]; ++d)
+                par[d] = (int32_t)(std::upper_bound(fl[k - 1].begin(), fl[k - 1].end(), fl[k][d]) - fl[k - 1].begin()) - 1;
+            HIP_TRY(upload(e->par[k], par.data(), par.size(), s));
+            td.par[k] = e->par[k].as<int32_t>();
+        }
+    }
+    HIP_TRY(upload(e->t_off, e->t_off_h, K + 1, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->topo = td;
+    e->K = K;
+    for (uint32_t k = 0; k < JSP_MAX_LEVELS; ++k) e->D[k] = k < K ? t->n_domains[k] : 0;
+    e->L_total = L;
+    e->have_topo = true;
+    e->have_snap = false;  // a snapshot is tied to its topology
+    e->have_cls = false;
+    return JSP_OK;
+}
+
+int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
+    if (!nd || !nd->leaf_start) return set_err(JSP_EINVAL, "nodes / leaf_start is NULL");
+    const uint32_t N = nd->n_nodes, W = nd->n_label_words, R = nd->n_res, NL = nd->n_leaves;
+    if (W < 1 || W > JSP_MAX_LABEL_WORDS) return set_err(JSP_EINVAL, "n_label_words %u out of range", W);
+    if (R < 1 || R > JSP_MAX_RES) return set_err(JSP_EINVAL, "n_res %u out of range", R);
+    if ((uint64_t)nd->leaf_begin + NL > e->L_total)
+        return set_err(JSP_EINVAL, "leaves [%u,%u) exceed topology (%u leaves)", nd->leaf_begin,
+                       nd->leaf_begin + NL, e->L_total);
+    if (N > 0 && (!nd->labels || !nd->taints || !nd->free_res || !nd->excl_owner))
+        return set_err(JSP_EINVAL, "a node column is NULL");
+    if (N > (1u << 30)) return set_err(JSP_ERANGE, "%u rows exceed the 2^30 row limit", N);
+    const uint32_t* ls = nd->leaf_start;
+    if (ls[0] != 0 || ls[NL] != N) return set_err(JSP_EINVAL, "leaf_start must run 0..%u", N);
+    uint32_t max_rows = 0;
+    for (uint32_t l = 0; l < NL; ++l) {
+        if (ls[l] > ls[l + 1]) return set_err(JSP_EINVAL, "leaf_start not monotone at %u", l);
+        max_rows = std::max(max_rows, ls[l + 1] - ls[l]);
+    }
+    // workgroup partition: whole leaves, ~one 1024-row chunk and <= 256 leaves each
+    std::vector<uint32_t> blk{0};
+    {
+        uint32_t rows = 0, leaves = 0;
+        for (uint32_t l = 0; l < NL; ++l) {
+            const uint32_t r = ls[l + 1] - ls[l];
+            if (leaves > 0 && (rows + r > kTargetBlockRows || leaves == (uint32_t)jsp::kMaxBlkLeaves)) {
+                blk.push_back(l);
+                rows = 0;
+                leaves = 0;
+            }
+            rows += r;
+            ++leaves;
+        }
+        if (NL > 0) blk.push_back(NL);
+    }
+    const uint32_t npad = ((N + 63) / 64) * 64 + 64;
+    hipStream_t s = e->stream;
+    HIP_TRY(e->labels.reserve((size_t)W * npad * 8));
+    HIP_TRY(e->taints.reserve((size_t)npad * 4));
+    HIP_TRY(e->freer.reserve((size_t)R * npad * 4));
+    HIP_TRY(e->excl.reserve((size_t)npad * 4));
+    HIP_TRY(hipMemsetAsync(e->labels.p, 0, (size_t)W * npad * 8, s));
+    HIP_TRY(hipMemsetAsync(e->taints.p, 0, (size_t)npad * 4, s));
+    HIP_TRY(hipMemsetAsync(e->freer.p, 0, (size_t)R * npad * 4, s));
+    HIP_TRY(hipMemsetAsync(e->excl.p, 0xFF, (size_t)npad * 4, s));
+    if (N > 0) {
+        for (uint32_t w = 0; w < W; ++w)
+            HIP_TRY(hipMemcpyAsync(e->labels.as<uint64_t>() + (size_t)w * npad, nd->labels + (size_t)w * N,
+                                   (size_t)N * 8, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->taints.p, nd->taints, (size_t)N * 4, hipMemcpyHostToDevice, s));
+        for (uint32_t r = 0; r < R; ++r)
+            HIP_TRY(hipMemcpyAsync(e->freer.as<uint32_t>() + (size_t)r * npad, nd->free_res + (size_t)r * N,
+                                   (size_t)N * 4, hipMemcpyHostToDevice, s));
+        HIP_TRY(hipMemcpyAsync(e->excl.p, nd->excl_owner, (size_t)N * 4, hipMemcpyHostToDevice, s));
+    }
+    HIP_TRY(upload(e->leaf_start, ls, (size_t)NL + 1, s));
+    HIP_TRY(upload(e->blk_leaf, blk.data(), blk.size(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->N = N;
+    e->npad = npad;
+    e->W = W;
+    e->R = R;
+    e->leaf_begin = nd->leaf_begin;
+    e->n_leaves = NL;
+    e->max_leaf_rows = max_rows;
+    e->n_blocks = (uint32_t)blk.size() - 1;
+    e->have_snap = true;
+    if (e->have_cls) {
+        for (auto& c : e->cls_h)
+            if ((uint64_t)c.pods * max_rows >= (1ull << 32)) {
+                e->have_cls = false;
+                return set_err(JSP_ERANGE, "pods x rows per leaf overflows 32-bit tallies; re-upload classes");
+            }
+    }
+    return JSP_OK;
+}
+
+int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
+                       const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
+    if (n == 0) return JSP_OK;
+    if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
+    for (uint32_t i = 0; i < n; ++i)
+        if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
+    hipStream_t s = e->stream;
+    HIP_TRY(upload(e->tmp_a, rows, n, s));
+    if (labels) HIP_TRY(upload(e->tmp_b, labels, (size_t)e->W * n, s));
+    if (taints) HIP_TRY(upload(e->tmp_c, taints, n, s));
+    if (free_res) HIP_TRY(upload(e->tmp_d, free_res, (size_t)e->R * n, s));
+    if (excl_owner) HIP_TRY(upload(e->tmp_e, excl_owner, n, s));
+    HIP_TRY(jsp::launch_patch(e->tmp_a.as<uint32_t>(), n, e->npad, e->W, e->R,
+                              labels ? e->tmp_b.as<uint64_t>() : nullptr, taints ? e->tmp_c.as<uint32_t>() : nullptr,
+                              free_res ? e->tmp_d.as<uint32_t>() : nullptr,
+                              excl_owner ? e->tmp_e.as<int32_t>() : nullptr, e->labels.as<uint64_t>(),
+                              e->taints.as<uint32_t>(), e->freer.as<uint32_t>(), e->excl.as<int32_t>(), s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return JSP_OK;
+}
+
+int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
+    if (C > (uint32_t)jsp::kMaxClasses) return set_err(JSP_ERANGE, "%u classes exceed the limit of %d", C, jsp::kMaxClasses);
+    if (C > 0 && !classes) return set_err(JSP_EINVAL, "classes is NULL");
+    std::vector<jsp::DevClass> h(std::max<uint32_t>(C, 1));
+    std::vector<uint32_t> woff(C + 1, 0);
+    for (uint32_t c = 0; c < C; ++c) {
+        const jsp_job_class& x = classes[c];
+        if (x.level >= e->K) return set_err(JSP_EINVAL, "class %u: level %u >= n_levels %u", c, x.level, e->K);
+        if (x.pods < 1) return set_err(JSP_EINVAL, "class %u: pods must be >= 1", c);
+        if (x.pods > (1u << 22)) return set_err(JSP_ERANGE, "class %u: pods %u exceed 2^22", c, x.pods);
+        if (e->have_snap && (uint64_t)x.pods * e->max_leaf_rows >= (1ull << 32))
+            return set_err(JSP_ERANGE, "class %u: pods x rows per leaf overflows 32-bit tallies", c);
+        jsp::DevClass& d = h[c];
+        std::memset(&d, 0, sizeof d);
+        for (int w = 0; w < 4; ++w) {
+            d.req[w] = x.req_labels[w];
+            d.forbid[w] = x.forbid_labels[w];
+        }
+        d.tol = x.tolerated_taints;
+        d.level = x.level;
+        d.pods = x.pods;
+        for (int r = 0; r < 4; ++r) {
+            d.res[r] = x.req_res[r];
+            d.rcp[r] = x.req_res[r] ? 1.0f / (float)x.req_res[r] : 0.f;
+        }
+        woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
+    }
+    hipStream_t s = e->stream;
+    HIP_TRY(upload(e->cls, h.data(), h.size(), s));
+    HIP_TRY(upload(e->word_off, woff.data(), woff.size(), s));
+    HIP_TRY(e->feas.reserve((size_t)std::max<uint32_t>(woff[C], 1) * 8));
+    HIP_TRY(e->cap.reserve((size_t)std::max<uint32_t>(C, 1) * std::max<uint32_t>(e->L_total, 1) * 4));
+    HIP_TRY(e->occ.reserve((size_t)std::max<uint32_t>(e->L_total, 1) * 4));
+    HIP_TRY(hipStreamSynchronize(s));
+    e->cls_h.assign(h.begin(), h.begin() + C);
+    e->C = C;
+    e->feas_words = woff[C];
+    e->have_cls = true;
+    return JSP_OK;
+}
+
+int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, void* stream) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
+    if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    return tally_impl(e, d_cap, d_occ, ld, pick(e, stream));
+}
+
+int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
+                      const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, void* stream) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    if (J > 0 && (!d_job_class || !d_assign)) return set_err(JSP_EINVAL, "job buffers are NULL");
+    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
+    return assign_impl(e, d_cap, d_occ, ld, d_job_class, J, d_assign, pick(e, stream));
+}
+
+int jsp_place_device(jsp_engine* e, const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, void* stream) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
+        return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
+    if (J > 0 && (!d_job_class || !d_assign)) return set_err(JSP_EINVAL, "job buffers are NULL");
+    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
+    hipStream_t s = pick(e, stream);
+    if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
+    return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_job_class, J, d_assign, s);
+}
+
+int jsp_place(jsp_engine* e, const uint32_t* job_class, uint32_t J, int32_t* assign_out, uint32_t* tally_out,
+              uint32_t* occ_out, jsp_stats* stats) {
+    if (int rc = check_engine(e)) return rc;
+    auto t0 = std::chrono::steady_clock::now();
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
+        return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
+    if (J > 0 && (!job_class || !assign_out)) return set_err(JSP_EINVAL, "job buffers are NULL");
+    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
+    for (uint32_t j = 0; j < J; ++j)
+        if (job_class[j] >= e->C) return set_err(JSP_EINVAL, "job %u: class %u out of range", j, job_class[j]);
+    hipStream_t s = e->stream;
+    HIP_TRY(upload(e->jobs, job_class, J, s));
+    HIP_TRY(e->assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
+    if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
+    if (int rc = assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, e->jobs.as<uint32_t>(), J,
+                             e->assign.as<int32_t>(), s))
+        return rc;
+    uint32_t st[2] = {0, 0};
+    if (J > 0) HIP_TRY(hipMemcpyAsync(assign_out, e->assign.p, (size_t)J * 4, hipMemcpyDeviceToHost, s));
+    if (tally_out && e->C > 0)
+        HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
+    if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
+    if (stats) HIP_TRY(hipMemcpyAsync(st, e->stats.p, sizeof st, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    if (stats) {
+        stats->jobs = J;
+        stats->runs = J > 0 ? st[0] : 0;
+        stats->placed = J > 0 ? st[1] : 0;
+        stats->reserved = 0;
+        stats->wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return JSP_OK;
+}
+
+int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels, uint32_t n,
+                               int32_t* domain_out) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, false)) return rc;
+    if (n == 0) return JSP_OK;
+    if (!leader_rows || !levels || !domain_out) return set_err(JSP_EINVAL, "NULL buffer");
+    hipStream_t s = e->stream;
+    HIP_TRY(upload(e->tmp_a, leader_rows, n, s));
+    HIP_TRY(upload(e->tmp_b, levels, n, s));
+    HIP_TRY(e->tmp_c.reserve((size_t)n * 4));
+    HIP_TRY(jsp::launch_resolve(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), n, e->N, e->leaf_start.as<uint32_t>(),
+                                e->n_leaves, e->leaf_begin, e->topo, e->tmp_c.as<int32_t>(), s));
+    HIP_TRY(hipMemcpyAsync(domain_out, e->tmp_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return JSP_OK;
+}
+
+int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels,
+                         const uint32_t* follower_off, const int32_t* follower_domains, uint32_t n_jobs,
+                         uint32_t* bad_out) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, false)) return rc;
+    if (n_jobs == 0) return JSP_OK;
+    if (!leader_rows || !levels || !follower_off || !bad_out) return set_err(JSP_EINVAL, "NULL buffer");
+    const uint32_t M = follower_off[n_jobs];
+    if (follower_off[0] != 0) return set_err(JSP_EINVAL, "follower_off[0] must be 0");
+    for (uint32_t i = 0; i < n_jobs; ++i)
+        if (follower_off[i] > follower_off[i + 1]) return set_err(JSP_EINVAL, "follower_off not monotone at %u", i);
+    if (M > 0 && !follower_domains) return set_err(JSP_EINVAL, "follower_domains is NULL");
+    hipStream_t s = e->stream;
+    HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s));
+    HIP_TRY(upload(e->tmp_b, levels, n_jobs, s));
+    HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s));
+    HIP_TRY(e->tmp_d.reserve((size_t)std::max<uint32_t>(M, 1) * 4));
+    if (M > 0) HIP_TRY(hipMemcpyAsync(e->tmp_d.p, follower_domains, (size_t)M * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(e->tmp_e.reserve((size_t)n_jobs * 4));
+    HIP_TRY(jsp::launch_audit(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), e->tmp_c.as<uint32_t>(),
+                              e->tmp_d.as<int32_t>(), n_jobs, e->N, e->leaf_start.as<uint32_t>(), e->n_leaves,
+                              e->leaf_begin, e->topo, e->tmp_e.as<uint32_t>(), s));
+    HIP_TRY(hipMemcpyAsync(bad_out, e->tmp_e.p, (size_t)n_jobs * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return JSP_OK;
+}
+
+int jsp_engine_set_timing(jsp_engine* e, int enable) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    e->timing = enable != 0;
+    return JSP_OK;
+}
+
+int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = resolve_timing(e)) return rc;
+    if (out) *out = e->acc;
+    if (reset) e->acc = jsp_timing{};
+    return JSP_OK;
+}
+
+void* jsp_engine_stream(jsp_engine* e) { return e ? static_cast<void*>(e->stream) : nullptr; }
+
+int jsp_engine_sync(jsp_engine* e) {
+    if (int rc = check_engine(e)) return rc;
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return JSP_OK;
+}
+
+}  // extern "C"

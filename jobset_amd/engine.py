@@ -1,0 +1,190 @@
+"""Python host mirror of the engine interface the Go `pkg/placement` package
+exposes: `Engine.place(problem) -> assign[]`.
+
+In the reference the domain for each child Job is chosen by kube-scheduler
+from the leader's exclusive affinity terms (pkg/webhooks/
+pod_mutating_webhook.go:95-135); this engine computes it deterministically for
+all Jobs of a JobSet at once, at first admission and at full recreate
+(pkg/controllers/failure_policy.go:155-175). Every call goes through the C ABI
+of include/jsplace.h into the gfx950 kernels; there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import native
+from .native import JspJobClass, JspNodes, JspStats, JspTiming, JspTopology, check
+from .snapshot import JobClass, Nodes, Problem, Topology
+
+
+def _p(a: Optional[np.ndarray]) -> Optional[int]:
+    return None if a is None else a.ctypes.data
+
+
+@dataclass
+class PlaceResult:
+    assign: np.ndarray           # int32 [J], domain id at the job's class level, -1 unplaceable
+    cap: Optional[np.ndarray]    # uint32 [C, L] per-(class, leaf) pod capacity
+    occ: Optional[np.ndarray]    # uint32 [L] rows covered by other exclusive jobs
+    placed: int
+    runs: int
+    wall_us: float
+
+
+class Engine:
+    """One engine per GPU (device id = local rank)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = native.lib()
+        h = ctypes.c_void_p()
+        check(self._lib.jsp_engine_create(device, ctypes.byref(h)))
+        self._h = h
+        self.device = device
+        self._keep: List[object] = []
+        self.topology: Optional[Topology] = None
+        self.nodes: Optional[Nodes] = None
+        self.n_classes = 0
+
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            self._lib.jsp_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---------------------------------------------------------------- snapshot
+    def upload_topology(self, topo: Topology) -> None:
+        t = JspTopology()
+        t.n_levels = topo.n_levels
+        keep = []
+        for k in range(topo.n_levels):
+            t.n_domains[k] = topo.n_domains[k]
+            fl = np.ascontiguousarray(topo.first_leaf[k], dtype=np.uint32)
+            keep.append(fl)
+            t.first_leaf[k] = fl.ctypes.data
+        check(self._lib.jsp_topology_upload(self._h, ctypes.byref(t)))
+        self.topology = topo
+        self.nodes = None
+        self.n_classes = 0
+
+    def upload_snapshot(self, nodes: Nodes) -> None:
+        cols = dict(
+            leaf_start=np.ascontiguousarray(nodes.leaf_start, dtype=np.uint32),
+            labels=np.ascontiguousarray(nodes.labels, dtype=np.uint64),
+            taints=np.ascontiguousarray(nodes.taints, dtype=np.uint32),
+            free=np.ascontiguousarray(nodes.free, dtype=np.uint32),
+            excl=np.ascontiguousarray(nodes.excl, dtype=np.int32),
+        )
+        n = JspNodes()
+        n.n_nodes = nodes.n_nodes
+        n.leaf_begin = nodes.leaf_begin
+        n.n_leaves = nodes.n_leaves
+        n.leaf_start = _p(cols["leaf_start"])
+        n.n_label_words = cols["labels"].shape[0]
+        n.labels = _p(cols["labels"])
+        n.taints = _p(cols["taints"])
+        n.n_res = cols["free"].shape[0]
+        n.free_res = _p(cols["free"])
+        n.excl_owner = _p(cols["excl"])
+        check(self._lib.jsp_snapshot_upload(self._h, ctypes.byref(n)))
+        self.nodes = nodes
+
+    def patch_rows(self, rows: np.ndarray, labels: Optional[np.ndarray] = None, taints: Optional[np.ndarray] = None,
+                   free: Optional[np.ndarray] = None, excl: Optional[np.ndarray] = None) -> None:
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=dt)
+                for a, dt in ((labels, np.uint64), (taints, np.uint32), (free, np.uint32), (excl, np.int32))]
+        check(self._lib.jsp_snapshot_patch(self._h, _p(rows), rows.shape[0], *[_p(a) for a in arrs]))
+
+    def upload_classes(self, classes: Sequence[JobClass]) -> None:
+        arr = (JspJobClass * max(len(classes), 1))()
+        for i, jc in enumerate(classes):
+            req, fb = jc.words(4)
+            for w in range(4):
+                arr[i].req_labels[w] = req[w] & ((1 << 64) - 1)
+                arr[i].forbid_labels[w] = fb[w] & ((1 << 64) - 1)
+            arr[i].tolerated_taints = jc.tolerated_taints & 0xFFFFFFFF
+            arr[i].level = jc.level
+            arr[i].pods = jc.pods
+            for r, v in enumerate(jc.res()):
+                arr[i].req_res[r] = v
+        check(self._lib.jsp_classes_upload(self._h, arr, len(classes)))
+        self.n_classes = len(classes)
+
+    def load(self, p: Problem, nodes: Optional[Nodes] = None) -> None:
+        self.upload_topology(p.topology)
+        self.upload_snapshot(nodes if nodes is not None else p.nodes)
+        self.upload_classes(p.classes)
+
+    # ---------------------------------------------------------------- placement
+    def place(self, job_class: np.ndarray, want_tally: bool = False) -> PlaceResult:
+        jc = np.ascontiguousarray(job_class, dtype=np.uint32)
+        J = jc.shape[0]
+        L = self.topology.n_leaves
+        assign = np.empty(max(J, 1), dtype=np.int32)
+        cap = np.empty((max(self.n_classes, 1), max(L, 1)), dtype=np.uint32) if want_tally else None
+        occ = np.empty(max(L, 1), dtype=np.uint32) if want_tally else None
+        st = JspStats()
+        check(self._lib.jsp_place(self._h, _p(jc), J, _p(assign), _p(cap), _p(occ), ctypes.byref(st)))
+        return PlaceResult(assign=assign[:J], cap=None if cap is None else cap[:self.n_classes, :L],
+                           occ=None if occ is None else occ[:L], placed=st.placed, runs=st.runs,
+                           wall_us=st.wall_us)
+
+    def place_device(self, d_job_class: int, n_jobs: int, d_assign: int, stream: Optional[int] = None) -> None:
+        check(self._lib.jsp_place_device(self._h, d_job_class, n_jobs, d_assign, stream))
+
+    def tally_device(self, d_cap: int, d_occ: int, ld: int, stream: Optional[int] = None) -> None:
+        check(self._lib.jsp_tally_device(self._h, d_cap, d_occ, ld, stream))
+
+    def assign_device(self, d_cap: int, d_occ: int, ld: int, d_job_class: int, n_jobs: int, d_assign: int,
+                      stream: Optional[int] = None) -> None:
+        check(self._lib.jsp_assign_device(self._h, d_cap, d_occ, ld, d_job_class, n_jobs, d_assign, stream))
+
+    # ---------------------------------------------------------------- webhook / reconciler batches
+    def resolve_leader_domains(self, leader_rows: np.ndarray, levels: np.ndarray) -> np.ndarray:
+        rows = np.ascontiguousarray(leader_rows, dtype=np.int32)
+        lv = np.ascontiguousarray(levels, dtype=np.uint32)
+        out = np.empty(max(rows.shape[0], 1), dtype=np.int32)
+        check(self._lib.jsp_resolve_leader_domains(self._h, _p(rows), _p(lv), rows.shape[0], _p(out)))
+        return out[:rows.shape[0]]
+
+    def audit_placements(self, leader_rows: np.ndarray, levels: np.ndarray, follower_off: np.ndarray,
+                         follower_domains: np.ndarray) -> np.ndarray:
+        rows = np.ascontiguousarray(leader_rows, dtype=np.int32)
+        lv = np.ascontiguousarray(levels, dtype=np.uint32)
+        off = np.ascontiguousarray(follower_off, dtype=np.uint32)
+        fd = np.ascontiguousarray(follower_domains, dtype=np.int32)
+        out = np.empty(max(rows.shape[0], 1), dtype=np.uint32)
+        check(self._lib.jsp_audit_placements(self._h, _p(rows), _p(lv), _p(off), _p(fd) if fd.size else None,
+                                             rows.shape[0], _p(out)))
+        return out[:rows.shape[0]]
+
+    # ---------------------------------------------------------------- instrumentation
+    def set_timing(self, enable: bool) -> None:
+        check(self._lib.jsp_engine_set_timing(self._h, 1 if enable else 0))
+
+    def timing(self, reset: bool = True) -> JspTiming:
+        t = JspTiming()
+        check(self._lib.jsp_engine_get_timing(self._h, ctypes.byref(t), 1 if reset else 0))
+        return t
+
+    @property
+    def stream(self) -> int:
+        return self._lib.jsp_engine_stream(self._h) or 0
+
+    def sync(self) -> None:
+        check(self._lib.jsp_engine_sync(self._h))

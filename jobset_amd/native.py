@@ -1,0 +1,113 @@
+"""ctypes binding of include/jsplace.h (the engine's C ABI).
+
+The shared library is built in-tree (`make` or __graft_entry__.build()) as
+jobset_amd/libjsplace.so. There is no fallback: if the library or a GPU is
+missing, engine construction raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libjsplace.so")
+
+JSP_OK, JSP_EINVAL, JSP_EHIP, JSP_ENOMEM, JSP_ESTATE, JSP_ERANGE = 0, -1, -2, -3, -4, -5
+ERROR_NAMES = {JSP_EINVAL: "JSP_EINVAL", JSP_EHIP: "JSP_EHIP", JSP_ENOMEM: "JSP_ENOMEM",
+               JSP_ESTATE: "JSP_ESTATE", JSP_ERANGE: "JSP_ERANGE"}
+
+MAX_LEVELS, MAX_LABEL_WORDS, MAX_RES = 4, 4, 4
+
+u32, i32, u64, vp = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64, ctypes.c_void_p
+
+
+class JspTopology(ctypes.Structure):
+    _fields_ = [("n_levels", u32), ("n_domains", u32 * MAX_LEVELS), ("first_leaf", vp * MAX_LEVELS)]
+
+
+class JspNodes(ctypes.Structure):
+    _fields_ = [("n_nodes", u32), ("leaf_begin", u32), ("n_leaves", u32), ("leaf_start", vp),
+                ("n_label_words", u32), ("labels", vp), ("taints", vp), ("n_res", u32),
+                ("free_res", vp), ("excl_owner", vp)]
+
+
+class JspJobClass(ctypes.Structure):
+    _fields_ = [("req_labels", u64 * MAX_LABEL_WORDS), ("forbid_labels", u64 * MAX_LABEL_WORDS),
+                ("tolerated_taints", u32), ("level", u32), ("pods", u32), ("req_res", u32 * MAX_RES)]
+
+
+class JspStats(ctypes.Structure):
+    _fields_ = [("jobs", u32), ("placed", u32), ("runs", u32), ("reserved", u32), ("wall_us", ctypes.c_double)]
+
+
+class JspTiming(ctypes.Structure):
+    _fields_ = [("calls", ctypes.c_uint64), ("tally_ms", ctypes.c_double), ("feas_ms", ctypes.c_double),
+                ("assign_ms", ctypes.c_double)]
+
+
+# (name, restype, argtypes) — every entry point declared in include/jsplace.h
+SIGNATURES = [
+    ("jsp_abi_version", ctypes.c_int, []),
+    ("jsp_last_error", ctypes.c_char_p, []),
+    ("jsp_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("jsp_engine_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+    ("jsp_engine_destroy", None, [vp]),
+    ("jsp_topology_upload", ctypes.c_int, [vp, ctypes.POINTER(JspTopology)]),
+    ("jsp_snapshot_upload", ctypes.c_int, [vp, ctypes.POINTER(JspNodes)]),
+    ("jsp_snapshot_patch", ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp]),
+    ("jsp_classes_upload", ctypes.c_int, [vp, ctypes.POINTER(JspJobClass), u32]),
+    ("jsp_place", ctypes.c_int, [vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
+    ("jsp_tally_device", ctypes.c_int, [vp, vp, vp, u32, vp]),
+    ("jsp_assign_device", ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp]),
+    ("jsp_place_device", ctypes.c_int, [vp, vp, u32, vp, vp]),
+    ("jsp_resolve_leader_domains", ctypes.c_int, [vp, vp, vp, u32, vp]),
+    ("jsp_audit_placements", ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp]),
+    ("jsp_engine_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
+    ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
+    ("jsp_engine_stream", vp, [vp]),
+    ("jsp_engine_sync", ctypes.c_int, [vp]),
+]
+
+_lib = None
+
+
+class JspError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"{ERROR_NAMES.get(code, code)}: {message}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Load libjsplace.so. Raises (no fallback) when it has not been built."""
+    global _lib
+    if _lib is None:
+        # One HIP runtime per process: when torch is installed its bundled
+        # libamdhip64 must be the one libjsplace.so binds to (same SONAME), or
+        # torch cannot initialise the GPU afterwards and the stream / device
+        # pointers handed across (bench.py, distributed.py) would belong to
+        # another runtime. Load it first.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} is missing: build it with `make` or __graft_entry__.build()")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def check(rc: int) -> None:
+    if rc != JSP_OK:
+        msg = lib().jsp_last_error()
+        raise JspError(rc, msg.decode() if msg else "")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().jsp_device_count(ctypes.byref(n))
+    return n.value if rc == JSP_OK else 0

@@ -1,0 +1,284 @@
+"""GPU parity tests: the HIP engine (through the C ABI) against the CPU oracle,
+bit-exact on assign[], the per-(class, leaf) tallies and the occupancy
+counts, on BASELINE.json configs 1-5 and on ragged random snapshots; plus the
+invariants of SURVEY.md §8c and the edge cases of the reference's own tests
+(empty inputs, unplaceable jobs, maximum sizes)."""
+import numpy as np
+import pytest
+
+from jobset_amd import synth
+from jobset_amd.engine import Engine
+from jobset_amd.native import JSP_EINVAL, JSP_ERANGE, JSP_ESTATE, JspError
+from jobset_amd.snapshot import JobClass, Nodes, Problem, Topology, shard_problem
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def run_both(engine: Engine, p: Problem):
+    engine.load(p)
+    got = engine.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    return got, a, cap, occ
+
+
+def assert_same(got, a, cap, occ):
+    np.testing.assert_array_equal(got.occ, occ)
+    np.testing.assert_array_equal(got.cap, cap)
+    np.testing.assert_array_equal(got.assign, a)
+    assert got.placed == int((a >= 0).sum())
+
+
+@pytest.mark.parametrize("cfg", [1, 2, 3, 5])
+def test_config_parity(engine, cfg):
+    p = synth.CONFIGS[cfg]()
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+    O.check_invariants(p, got.assign, got.cap, got.occ)
+
+
+def test_config4_1M_parity(engine):
+    p = synth.config4()
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+    # size-independent property: every placed job's domain is distinct (I2)
+    placed = got.assign[got.assign >= 0]
+    assert np.unique(placed).shape[0] == placed.shape[0]
+
+
+def test_config2_expected_shape(engine):
+    """cfg2 mirrors the 290 pods/s recovery: 990 jobs onto the 990 healthy racks."""
+    p = synth.config2()
+    engine.load(p)
+    got = engine.place(p.job_class)
+    healthy = np.setdiff1d(np.arange(1000), p.meta["bad_racks"])
+    np.testing.assert_array_equal(got.assign, healthy)
+
+
+@pytest.mark.parametrize("seed", range(120))
+def test_random_parity(engine, seed):
+    p = synth.random_problem(seed)
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_parity_large(engine, seed):
+    p = synth.random_problem(1000 + seed, max_nodes=400_000, max_jobs=30_000, max_leaves=20_000)
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+
+
+def test_trials_parity(engine):
+    """Recovery trials (seed = 2*1000 + trial) as timed by bench.py's p99 leg."""
+    for t in range(20):
+        p = synth.config2(trial=t)
+        got, a, cap, occ = run_both(engine, p)
+        assert_same(got, a, cap, occ)
+
+
+def _tiny(n_leaves=3, per=2, K=1):
+    topo = Topology(level_keys=["k"], n_domains=[n_leaves], first_leaf=[np.arange(n_leaves + 1, dtype=np.uint32)])
+    N = n_leaves * per
+    nodes = Nodes(leaf_start=(np.arange(n_leaves + 1) * per).astype(np.uint32),
+                  labels=np.ones((1, N), dtype=np.uint64), taints=np.zeros(N, dtype=np.uint32),
+                  free=np.full((1, N), 10, dtype=np.uint32), excl=np.full(N, -1, dtype=np.int32))
+    return topo, nodes
+
+
+def test_zero_jobs(engine):
+    topo, nodes = _tiny()
+    p = Problem(topology=topo, nodes=nodes, classes=[JobClass(pods=1)], job_class=np.zeros(0, dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    assert got.assign.shape == (0,)
+    np.testing.assert_array_equal(got.cap, cap)
+
+
+def test_more_jobs_than_domains(engine):
+    topo, nodes = _tiny(n_leaves=3)
+    p = Problem(topology=topo, nodes=nodes, classes=[JobClass(pods=2, req_res=(5,))],
+                job_class=np.zeros(7, dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+    np.testing.assert_array_equal(got.assign, [0, 1, 2, -1, -1, -1, -1])
+
+
+def test_all_infeasible(engine):
+    topo, nodes = _tiny()
+    p = Problem(topology=topo, nodes=nodes, classes=[JobClass(req_labels=(2,), pods=1)],
+                job_class=np.zeros(4, dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    assert (got.assign == -1).all()
+    assert_same(got, a, cap, occ)
+
+
+def test_empty_leaves_and_zero_rows(engine):
+    topo = Topology(level_keys=["z", "r"], n_domains=[2, 5],
+                    first_leaf=[np.array([0, 3, 5], dtype=np.uint32), np.arange(6, dtype=np.uint32)])
+    ls = np.array([0, 0, 4, 4, 4, 9], dtype=np.uint32)  # leaves 0, 2, 3 are empty
+    N = 9
+    nodes = Nodes(leaf_start=ls, labels=np.ones((1, N), dtype=np.uint64), taints=np.zeros(N, dtype=np.uint32),
+                  free=np.full((2, N), 7, dtype=np.uint32), excl=np.full(N, -1, dtype=np.int32))
+    classes = [JobClass(pods=4, level=1, req_res=(7, 1)), JobClass(pods=9, level=0, req_res=(7, 0))]
+    p = Problem(topology=topo, nodes=nodes, classes=classes, job_class=np.array([1, 0, 0, 1, 0], dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+
+
+def test_max_levels_words_resources(engine):
+    """K = 4 nested levels, W = 4 label words, R = 4 resources, 64 classes."""
+    rng = np.random.default_rng(7)
+    L = 256
+    fl3 = np.arange(L + 1, dtype=np.uint32)
+    fl2 = np.arange(0, L + 1, 4, dtype=np.uint32)
+    fl1 = np.arange(0, L + 1, 16, dtype=np.uint32)
+    fl0 = np.arange(0, L + 1, 64, dtype=np.uint32)
+    topo = Topology(level_keys=["a", "b", "c", "d"], n_domains=[4, 16, 64, 256], first_leaf=[fl0, fl1, fl2, fl3])
+    sizes = rng.integers(0, 9, L)
+    ls = np.zeros(L + 1, dtype=np.uint32)
+    np.cumsum(sizes, out=ls[1:])
+    N = int(ls[-1])
+    labels = rng.integers(0, 2**63, (4, N), dtype=np.uint64) | rng.integers(0, 2**63, (4, N), dtype=np.uint64)
+    nodes = Nodes(leaf_start=ls, labels=labels, taints=rng.integers(0, 4, N).astype(np.uint32),
+                  free=rng.integers(0, 100, (4, N)).astype(np.uint32),
+                  excl=np.where(rng.random(N) < 0.02, 5, -1).astype(np.int32))
+    classes = [JobClass(req_labels=tuple(int(x) for x in (rng.integers(0, 2**63, 4) & rng.integers(0, 2**63, 4)
+                                                            & rng.integers(0, 2**63, 4))),
+                        tolerated_taints=int(rng.integers(0, 4)), level=int(rng.integers(0, 4)),
+                        pods=int(rng.integers(1, 40)), req_res=tuple(int(x) for x in rng.integers(0, 30, 4)))
+               for _ in range(64)]
+    p = Problem(topology=topo, nodes=nodes, classes=classes,
+                job_class=rng.integers(0, 64, 500).astype(np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    assert_same(got, a, cap, occ)
+
+
+def test_exact_division_boundaries(engine):
+    """fit_count must equal floor(free/req) for every 32-bit value, incl. values
+    that break a float quotient (2^24+1, 2^32-1)."""
+    vals = np.array([0, 1, 2, 3, 7, 8, 9, 1 << 24, (1 << 24) + 1, (1 << 24) - 1, 123456789, (1 << 31) - 1,
+                     1 << 31, (1 << 32) - 1, 999_999_937, 4_000_000_000], dtype=np.uint64)
+    reqs = [1, 2, 3, 7, 1000, 4097, (1 << 20) + 3, 65521, 4_000_000_001, (1 << 32) - 1]
+    N = vals.shape[0]
+    topo = Topology(level_keys=["k"], n_domains=[N], first_leaf=[np.arange(N + 1, dtype=np.uint32)])
+    nodes = Nodes(leaf_start=np.arange(N + 1, dtype=np.uint32), labels=np.zeros((1, N), dtype=np.uint64),
+                  taints=np.zeros(N, dtype=np.uint32), free=vals.astype(np.uint32)[None, :],
+                  excl=np.full(N, -1, dtype=np.int32))
+    classes = [JobClass(pods=1 << 22, req_res=(r,)) for r in reqs]
+    p = Problem(topology=topo, nodes=nodes, classes=classes, job_class=np.zeros(0, dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    exp = np.minimum(vals[None, :] // np.array(reqs, dtype=np.uint64)[:, None], 1 << 22).astype(np.uint32)
+    np.testing.assert_array_equal(got.cap, exp)
+    np.testing.assert_array_equal(cap, exp)
+
+
+def test_patch_then_place(engine):
+    p = synth.config2()
+    engine.load(p)
+    rows = np.array([0, 15 * 500 + 3, 14999], dtype=np.uint32)
+    taints = np.array([1, 1, 0], dtype=np.uint32)
+    engine.patch_rows(rows, taints=taints)
+    got = engine.place(p.job_class, want_tally=True)
+    p.nodes.taints[rows] = taints
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+
+
+def test_sharded_tally_allreduce_parity(engine):
+    """The multi-GPU protocol on one device: domain-aligned shards tally into
+    zero-initialised buffers, the buffers are summed (what the RCCL all-reduce
+    does), and every shard's assignment equals the unsharded one."""
+    import torch
+    p = synth.config5()
+    a_ref, cap_ref, occ_ref = O.place_c(p)
+    world = 3
+    L, C = p.topology.n_leaves, len(p.classes)
+    cap_sum = torch.zeros((C, L), dtype=torch.int32, device="cuda")
+    occ_sum = torch.zeros(L, dtype=torch.int32, device="cuda")
+    engines = [Engine(0) for _ in range(world)]
+    try:
+        for r, e in enumerate(engines):
+            e.upload_topology(p.topology)
+            e.upload_snapshot(shard_problem(p, r, world))
+            e.upload_classes(p.classes)
+            cap = torch.zeros((C, L), dtype=torch.int32, device="cuda")
+            occ = torch.zeros(L, dtype=torch.int32, device="cuda")
+            e.tally_device(cap.data_ptr(), occ.data_ptr(), L, torch.cuda.current_stream().cuda_stream)
+            cap_sum += cap
+            occ_sum += occ
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(cap_sum.cpu().numpy().astype(np.uint32), cap_ref)
+        np.testing.assert_array_equal(occ_sum.cpu().numpy().astype(np.uint32), occ_ref)
+        jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+        for e in engines:
+            out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+            e.assign_device(cap_sum.data_ptr(), occ_sum.data_ptr(), L, jc.data_ptr(), p.n_jobs, out.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(out.cpu().numpy(), a_ref)
+    finally:
+        for e in engines:
+            e.close()
+
+
+def test_place_device_matches_host_api(engine):
+    import torch
+    p = synth.config3()
+    engine.load(p)
+    jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+    out = torch.full((p.n_jobs,), -7, dtype=torch.int32, device="cuda")
+    engine.place_device(jc.data_ptr(), p.n_jobs, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), O.place_c(p)[0])
+
+
+def test_resolve_and_audit(engine):
+    """Batched A5/A9: leader row -> domain at the job's level, and follower
+    nodeSelector domains audited against it (validatePodPlacements)."""
+    p = synth.config5()
+    engine.load(p)
+    leaf_of_row = p.nodes.leaf_of_row()
+    rows = np.array([0, 17, 16383, -1, 2048, 5000], dtype=np.int32)
+    levels = np.array([1, 0, 1, 1, 0, 1], dtype=np.uint32)
+    got = engine.resolve_leader_domains(rows, levels)
+    zone_of_leaf = p.topology.parent_of_leaf(0)
+    exp = []
+    for r, k in zip(rows, levels):
+        if r < 0:
+            exp.append(-1)
+        else:
+            leaf = leaf_of_row[r]
+            exp.append(int(leaf) if k == 1 else int(zone_of_leaf[leaf]))
+    np.testing.assert_array_equal(got, exp)
+    off = np.array([0, 3, 3, 5, 6, 6, 9], dtype=np.uint32)
+    fd = np.array([exp[0], exp[0], exp[0], 999, exp[2], 0, exp[4], 3, exp[4]], dtype=np.int32)
+    bad = engine.audit_placements(rows, levels, off, fd)
+    np.testing.assert_array_equal(bad, [0, 0, 1, 0xFFFFFFFF, 0, 1])
+
+
+def test_error_paths(engine):
+    e = Engine(0)
+    try:
+        with pytest.raises(JspError) as ei:
+            e.place(np.zeros(1, dtype=np.uint32))
+        assert ei.value.code == JSP_ESTATE
+        topo, nodes = _tiny()
+        e.upload_topology(topo)
+        with pytest.raises(JspError) as ei:
+            e.upload_classes([JobClass(pods=0)])
+        assert ei.value.code == JSP_EINVAL
+        bad = Topology(level_keys=["a", "b"], n_domains=[2, 3],
+                       first_leaf=[np.array([0, 2, 3], dtype=np.uint32), np.arange(4, dtype=np.uint32)])
+        bad.first_leaf[0] = np.array([0, 1, 3], dtype=np.uint32)
+        e.upload_topology(bad)  # 1 and 3 are level-1 boundaries: nested, accepted
+        with pytest.raises(JspError) as ei:
+            e.upload_topology(Topology(level_keys=["a"], n_domains=[3],
+                                       first_leaf=[np.array([0, 2, 1, 3], dtype=np.uint32)]))
+        assert ei.value.code == JSP_EINVAL
+        with pytest.raises(JspError) as ei:
+            e.upload_topology(Topology(level_keys=["a"], n_domains=[2_000_000],
+                                       first_leaf=[np.arange(2_000_001, dtype=np.uint32)]))
+        assert ei.value.code == JSP_ERANGE
+    finally:
+        e.close()
