@@ -106,17 +106,24 @@ typedef struct jsp_job_class {
 typedef struct jsp_stats {
     uint32_t jobs;             /* J */
     uint32_t placed;           /* assign[j] != -1 */
-    uint32_t runs;             /* same-class job runs the assignment walked */
-    uint32_t reserved;
+    uint32_t runs;             /* replicated-job runs the assignment walked */
+    uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
 typedef struct jsp_timing {
-    uint64_t calls;            /* timed jsp_*_device calls since last reset */
+    uint64_t calls;            /* timed placements (or tallies) since last reset */
     double tally_ms;           /* summed HIP-event time of the tally kernel */
     double feas_ms;            /* summed HIP-event time of the feasibility-bitmap kernel */
     double assign_ms;          /* summed HIP-event time of the assignment kernel */
+    double fused_ms;           /* summed HIP-event time of single-launch placements (fused / compaction) */
+    uint64_t fused_calls;      /* placements that ran as a single launch */
 } jsp_timing;
+
+/* jsp_engine_set_fused modes */
+#define JSP_FUSED_OFF 0       /* always tally -> feas -> assign (three launches) */
+#define JSP_FUSED_AUTO 1      /* one launch when possible (default): the single-class compaction
+                                 for one leaf-level class, the fused tail for small snapshots */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);
@@ -136,25 +143,34 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n,
                        const uint32_t* free_res, const int32_t* excl_owner);
 int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t n_classes);
 
-/* ---- placement (host buffers; includes H2D of job_class and D2H of results) ----
- * assign_out [J]: domain id at the job's class level, -1 = unplaceable.
+/* ---- placement (host buffers; includes H2D of the runs and D2H of results) ----
+ * Jobs arrive as replicated-job runs in global order: run i is run_len[i]
+ * consecutive jobs of class run_class[i] (one ReplicatedJob with
+ * rjob.Replicas children, jobset_controller.go:638-649; global job index =
+ * globalJobIndex, :1056-1065). n_jobs = sum of run_len.
+ * assign_out [n_jobs]: domain id at the job's class level, -1 = unplaceable.
  * tally_out (nullable) [C][n_leaves_total]: per-(class, leaf) pod capacity.
  * occ_out (nullable) [n_leaves_total]: rows covered by other exclusive jobs. */
-int jsp_place(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
-              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out,
-              jsp_stats* stats);
+int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);
+/* Same with one class id per job (run-length encoded on the host). */
+int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
+                   int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);
 
-/* ---- placement (device-resident buffers; stream = hipStream_t or NULL) ----
+/* ---- placement (device-resident buffers) ----
+ * `stream` is a hipStream_t used as given: NULL = the HIP null stream (torch's
+ * default stream), jsp_engine_stream(e) = the engine's own stream.
  * d_cap [C][ld] and d_occ [ld] with ld >= total leaves; a shard writes only
  * columns [leaf_begin, leaf_begin+n_leaves) so the caller can SUM-all-reduce
- * zero-initialised buffers across shards before jsp_assign_device. */
+ * zero-initialised buffers across shards before jsp_assign_device.
+ * d_run_class / d_run_len [n_runs] as for jsp_place; n_jobs = their sum. */
 int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld,
                      void* stream);
 int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ,
-                      uint32_t ld, const uint32_t* d_job_class, uint32_t n_jobs,
-                      int32_t* d_assign, void* stream);
-int jsp_place_device(jsp_engine* e, const uint32_t* d_job_class, uint32_t n_jobs,
-                     int32_t* d_assign, void* stream);
+                      uint32_t ld, const uint32_t* d_run_class, const uint32_t* d_run_len,
+                      uint32_t n_runs, uint32_t n_jobs, int32_t* d_assign, void* stream);
+int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len,
+                     uint32_t n_runs, uint32_t n_jobs, int32_t* d_assign, void* stream);
 
 /* ---- follower pinning and audit (batched webhook / PodReconciler work) ----
  * jsp_resolve_leader_domains: for each job, the domain (at `levels[i]`) of
@@ -171,7 +187,8 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
                          const uint32_t* follower_off, const int32_t* follower_domains,
                          uint32_t n_jobs, uint32_t* bad_out);
 
-/* ---- instrumentation ---- */
+/* ---- instrumentation / tuning ---- */
+int jsp_engine_set_fused(jsp_engine* e, int mode);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

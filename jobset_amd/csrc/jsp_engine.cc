@@ -60,7 +60,7 @@ struct DevBuf {
 
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
-    int tag = 0;  // 0 tally, 1 feas, 2 assign
+    int tag = 0;  // 0 tally, 1 feas, 2 assign, 3 fused
 };
 
 }  // namespace
@@ -83,8 +83,9 @@ struct jsp_engine {
     // snapshot
     bool have_snap = false;
     uint32_t N = 0, npad = 0, W = 0, R = 0, leaf_begin = 0, n_leaves = 0, max_leaf_rows = 0;
-    DevBuf labels, taints, freer, excl, leaf_start, blk_leaf;
+    DevBuf labels, taints, freer, excl, leaf_start, blk;
     uint32_t n_blocks = 0;
+    uint32_t epoch = 0;  // compaction launches so far (granule tags)
 
     // classes
     bool have_cls = false;
@@ -94,7 +95,9 @@ struct jsp_engine {
     uint32_t feas_words = 0;
 
     // scratch
-    DevBuf cap, occ, jobs, assign, stats, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+    DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+    int fused_mode = JSP_FUSED_AUTO;
+    uint32_t last_shape = 0;  // 0 three launches, 1 fused tail, 2 single-class compaction
 
     // timing
     bool timing = false;
@@ -116,6 +119,13 @@ namespace {
 
 constexpr uint32_t kTargetBlockRows = jsp::kChunkRows - 4;  // one chunk even when unaligned
 constexpr size_t kMaxEvents = 3 * 4096;
+// Above this many tally workgroups the three-launch shape wins: the fused tail
+// runs feasibility + assignment on one 256-thread workgroup.
+constexpr uint32_t kFusedMaxBlocks = 64;
+// Compaction workgroups resident at once without doubt: 256 CUs x 4 (LDS and
+// VGPRs admit more). Up to this grid the tile is blockIdx.x; above it tiles
+// are taken from a ticket so a workgroup only waits on started ones.
+constexpr uint32_t kCoresidentBlocks = 1024;
 
 int resolve_timing(jsp_engine* e) {
     if (e->ev_used == 0) return JSP_OK;
@@ -125,7 +135,8 @@ int resolve_timing(jsp_engine* e) {
         HIP_TRY(hipEventElapsedTime(&ms, e->ev[i].a, e->ev[i].b));
         if (e->ev[i].tag == 0) e->acc.tally_ms += ms;
         else if (e->ev[i].tag == 1) e->acc.feas_ms += ms;
-        else e->acc.assign_ms += ms;
+        else if (e->ev[i].tag == 2) e->acc.assign_ms += ms;
+        else e->acc.fused_ms += ms;
     }
     e->ev_used = 0;
     return JSP_OK;
@@ -142,7 +153,8 @@ EvPair* ev_begin(jsp_engine* e, int tag, hipStream_t s) {
     }
     EvPair* p = &e->ev[e->ev_used++];
     p->tag = tag;
-    if (tag == 0) e->acc.calls += 1;
+    if (tag == 0 || tag == 3) e->acc.calls += 1;
+    if (tag == 3) e->acc.fused_calls += 1;
     (void)hipEventRecord(p->a, s);
     return p;
 }
@@ -151,7 +163,9 @@ void ev_end(EvPair* p, hipStream_t s) {
     if (p) (void)hipEventRecord(p->b, s);
 }
 
-hipStream_t pick(jsp_engine* e, void* s) { return s ? static_cast<hipStream_t>(s) : e->stream; }
+// The caller's stream is used as given: NULL is the HIP null stream (what
+// torch's default stream is), jsp_engine_stream(e) the engine's own.
+hipStream_t pick(jsp_engine*, void* s) { return static_cast<hipStream_t>(s); }
 
 int check_engine(jsp_engine* e) {
     if (!e) return set_err(JSP_EINVAL, "engine is NULL");
@@ -166,7 +180,7 @@ hipError_t upload(DevBuf& b, const T* src, size_t n, hipStream_t s) {
     return hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s);
 }
 
-int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s) {
+jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld) {
     jsp::TallyArgs a{};
     a.labels = e->labels.as<uint64_t>();
     a.taints = e->taints.as<uint32_t>();
@@ -174,7 +188,7 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
     a.excl = e->excl.as<int32_t>();
     a.npad = e->npad;
     a.leaf_start = e->leaf_start.as<uint32_t>();
-    a.blk_leaf = e->blk_leaf.as<uint32_t>();
+    a.blk = e->blk.as<uint4>();
     a.n_blocks = e->n_blocks;
     a.cls = e->cls.as<jsp::DevClass>();
     a.cap_out = d_cap;
@@ -183,6 +197,14 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
     a.leaf_base = e->leaf_begin;
     a.W = (int)e->W;
     a.R = (int)e->R;
+    a.c0 = 0;
+    a.nc = std::min<uint32_t>(e->C, jsp::kTallyClasses);
+    a.do_occ = 1;
+    return a;
+}
+
+int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s) {
+    jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
     if (e->n_blocks == 0) return JSP_OK;
     EvPair* p = ev_begin(e, 0, s);
     uint32_t c0 = 0;
@@ -198,17 +220,117 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
 }
 
 int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
-                const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, hipStream_t s) {
+                const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
+                int32_t* d_assign, hipStream_t s) {
     EvPair* p = ev_begin(e, 1, s);
     HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
                              e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
     ev_end(p, s);
     p = ev_begin(e, 2, s);
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
-                               e->C, e->topo, e->t_off.as<uint32_t>(), e->t_off_h[e->K], d_job_class, J, d_assign,
+                               e->C, e->topo, e->t_off_h[e->K], d_run_class, d_run_len, n_runs, J, d_assign,
                                e->stats.as<uint32_t>(), s));
     ev_end(p, s);
     return JSP_OK;
+}
+
+bool fused_ok(jsp_engine* e) {
+    return e->fused_mode == JSP_FUSED_AUTO && e->n_blocks > 0 && e->n_blocks <= kFusedMaxBlocks &&
+           e->C <= (uint32_t)jsp::kTallyClasses &&
+           e->leaf_begin == 0 && e->n_leaves == e->L_total &&
+           e->t_off_h[e->K] + e->feas_words <= jsp::kFusedMaxWords;
+}
+
+// One class at the leaf level: job j takes the j-th feasible leaf (any size).
+bool compact_ok(jsp_engine* e) {
+    return e->fused_mode == JSP_FUSED_AUTO && e->n_blocks > 0 && e->C == 1 && e->cls_h[0].level + 1 == e->K &&
+           e->leaf_begin == 0 && e->n_leaves == e->L_total;
+}
+
+// Whole placement on the engine's own tally buffers: one compaction launch for
+// a single leaf-level class, one fused launch when the snapshot is small, else
+// tally -> feas -> assign.
+int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
+               int32_t* d_assign, hipStream_t s) {
+    if (compact_ok(e)) {
+        e->last_shape = 2;
+        jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
+        jsp::CompactArgs f{};
+        f.ticket = e->ticket.as<unsigned long long>();
+        f.granules = e->granules.as<unsigned long long>();
+        f.pods = e->cls_h[0].pods;
+        f.n_runs = n_runs;
+        f.J = J;
+        f.assign = d_assign;
+        f.stats = e->stats.as<uint32_t>();
+        e->epoch = e->epoch % 0x3FFFFFFFu + 1u;
+        f.epoch = e->epoch;
+        f.coresident = e->n_blocks <= kCoresidentBlocks ? 1u : 0u;
+        EvPair* p = ev_begin(e, 3, s);
+        HIP_TRY(jsp::launch_compact(a, f, s));
+        ev_end(p, s);
+        return JSP_OK;
+    }
+    e->last_shape = fused_ok(e) ? 1 : 0;
+    if (e->last_shape == 0) {
+        if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
+        return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_run_class, d_run_len,
+                           n_runs, J, d_assign, s);
+    }
+    jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
+    jsp::FusedArgs f{};
+    f.ticket = e->ticket.as<unsigned long long>();
+    f.C = e->C;
+    f.topo = e->topo;
+    f.t_off = e->t_off.as<uint32_t>();
+    f.t_words = e->t_off_h[e->K];
+    f.word_off = e->word_off.as<uint32_t>();
+    f.feas_words = e->feas_words;
+    f.run_class = d_run_class;
+    f.run_len = d_run_len;
+    f.n_runs = n_runs;
+    f.J = J;
+    f.assign = d_assign;
+    f.stats = e->stats.as<uint32_t>();
+    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc + a.do_occ);
+    EvPair* p = ev_begin(e, 3, s);
+    HIP_TRY(jsp::launch_fused(a, f, s));
+    ev_end(p, s);
+    return JSP_OK;
+}
+
+// Host-side validation of a run list; returns the job count through *J.
+int check_runs(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint64_t* J) {
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < n_runs; ++i) {
+        if (run_class[i] >= e->C) return set_err(JSP_EINVAL, "run %u: class %u out of range (%u classes)", i,
+                                                  run_class[i], e->C);
+        n += run_len[i];
+    }
+    if (n > (1u << 30)) return set_err(JSP_ERANGE, "%llu jobs exceed the 2^30 limit", (unsigned long long)n);
+    *J = n;
+    return JSP_OK;
+}
+
+// Branch-free invariant-divisor constants for floor(n / d) over uint32 n
+// (the form of libdivide's u32 "branchfree" divider; exactness is checked by
+// tests/test_engine_gpu.py::test_exact_division_boundaries).
+void divisor_magic(uint32_t d, uint32_t* magic, uint32_t* shift) {
+    *magic = 0;
+    *shift = jsp::kDivIdentity;
+    if (d <= 1) return;  // d == 0: resource not requested (never divided)
+    uint32_t L = 31 - (uint32_t)__builtin_clz(d);
+    if ((d & (d - 1)) == 0) {  // 2^L: t = n >> 1, then >> (L - 1)
+        *shift = L - 1;
+        return;
+    }
+    const uint64_t num = 1ull << (32 + L);
+    uint64_t m = num / d;
+    const uint64_t rem = num % d;
+    m = (m + m) & 0xFFFFFFFFull;
+    if (rem + rem >= d) m = (m + 1) & 0xFFFFFFFFull;
+    *magic = (uint32_t)((1 + m) & 0xFFFFFFFFull);
+    *shift = L;
 }
 
 int ready(jsp_engine* e, bool need_cls) {
@@ -260,7 +382,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         delete e;
         return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
     }
-    if (e->stats.reserve(16) != hipSuccess) {
+    if (e->stats.reserve(16) != hipSuccess || hipMemset(e->stats.p, 0, 16) != hipSuccess) {
         delete e;
         return set_err(JSP_ENOMEM, "stats buffer");
     }
@@ -405,7 +527,13 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
         HIP_TRY(hipMemcpyAsync(e->excl.p, nd->excl_owner, (size_t)N * 4, hipMemcpyHostToDevice, s));
     }
     HIP_TRY(upload(e->leaf_start, ls, (size_t)NL + 1, s));
-    HIP_TRY(upload(e->blk_leaf, blk.data(), blk.size(), s));
+    std::vector<uint4> bt(blk.size() > 0 ? blk.size() - 1 : 0);
+    for (size_t b = 0; b + 1 < blk.size(); ++b) bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
+    HIP_TRY(upload(e->blk, bt.data(), std::max<size_t>(bt.size(), 1), s));
+    HIP_TRY(e->ticket.reserve(16));
+    HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch ticket: grows by n_blocks per launch
+    HIP_TRY(e->granules.reserve(8 * blk.size()));
+    HIP_TRY(hipMemsetAsync(e->granules.p, 0, 8 * blk.size(), s));  // look-back granules (epoch 0 never matches)
     HIP_TRY(hipStreamSynchronize(s));
     e->N = N;
     e->npad = npad;
@@ -469,14 +597,14 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
         std::memset(&d, 0, sizeof d);
         for (int w = 0; w < 4; ++w) {
             d.req[w] = x.req_labels[w];
-            d.forbid[w] = x.forbid_labels[w];
+            d.mask[w] = x.req_labels[w] | x.forbid_labels[w];
         }
-        d.tol = x.tolerated_taints;
+        d.tol_inv = ~x.tolerated_taints;
         d.level = x.level;
         d.pods = x.pods;
         for (int r = 0; r < 4; ++r) {
             d.res[r] = x.req_res[r];
-            d.rcp[r] = x.req_res[r] ? 1.0f / (float)x.req_res[r] : 0.f;
+            divisor_magic(x.req_res[r], &d.magic[r], &d.shift[r]);
         }
         woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
     }
@@ -504,63 +632,81 @@ int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t l
 }
 
 int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
-                      const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, void* stream) {
+                      const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t n_jobs,
+                      int32_t* d_assign, void* stream) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
-    if (J > 0 && (!d_job_class || !d_assign)) return set_err(JSP_EINVAL, "job buffers are NULL");
-    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
-    return assign_impl(e, d_cap, d_occ, ld, d_job_class, J, d_assign, pick(e, stream));
+    if (!d_cap || !d_occ) return set_err(JSP_EINVAL, "tally buffers are NULL");
+    if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
+    if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
+    return assign_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
 }
 
-int jsp_place_device(jsp_engine* e, const uint32_t* d_job_class, uint32_t J, int32_t* d_assign, void* stream) {
+int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
+                     uint32_t n_jobs, int32_t* d_assign, void* stream) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
         return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
-    if (J > 0 && (!d_job_class || !d_assign)) return set_err(JSP_EINVAL, "job buffers are NULL");
-    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
-    hipStream_t s = pick(e, stream);
-    if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
-    return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_job_class, J, d_assign, s);
+    if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
+    if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
+    return place_impl(e, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
 }
 
-int jsp_place(jsp_engine* e, const uint32_t* job_class, uint32_t J, int32_t* assign_out, uint32_t* tally_out,
-              uint32_t* occ_out, jsp_stats* stats) {
+int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (int rc = check_engine(e)) return rc;
     auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
         return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
-    if (J > 0 && (!job_class || !assign_out)) return set_err(JSP_EINVAL, "job buffers are NULL");
-    if (J > 0 && e->C == 0) return set_err(JSP_EINVAL, "jobs given but no classes");
-    for (uint32_t j = 0; j < J; ++j)
-        if (job_class[j] >= e->C) return set_err(JSP_EINVAL, "job %u: class %u out of range", j, job_class[j]);
+    if (n_runs > 0 && (!run_class || !run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
+    uint64_t J64 = 0;
+    if (int rc = check_runs(e, run_class, run_len, n_runs, &J64)) return rc;
+    const uint32_t J = (uint32_t)J64;
+    if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     hipStream_t s = e->stream;
-    HIP_TRY(upload(e->jobs, job_class, J, s));
+    HIP_TRY(upload(e->run_class, run_class, n_runs, s));
+    HIP_TRY(upload(e->run_len, run_len, n_runs, s));
     HIP_TRY(e->assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
-    if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
-    if (int rc = assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, e->jobs.as<uint32_t>(), J,
-                             e->assign.as<int32_t>(), s))
+    if (int rc = place_impl(e, e->run_class.as<uint32_t>(), e->run_len.as<uint32_t>(), n_runs, J,
+                            e->assign.as<int32_t>(), s))
         return rc;
-    uint32_t st[2] = {0, 0};
+    uint32_t st[3] = {0, 0, 0};
     if (J > 0) HIP_TRY(hipMemcpyAsync(assign_out, e->assign.p, (size_t)J * 4, hipMemcpyDeviceToHost, s));
     if (tally_out && e->C > 0)
         HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
     if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
-    if (stats) HIP_TRY(hipMemcpyAsync(st, e->stats.p, sizeof st, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(st, e->stats.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (e->last_shape == 2 && st[2] != 0)
+        return set_err(JSP_EHIP, "compaction look-back timed out (a workgroup never published its count)");
     if (stats) {
         stats->jobs = J;
-        stats->runs = J > 0 ? st[0] : 0;
-        stats->placed = J > 0 ? st[1] : 0;
-        stats->reserved = 0;
+        stats->runs = n_runs > 0 ? st[0] : 0;
+        stats->placed = n_runs > 0 ? st[1] : 0;
+        stats->fused = e->last_shape;
         stats->wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     }
     return JSP_OK;
+}
+
+int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs, int32_t* assign_out,
+                   uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
+    if (n_jobs > 0 && !job_class) return set_err(JSP_EINVAL, "job_class is NULL");
+    std::vector<uint32_t> rc, rl;
+    for (uint32_t j = 0; j < n_jobs; ++j) {
+        if (rc.empty() || rc.back() != job_class[j]) {
+            rc.push_back(job_class[j]);
+            rl.push_back(0);
+        }
+        ++rl.back();
+    }
+    return jsp_place(e, rc.data(), rl.data(), (uint32_t)rc.size(), assign_out, tally_out, occ_out, stats);
 }
 
 int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels, uint32_t n,
@@ -606,6 +752,14 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
                               e->leaf_begin, e->topo, e->tmp_e.as<uint32_t>(), s));
     HIP_TRY(hipMemcpyAsync(bad_out, e->tmp_e.p, (size_t)n_jobs * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    return JSP_OK;
+}
+
+int jsp_engine_set_fused(jsp_engine* e, int mode) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (mode != JSP_FUSED_OFF && mode != JSP_FUSED_AUTO) return set_err(JSP_EINVAL, "fused mode %d", mode);
+    e->fused_mode = mode;
     return JSP_OK;
 }
 

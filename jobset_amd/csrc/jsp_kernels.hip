@@ -1,17 +1,24 @@
 // jsp_kernels.hip — gfx950 kernels of the exclusive-topology placement engine.
 //
-// Three kernels make one placement (SURVEY.md §8a rows A8 then A7):
-//   tally_kernel   HBM-streaming predicate + per-(class, leaf) capacity tally.
-//                  One workgroup owns a contiguous run of whole leaves, so every
-//                  leaf sum is finished inside one workgroup: no global atomics,
-//                  no memset, bit-exact integer sums written exactly once.
-//   feas_kernel    per-(class, domain) feasibility bitmap at the class's level
-//                  (wave64 ballot -> one 64-bit word per wave).
-//   assign_kernel  single-workgroup lowest-index 1:1 assignment over same-class
-//                  job runs: block-wide popcount prefix over bitmap words gives
-//                  the k-th available domain to the k-th job of the run.
-// Plus two small gather kernels for the webhook / reconciler batch paths
-// (A5 follower pinning, A9 placement audit).
+// A placement is (SURVEY.md §8a rows A8 then A7):
+//   tally   HBM-streaming predicate + per-(class, leaf) pod-capacity tally.
+//           One workgroup owns a contiguous run of whole leaves, so every leaf
+//           sum finishes inside one workgroup: no global atomics, no memset,
+//           bit-exact integer sums, each written exactly once.
+//   feas    per-(class, domain) feasibility bitmap at the class's topology
+//           level (wave64 ballot -> one 64-bit word per wave).
+//   assign  lowest-index 1:1 assignment, walked as replicated-job runs (one
+//           class each): a block-wide prefix of word popcounts hands the k-th
+//           available domain to the k-th job of the run.
+// Two launch shapes:
+//   large snapshots: tally_kernel (grid) -> feas_kernel (grid) -> assign_kernel
+//                    (one 1024-thread workgroup);
+//   small snapshots: place_fused_kernel — the tally grid, after which the last
+//                    workgroup to finish (agent-scope release/acquire ticket)
+//                    builds the bitmaps in LDS and runs the assignment; one
+//                    launch per placement.
+// Plus gather kernels for the webhook / reconciler batch paths (A5, A9) and the
+// snapshot patch.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -20,98 +27,104 @@
 namespace jsp {
 
 // ----------------------------------------------------------------- helpers
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int lane) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        uint32_t y = __shfl_up(x, off, 64);
-        if (lane >= off) x += y;
-    }
+// Inclusive wave64 prefix sum on the VALU with DPP (no LDS traffic):
+// row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry the
+// row totals across rows (GFX9/CDNA DPP controls).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int /*lane*/) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
 }
 
-// floor(free / req) clamped to `pods`, exact for every uint32 input: the
-// float quotient is only an estimate, corrected by one step either way.
-__device__ __forceinline__ uint32_t fit_count(uint32_t free, uint32_t req, float rcp, uint32_t pods) {
-    if ((uint64_t)req * pods <= (uint64_t)free) return pods;
-    uint32_t q = (uint32_t)((float)free * rcp);
-    if ((uint64_t)q * req > (uint64_t)free) q -= 1;
-    else if ((uint64_t)(q + 1) * req <= (uint64_t)free) q += 1;
-    return q < pods ? q : pods;
+// floor(n / d) for a divisor known per class, exact for every uint32 n
+// (branch-free invariant-divisor division: one multiply-high, shifts, adds).
+__device__ __forceinline__ uint32_t div_invariant(uint32_t n, uint32_t magic, uint32_t shift) {
+    const uint32_t q = __umulhi(n, magic);
+    const uint32_t t = (((n - q) >> 1) + q) >> (shift & 31u);
+    return shift == kDivIdentity ? n : t;
 }
 
-// ----------------------------------------------------------------- A8 tally
-// Rows of the workgroup: [leaf_start[l0], leaf_start[l1]) for leaves
-// [blk_leaf[b], blk_leaf[b+1]). Each thread holds 4 consecutive rows (16-B
-// column loads; a wave streams 1 KiB per column instruction). Per class the
-// workgroup computes an inclusive prefix over its rows; a leaf's sum is
-// prefix(last row) - prefix(before first row), folded into acc[c][leaf] with
-// two LDS atomics placed at the leaf's first and last rows.
+// last leaf index l in [0, n) with ls[l] <= row (ls ascending, n+1 entries)
+__device__ __forceinline__ uint32_t leaf_search(const uint32_t* ls, uint32_t n, uint32_t row) {
+    uint32_t lo = 0, hi = n;  // invariant: ls[lo] <= row, answer < hi
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ls[mid] <= row) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// ----------------------------------------------------------------- A8 tally (one workgroup)
+// LDS carve (uint32 words), sized per launch by nv = classes in this pass + 1:
+//   [classes kTallyClasses x DevClass][acc nv x kMaxBlkLeaves][wsum nv x 4]
+//   [leaf starts kMaxBlkLeaves+1 (+3 pad)][row prefixes nv x kChunkRows]
+// Class records are staged in LDS once per workgroup (read per row from global
+// memory they were re-fetched by vector loads: a generic pointer may alias
+// LDS, and SGPRs are too few to hold them).
+constexpr int kClsWords = kTallyClasses * (int)(sizeof(DevClass) / 4);
+__host__ __device__ constexpr int tally_acc_off() { return kClsWords; }
+__host__ __device__ constexpr int tally_wsum_off(int nv) { return kClsWords + nv * kMaxBlkLeaves; }
+__host__ __device__ constexpr int tally_ls_off(int nv) { return tally_wsum_off(nv) + nv * kTallyWaves; }
+__host__ __device__ constexpr int tally_pre_off(int nv) { return tally_ls_off(nv) + kMaxBlkLeaves + 4; }
+__host__ __device__ constexpr int tally_lds_words(int nv) { return tally_pre_off(nv) + nv * kChunkRows; }
+
+// Rows of the workgroup: [r0, r1) = leaves [l0, l1). Per chunk of 1024 rows
+// each thread holds 4 consecutive rows (16-B column loads: a wave streams
+// 1 KiB per column instruction), evaluates every class on them, and writes its
+// rows' in-wave inclusive prefixes (DPP wave scan) to LDS — a pure streaming
+// pass, no branches on leaf boundaries. Then one thread per leaf adds
+// prefix(last row in chunk) - prefix(row before first in chunk) of its leaf
+// (plus the earlier waves' totals) to acc[v][leaf]; the leaf is owned by that
+// thread, so no atomics.
 template <int W, int R>
-__global__ __launch_bounds__(kTallyThreads) void tally_kernel(
-    const uint64_t* __restrict__ labels, const uint32_t* __restrict__ taints,
-    const uint32_t* __restrict__ freer, const int32_t* __restrict__ excl, uint32_t npad,
-    const uint32_t* __restrict__ leaf_start, const uint32_t* __restrict__ blk_leaf,
-    const DevClass* __restrict__ cls, uint32_t c0, uint32_t nc, int do_occ,
-    uint32_t* __restrict__ cap_out, uint32_t* __restrict__ occ_out, uint32_t ld, uint32_t leaf_base) {
-    __shared__ int16_t s_start[kChunkRows];
-    __shared__ int16_t s_end[kChunkRows];
-    __shared__ uint32_t s_acc[(kTallyClasses + 1) * kMaxBlkLeaves];
-    __shared__ uint32_t s_wsum[(kTallyClasses + 1) * kTallyWaves];
-    __shared__ uint32_t s_carry[kTallyClasses + 1];
+__device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
+    const int nc = (int)a.nc;
+    const int nv = nc + a.do_occ;
+    DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
+    uint32_t* s_acc = lds + tally_acc_off();
+    uint32_t* s_wsum = lds + tally_wsum_off(nv);
+    uint32_t* s_ls = lds + tally_ls_off(nv);
+    uint32_t* s_pre = lds + tally_pre_off(nv);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t l0 = blk_leaf[blockIdx.x], l1 = blk_leaf[blockIdx.x + 1];
-    const uint32_t nl = l1 - l0;
-    const uint32_t r0 = leaf_start[l0], r1 = leaf_start[l1];
-    const int nv = (int)nc + do_occ;
+    const uint4 bt = a.blk[blk];  // {first leaf, end leaf, first row, end row}
+    const uint32_t l0 = bt.x, nl = bt.y - bt.x, r0 = bt.z, r1 = bt.w;
 
+    for (uint32_t i = tid; i <= nl; i += kTallyThreads) s_ls[i] = a.leaf_start[l0 + i];
     for (int i = tid; i < nv * kMaxBlkLeaves; i += kTallyThreads) s_acc[i] = 0;
-    if (tid < nv) s_carry[tid] = 0;
+    {
+        const uint4* src = reinterpret_cast<const uint4*>(a.cls + a.c0);
+        uint4* dst = reinterpret_cast<uint4*>(s_cls);
+        for (int i = tid; i < nc * (int)(sizeof(DevClass) / 16); i += kTallyThreads) dst[i] = src[i];
+    }
 
     for (uint32_t base = r0 & ~3u; base < r1; base += kChunkRows) {
-        for (int i = tid; i < kChunkRows; i += kTallyThreads) { s_start[i] = -1; s_end[i] = -1; }
-        __syncthreads();
-        for (uint32_t li = tid; li < nl; li += kTallyThreads) {
-            uint32_t s = leaf_start[l0 + li], e = leaf_start[l0 + li + 1];
-            if (s < e) {
-                if (s >= base && s < base + kChunkRows) s_start[s - base] = (int16_t)li;
-                if (e - 1 >= base && e - 1 < base + kChunkRows) s_end[e - 1 - base] = (int16_t)li;
-            }
-        }
-        __syncthreads();
-
+        // ---- issue this chunk's row loads before any barrier
         const uint32_t row = base + 4u * tid;
-        const bool any = (row < r1) && (row + 3 >= r0) && (row < npad);
+        const bool any = (row < r1) && (row + 3 >= r0);
         uint64_t lab[W][4];
         uint32_t tn[4], fr[R][4];
         int32_t ex[4];
-        bool valid[4];
-        int16_t ms[4], me[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            valid[i] = any && (row + i >= r0) && (row + i < r1);
-            ms[i] = -1;
-            me[i] = -1;
-        }
         if (any) {
 #pragma unroll
             for (int w = 0; w < W; ++w) {
-                const ulonglong2* p = reinterpret_cast<const ulonglong2*>(labels + (size_t)w * npad + row);
-                ulonglong2 a = p[0], b = p[1];
-                lab[w][0] = a.x; lab[w][1] = a.y; lab[w][2] = b.x; lab[w][3] = b.y;
+                const ulonglong2* p = reinterpret_cast<const ulonglong2*>(a.labels + (size_t)w * a.npad + row);
+                const ulonglong2 x = p[0], y = p[1];
+                lab[w][0] = x.x; lab[w][1] = x.y; lab[w][2] = y.x; lab[w][3] = y.y;
             }
-            uint4 t4 = *reinterpret_cast<const uint4*>(taints + row);
+            const uint4 t4 = *reinterpret_cast<const uint4*>(a.taints + row);
             tn[0] = t4.x; tn[1] = t4.y; tn[2] = t4.z; tn[3] = t4.w;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                uint4 f4 = *reinterpret_cast<const uint4*>(freer + (size_t)r * npad + row);
+                const uint4 f4 = *reinterpret_cast<const uint4*>(a.freer + (size_t)r * a.npad + row);
                 fr[r][0] = f4.x; fr[r][1] = f4.y; fr[r][2] = f4.z; fr[r][3] = f4.w;
             }
-            int4 e4 = *reinterpret_cast<const int4*>(excl + row);
+            const int4 e4 = *reinterpret_cast<const int4*>(a.excl + row);
             ex[0] = e4.x; ex[1] = e4.y; ex[2] = e4.z; ex[3] = e4.w;
-            const uint32_t o = 4u * tid;
-#pragma unroll
-            for (int i = 0; i < 4; ++i) { ms[i] = s_start[o + i]; me[i] = s_end[o + i]; }
         } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -123,27 +136,26 @@ __global__ __launch_bounds__(kTallyThreads) void tally_kernel(
                 ex[i] = -1;
             }
         }
-        bool has_bnd = false;
+        bool valid[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) has_bnd = has_bnd || ms[i] >= 0 || me[i] >= 0;
+        for (int i = 0; i < 4; ++i) valid[i] = any && (row + i >= r0) && (row + i < r1);
+        __syncthreads();  // s_cls / s_ls / s_acc ready (first chunk); previous leaf pass done (later ones)
 
-        // pass 1: per-value wave scans; boundary rows fold their in-wave prefix
+        // ---- row pass: per value, evaluate 4 rows, scan, store row prefixes
         for (int c = 0; c < nv; ++c) {
             uint32_t v[4];
-            if (c < (int)nc) {
-                const DevClass& k = cls[c0 + c];
+            if (c < nc) {
+                const DevClass& k = s_cls[c];
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
-                    bool ok = valid[i];
+                    bool ok = valid[i] & ((tn[i] & k.tol_inv) == 0);
 #pragma unroll
-                    for (int w = 0; w < W; ++w)
-                        ok = ok && ((lab[w][i] & k.req[w]) == k.req[w]) && ((lab[w][i] & k.forbid[w]) == 0);
-                    ok = ok && ((tn[i] & ~k.tol) == 0);
+                    for (int w = 0; w < W; ++w) ok = ok & ((lab[w][i] & k.mask[w]) == k.req[w]);
                     uint32_t cap = k.pods;
 #pragma unroll
                     for (int r = 0; r < R; ++r)
-                        if (k.res[r] != 0) {
-                            uint32_t q = fit_count(fr[r][i], k.res[r], k.rcp[r], k.pods);
+                        if (k.res[r] != 0) {  // wave-uniform
+                            const uint32_t q = div_invariant(fr[r][i], k.magic[r], k.shift[r]);
                             cap = q < cap ? q : cap;
                         }
                     v[i] = ok ? cap : 0u;
@@ -154,52 +166,67 @@ __global__ __launch_bounds__(kTallyThreads) void tally_kernel(
             }
             const uint32_t p0 = v[0], p1 = p0 + v[1], p2 = p1 + v[2], p3 = p2 + v[3];
             const uint32_t incl = wave_incl_scan(p3, lane);
-            const uint32_t wex = incl - p3;  // exclusive prefix of this lane inside the wave
+            const uint32_t wex = incl - p3;
+            reinterpret_cast<uint4*>(s_pre + c * kChunkRows)[tid] = make_uint4(wex + p0, wex + p1, wex + p2, incl);
             if (lane == 63) s_wsum[c * kTallyWaves + wid] = incl;
-            if (has_bnd) {
-                const uint32_t pex[4] = {0u, p0, p1, p2};
-                const uint32_t pin[4] = {p0, p1, p2, p3};
-                uint32_t* acc = s_acc + c * kMaxBlkLeaves;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (ms[i] >= 0) atomicSub(&acc[ms[i]], wex + pex[i]);
-                    if (me[i] >= 0) atomicAdd(&acc[me[i]], wex + pin[i]);
-                }
-            }
         }
         __syncthreads();
-        // pass 2: add the workgroup-level offset (earlier waves + earlier chunks)
-        if (has_bnd) {
+
+        // ---- leaf pass: one thread per leaf folds its rows of this chunk
+        for (uint32_t li = tid; li < nl; li += kTallyThreads) {
+            const uint32_t s = s_ls[li], e = s_ls[li + 1];
+            const uint32_t lo = s > base ? s : base;
+            const uint32_t hi = e < base + kChunkRows ? e : base + kChunkRows;
+            if (lo >= hi) continue;
+            const uint32_t xl = lo - base, xh = hi - 1 - base;  // chunk-local first / last row
+            const uint32_t wl = xl >> 8, wh = xh >> 8;           // their waves (256 rows per wave)
             for (int c = 0; c < nv; ++c) {
-                uint32_t off = s_carry[c];
-                for (int w = 0; w < wid; ++w) off += s_wsum[c * kTallyWaves + w];
-                uint32_t* acc = s_acc + c * kMaxBlkLeaves;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if (ms[i] >= 0) atomicSub(&acc[ms[i]], off);
-                    if (me[i] >= 0) atomicAdd(&acc[me[i]], off);
+                const uint32_t* pre = s_pre + c * kChunkRows;
+                const uint32_t* ws = s_wsum + c * kTallyWaves;
+                uint32_t hi_p = pre[xh], lo_p = xl > 0 ? pre[xl - 1] : 0u;
+                for (uint32_t w = 0; w < wh; ++w) hi_p += ws[w];
+                if (xl > 0) {
+                    const uint32_t wlo = (xl - 1) >> 8;
+                    for (uint32_t w = 0; w < wlo; ++w) lo_p += ws[w];
                 }
+                (void)wl;
+                s_acc[c * kMaxBlkLeaves + li] += hi_p - lo_p;
             }
         }
-        __syncthreads();
-        if (tid < nv) {
-            uint32_t t = s_carry[tid];
-            for (int w = 0; w < kTallyWaves; ++w) t += s_wsum[tid * kTallyWaves + w];
-            s_carry[tid] = t;
-        }
-        // the next chunk's first barrier orders this update before any read
     }
     __syncthreads();
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
-        const uint32_t leaf = leaf_base + l0 + li;
-        for (int c = 0; c < (int)nc; ++c) cap_out[(size_t)(c0 + c) * ld + leaf] = s_acc[c * kMaxBlkLeaves + li];
-        if (do_occ) occ_out[leaf] = s_acc[nc * kMaxBlkLeaves + li];
+        const uint32_t leaf = a.leaf_base + l0 + li;
+        for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * kMaxBlkLeaves + li];
+        if (a.do_occ) a.occ_out[leaf] = s_acc[nc * kMaxBlkLeaves + li];
     }
 }
 
-// ----------------------------------------------------------------- feasibility bitmap
-// One wave per 64-domain word of one class. Bit d of class c's bitmap:
-// capsum(c, d) >= pods[c] && occsum(d) == 0 over the leaves of d at level[c].
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void tally_kernel(TallyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    tally_block<W, R>(a, blockIdx.x, lds);
+}
+
+// ----------------------------------------------------------------- feasibility
+// Bit d of class c's word w: capsum(c, d) >= pods[c] && occsum(d) == 0 over the
+// leaves of domain d = 64w + lane at level lvl. One wave computes one word.
+__device__ __forceinline__ uint64_t feas_word(const uint32_t* __restrict__ cap, const uint32_t* __restrict__ occ,
+                                              uint32_t ld, uint32_t lvl, uint32_t pods, uint32_t c, uint32_t w,
+                                              const TopoDev& topo, int lane) {
+    const uint32_t d = w * 64 + lane;
+    bool ok = false;
+    if (d < topo.D[lvl]) {
+        uint32_t lo = d, hi = d + 1;
+        if (lvl + 1 < topo.K) { lo = topo.fl[lvl][d]; hi = topo.fl[lvl][d + 1]; }
+        uint64_t cs = 0, os = 0;
+        const uint32_t* cp = cap + (size_t)c * ld;
+        for (uint32_t leaf = lo; leaf < hi; ++leaf) { cs += cp[leaf]; os += occ[leaf]; }
+        ok = (cs >= pods) && (os == 0);
+    }
+    return __ballot(ok);
+}
+
 __global__ __launch_bounds__(256) void feas_kernel(const uint32_t* __restrict__ cap,
                                                    const uint32_t* __restrict__ occ, uint32_t ld,
                                                    const DevClass* __restrict__ cls, uint32_t C,
@@ -210,28 +237,11 @@ __global__ __launch_bounds__(256) void feas_kernel(const uint32_t* __restrict__ 
     if (gw >= word_off[C]) return;
     uint32_t c = 0;
     while (word_off[c + 1] <= gw) ++c;  // wave-uniform, C <= 64
-    const uint32_t w = gw - word_off[c];
-    const uint32_t k = cls[c].level;
-    const uint32_t d = w * 64 + lane;
-    bool ok = false;
-    if (d < topo.D[k]) {
-        uint32_t a = d, b = d + 1;
-        if (k + 1 < topo.K) { a = topo.fl[k][d]; b = topo.fl[k][d + 1]; }
-        uint64_t cs = 0, os = 0;
-        const uint32_t* cp = cap + (size_t)c * ld;
-        for (uint32_t leaf = a; leaf < b; ++leaf) { cs += cp[leaf]; os += occ[leaf]; }
-        ok = (cs >= cls[c].pods) && (os == 0);
-    }
-    const uint64_t word = __ballot(ok);
+    const uint64_t word = feas_word(cap, occ, ld, cls[c].level, cls[c].pods, c, gw - word_off[c], topo, lane);
     if (lane == 0) feas[gw] = word;
 }
 
-// ----------------------------------------------------------------- A7 assignment
-// Single workgroup of kAssignThreads. Jobs are walked in global order as runs
-// of equal class; within a run the jobs take the first `len` available
-// domains (feasible for the class, not yet taken) at or after the class's
-// cursor, found with a block-wide prefix sum of word popcounts. Taking a
-// domain marks it, its ancestors and its descendants taken (LDS bitmaps).
+// ----------------------------------------------------------------- A7 assignment (one workgroup)
 __device__ __forceinline__ void lds_set_bit(uint64_t* t, uint32_t d) {
     atomicOr(reinterpret_cast<unsigned long long*>(&t[d >> 6]), 1ull << (d & 63));
 }
@@ -246,112 +256,317 @@ __device__ void lds_set_range(uint64_t* t, uint32_t lo, uint32_t hi) {
     }
 }
 
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total, int tid) {
-    const int lane = tid & 63, wid = tid >> 6;
+template <int NT>
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t incl = wave_incl_scan(x, lane);
     if (lane == 63) s_w[wid] = incl;
     __syncthreads();
     if (wid == 0) {
-        uint32_t v = lane < kAssignWaves ? s_w[lane] : 0u;
-        uint32_t s = wave_incl_scan(v, lane);
-        if (lane < kAssignWaves) s_w[kAssignWaves + lane] = s - v;  // exclusive
-        if (lane == kAssignWaves - 1) s_w[2 * kAssignWaves] = s;
+        const uint32_t v = lane < NW ? s_w[lane] : 0u;
+        const uint32_t s = wave_incl_scan(v, lane);
+        if (lane < NW) s_w[NW + lane] = s - v;  // exclusive
+        if (lane == NW - 1) s_w[2 * NW] = s;
     }
     __syncthreads();
-    *total = s_w[2 * kAssignWaves];
-    return s_w[kAssignWaves + wid] + incl - x;
+    *total = s_w[2 * NW];
+    return s_w[NW + wid] + incl - x;
+}
+
+// Small LDS tables of the assignment (all filled in one round of loads):
+// per class its level, pods, bitmap word offset and cursor; per level the
+// offset of its taken bitmap (computed from topo.D, no memory).
+struct AssignMeta {
+    uint32_t* s_w;       // 2*NW + 4 (block scans)
+    uint32_t* s_misc;    // 4
+    uint32_t* s_cursor;  // kMaxClasses
+    uint32_t* s_lvl;     // kMaxClasses
+    uint32_t* s_pods;    // kMaxClasses
+    uint32_t* s_woff;    // kMaxClasses + 1
+    uint32_t* s_toff;    // 8
+    uint32_t* s_rc;      // NT run classes (tile)
+    uint32_t* s_ro;      // NT run job offsets (tile)
+};
+
+template <int NT>
+__device__ __forceinline__ AssignMeta carve_meta(uint32_t* s_small) {
+    constexpr int NW = NT / 64;
+    AssignMeta m;
+    m.s_w = s_small;
+    m.s_misc = m.s_w + 2 * NW + 4;
+    m.s_cursor = m.s_misc + 4;
+    m.s_lvl = m.s_cursor + kMaxClasses;
+    m.s_pods = m.s_lvl + kMaxClasses;
+    m.s_woff = m.s_pods + kMaxClasses;
+    m.s_toff = m.s_woff + kMaxClasses + 1;
+    m.s_rc = m.s_toff + 8;
+    m.s_ro = m.s_rc + NT;
+    return m;
+}
+
+// Issue every small-table load at once (no barrier inside: the caller's next
+// barrier publishes them).
+template <int NT>
+__device__ __forceinline__ void stage_meta(const AssignMeta& m, const DevClass* __restrict__ cls, uint32_t C,
+                                           const uint32_t* __restrict__ word_off, const TopoDev& topo) {
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < C; i += NT) {
+        m.s_cursor[i] = 0;
+        m.s_lvl[i] = cls[i].level;
+        m.s_pods[i] = cls[i].pods;
+    }
+    for (uint32_t i = tid; i <= C; i += NT) m.s_woff[i] = word_off[i];
+    if (tid == 0) {
+        uint32_t off = 0;
+        for (uint32_t k = 0; k < topo.K; ++k) {
+            m.s_toff[k] = off;
+            off += (topo.D[k] + 63) >> 6;
+        }
+        m.s_toff[topo.K] = off;
+    }
+}
+
+__device__ __forceinline__ uint32_t taken_words(const TopoDev& topo) {
+    uint32_t off = 0;
+    for (uint32_t k = 0; k < topo.K; ++k) off += (topo.D[k] + 63) >> 6;
+    return off;
+}
+
+// Runs walk. Requires stage_meta + a barrier first, and s_taken zeroed.
+template <int NT>
+__device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, const TopoDev& topo,
+                             const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
+                             uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
+                             uint64_t* s_taken, const AssignMeta& m) {
+    const int tid = threadIdx.x;
+    uint32_t placed = 0, jbase = 0;
+    for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
+        // ---- a tile of runs and their job offsets (block scan of run lengths)
+        const uint32_t ri = r0 + tid;
+        const uint32_t len = ri < n_runs ? run_len[ri] : 0u;
+        m.s_rc[tid] = ri < n_runs ? run_class[ri] : 0u;
+        uint32_t tile_total;
+        const uint32_t off = block_excl_scan<NT>(len, m.s_w, &tile_total);
+        m.s_ro[tid] = off;
+        __syncthreads();
+        const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
+        for (uint32_t t = 0; t < nr; ++t) {
+            const uint32_t c = m.s_rc[t];
+            const uint32_t j0 = jbase + m.s_ro[t];
+            uint32_t jend = (t + 1 < nr) ? jbase + m.s_ro[t + 1] : jbase + tile_total;
+            if (jend > J) jend = J;
+            if (j0 >= jend) continue;
+            if (c >= C) {  // malformed run: its jobs are unplaceable
+                for (uint32_t j = j0 + tid; j < jend; j += NT) assign[j] = -1;
+                continue;
+            }
+            const uint32_t lvl = m.s_lvl[c];
+            const uint32_t D = topo.D[lvl];
+            const uint32_t nw = (D + 63) >> 6;
+            uint64_t* Tk = s_taken + m.s_toff[lvl];
+            const uint64_t* F = feas + m.s_woff[c];
+            uint32_t need = jend - j0, jpos = j0;
+            uint32_t cur = m.s_cursor[c];
+            while (need > 0 && cur < D) {
+                const uint32_t w = (cur >> 6) + tid;
+                uint64_t bits = 0;
+                if (w < nw) {
+                    bits = F[w] & ~Tk[w];
+                    if (w == (cur >> 6)) bits &= ~0ull << (cur & 63);
+                }
+                uint32_t total;
+                const uint32_t pre = block_excl_scan<NT>((uint32_t)__popcll(bits), m.s_w, &total);
+                if (tid == 0) m.s_misc[0] = ((cur >> 6) + NT) * 64u;
+                __syncthreads();
+                if (bits && pre < need) {
+                    uint32_t r = pre;
+                    uint64_t took = 0;
+                    while (bits && r < need) {
+                        const uint32_t b = __builtin_ctzll(bits);
+                        bits &= bits - 1;
+                        const uint32_t d = w * 64 + b;
+                        assign[jpos + r] = (int32_t)d;
+                        took |= 1ull << b;
+                        uint32_t dd = d;  // ancestors
+                        for (int kk = (int)lvl - 1; kk >= 0; --kk) {
+                            dd = (uint32_t)topo.par[kk + 1][dd];
+                            lds_set_bit(s_taken + m.s_toff[kk], dd);
+                        }
+                        uint32_t lo = d, hi = d + 1;  // descendants
+                        for (uint32_t kk = lvl + 1; kk < topo.K; ++kk) {
+                            lo = topo.cs[kk - 1][lo];
+                            hi = topo.cs[kk - 1][hi];
+                            lds_set_range(s_taken + m.s_toff[kk], lo, hi);
+                        }
+                        ++r;
+                        if (r == need) m.s_misc[0] = d + 1;
+                    }
+                    atomicOr(reinterpret_cast<unsigned long long*>(&Tk[w]), (unsigned long long)took);
+                }
+                __syncthreads();
+                const uint32_t used = total < need ? total : need;
+                need -= used;
+                jpos += used;
+                placed += used;
+                cur = m.s_misc[0] < D ? m.s_misc[0] : D;
+                __syncthreads();
+            }
+            for (uint32_t j = jpos + tid; j < jend; j += NT) assign[j] = -1;
+            if (tid == 0) m.s_cursor[c] = cur;
+            __syncthreads();
+        }
+        jbase += tile_total;
+        __syncthreads();
+    }
+    if (tid == 0 && stats != nullptr) { stats[0] = n_runs; stats[1] = placed; }
 }
 
 __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
-    const uint64_t* __restrict__ feas, const uint32_t* __restrict__ word_off,
-    const DevClass* __restrict__ cls, uint32_t C, TopoDev topo, const uint32_t* __restrict__ t_off,
-    const uint32_t* __restrict__ job_class, uint32_t J, int32_t* __restrict__ assign,
-    uint32_t* __restrict__ stats) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_taken[];  // all levels, t_off[k] words each
-    __shared__ uint32_t s_cursor[kMaxClasses];
-    __shared__ uint32_t s_w[2 * kAssignWaves + 4];
-    __shared__ uint32_t s_runend, s_newcur;
-
-    const int tid = threadIdx.x;
-    for (uint32_t i = tid; i < t_off[topo.K]; i += kAssignThreads) s_taken[i] = 0;
-    for (uint32_t i = tid; i < C; i += kAssignThreads) s_cursor[i] = 0;
+    const uint64_t* __restrict__ feas, const uint32_t* __restrict__ word_off, const DevClass* __restrict__ cls,
+    uint32_t C, TopoDev topo, const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
+    uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];  // [taken][small]
+    const uint32_t tw = taken_words(topo);
+    const AssignMeta m = carve_meta<kAssignThreads>(reinterpret_cast<uint32_t*>(s_dyn + tw));
+    stage_meta<kAssignThreads>(m, cls, C, word_off, topo);
+    for (uint32_t i = threadIdx.x; i < tw; i += kAssignThreads) s_dyn[i] = 0;
     __syncthreads();
+    assign_block<kAssignThreads>(feas, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m);
+}
 
-    uint32_t runs = 0, placed = 0;
-    uint32_t j0 = 0;
-    while (j0 < J) {
-        const uint32_t c = job_class[j0];
-        // ---- end of the same-class run starting at j0
-        if (tid == 0) s_runend = J;
-        __syncthreads();
-        for (uint32_t base = j0 + 1; base < J; base += kAssignThreads) {
-            const uint32_t j = base + tid;
-            if (j < J && job_class[j] != c) atomicMin(&s_runend, j);
-            __syncthreads();
-            if (s_runend != J) break;
-        }
-        const uint32_t runend = s_runend;
-        ++runs;
-        const uint32_t k = cls[c].level;
-        const uint32_t D = topo.D[k];
-        const uint32_t nw = (D + 63) >> 6;
-        uint64_t* Tk = s_taken + t_off[k];
-        const uint64_t* F = feas + word_off[c];
-        uint32_t need = runend - j0;
-        uint32_t jpos = j0;
-        uint32_t cur = s_cursor[c];
-        while (need > 0 && cur < D) {
-            const uint32_t w = (cur >> 6) + tid;
-            uint64_t bits = 0;
-            if (w < nw) {
-                bits = F[w] & ~Tk[w];
-                if (w == (cur >> 6)) bits &= ~0ull << (cur & 63);
-            }
-            uint32_t total;
-            const uint32_t pre = block_excl_scan((uint32_t)__popcll(bits), s_w, &total, tid);
-            if (tid == 0) s_newcur = ((cur >> 6) + kAssignThreads) * 64u;
-            __syncthreads();
-            if (bits && pre < need) {
-                uint32_t r = pre;
-                uint64_t took = 0;
-                while (bits && r < need) {
-                    const uint32_t b = __builtin_ctzll(bits);
-                    bits &= bits - 1;
-                    const uint32_t d = w * 64 + b;
-                    assign[jpos + r] = (int32_t)d;
-                    took |= 1ull << b;
-                    // ancestors
-                    uint32_t dd = d;
-                    for (int kk = (int)k - 1; kk >= 0; --kk) {
-                        dd = (uint32_t)topo.par[kk + 1][dd];
-                        lds_set_bit(s_taken + t_off[kk], dd);
-                    }
-                    // descendants
-                    uint32_t lo = d, hi = d + 1;
-                    for (uint32_t kk = k + 1; kk < topo.K; ++kk) {
-                        lo = topo.cs[kk - 1][lo];
-                        hi = topo.cs[kk - 1][hi];
-                        lds_set_range(s_taken + t_off[kk], lo, hi);
-                    }
-                    ++r;
-                    if (r == need) s_newcur = d + 1;
-                }
-                atomicOr(reinterpret_cast<unsigned long long*>(&Tk[w]), (unsigned long long)took);
-            }
-            __syncthreads();
-            const uint32_t used = total < need ? total : need;
-            need -= used;
-            jpos += used;
-            placed += used;
-            cur = s_newcur < D ? s_newcur : D;
-            __syncthreads();
-        }
-        for (uint32_t j = jpos + tid; j < runend; j += kAssignThreads) assign[j] = -1;
-        if (tid == 0) s_cursor[c] = cur;
-        __syncthreads();
-        j0 = runend;
+// ----------------------------------------------------------------- fused small-snapshot placement
+// Tally workgroups publish their leaf sums (plain stores, every wave drains
+// vmcnt, workgroup barrier, one lane: agent release fence, drain, relaxed agent
+// ticket add). The workgroup that draws the last ticket of this launch
+// acquires (agent fence + drain + barrier), builds every class's feasibility
+// bitmap in LDS and runs the assignment (cdna_hip_programming.md §6 G16).
+// The 64-bit ticket is zeroed at snapshot upload and only ever grows by
+// n_blocks per launch, so "last" = (old + 1) % n_blocks == 0.
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a, FusedArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    tally_block<W, R>(a, blockIdx.x, lds);
+
+    // publish
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t* s_flag = lds + tally_lds_words((int)a.nc + a.do_occ);
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long old =
+            __hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = ((old + 1) % a.n_blocks) == 0 ? 1u : 0u;
     }
-    if (tid == 0 && stats != nullptr) { stats[0] = runs; stats[1] = placed; }
+    __syncthreads();
+    if (*s_flag == 0) return;
+    // the tail: small tables first (independent of the other workgroups' sums)
+    uint64_t* s_taken = reinterpret_cast<uint64_t*>(lds);
+    uint64_t* s_feas = s_taken + f.t_words;
+    const AssignMeta m = carve_meta<kTallyThreads>(reinterpret_cast<uint32_t*>(s_feas + f.feas_words));
+    stage_meta<kTallyThreads>(m, a.cls, f.C, f.word_off, f.topo);
+    for (uint32_t i = threadIdx.x; i < f.t_words; i += kTallyThreads) s_taken[i] = 0;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    // feasibility bitmaps of every class into LDS
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (uint32_t gw = wid; gw < f.feas_words; gw += kTallyWaves) {
+        uint32_t c = 0;
+        while (m.s_woff[c + 1] <= gw) ++c;
+        const uint64_t word = feas_word(a.cap_out, a.occ_out, a.ld, m.s_lvl[c], m.s_pods[c], c, gw - m.s_woff[c],
+                                        f.topo, lane);
+        if (lane == 0) s_feas[gw] = word;
+    }
+    __syncthreads();
+    assign_block<kTallyThreads>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign, f.stats,
+                                s_taken, m);
+}
+
+// ----------------------------------------------------------------- single-class compaction
+// When the engine holds one class and it sits at the leaf level, the greedy is
+// a stream compaction: job j gets the j-th feasible leaf. Each workgroup
+// tallies its leaves, counts its feasible ones, and learns how many feasible
+// leaves precede it by a decoupled look-back over 8-byte {epoch|status, value}
+// granules (sc1 stores / loads: the data is the flag, G16 R2). Tile order comes
+// from a ticket, so a workgroup only ever waits on tiles that already started.
+constexpr uint32_t kAggregate = 1, kPrefix = 2;
+static_assert(kMaxBlkLeaves <= kTallyThreads, "compaction keeps one leaf per thread");
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoch, uint32_t status, uint32_t v) {
+    const unsigned long long x = ((unsigned long long)((epoch << 2) | status) << 32) | v;
+    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs a, CompactArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* s_x = lds + tally_lds_words(2);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
+    const int tid = threadIdx.x, lane = tid & 63;
+    const uint32_t epoch = f.epoch;  // host launch counter, 30-bit, never 0
+    uint32_t tile = blockIdx.x;
+    if (!f.coresident) {  // more tiles than resident slots: take tiles in start order
+        if (tid == 0)
+            s_x[0] = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
+                                a.n_blocks);
+        __syncthreads();
+        tile = s_x[0];
+    }
+    tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+
+    const uint32_t* s_acc = lds + tally_acc_off();
+    const uint4 bt = a.blk[tile];
+    const uint32_t l0 = bt.x, nl = bt.y - bt.x;
+    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= f.pods && s_acc[kMaxBlkLeaves + tid] == 0;
+    uint32_t total;
+    const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
+    unsigned long long* g = f.granules;
+    if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total);
+    if (tid < 64) {  // wave 0: look back
+        uint32_t prefix = 0, spins = 0;
+        bool timeout = false;
+        for (int p = (int)tile - 1; p >= 0; p -= 64) {
+            const int idx = p - lane;
+            uint32_t st = 0, v = 0;
+            while (true) {
+                if (idx >= 0) {
+                    const unsigned long long x = __hip_atomic_load(g + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t tag = (uint32_t)(x >> 32);
+                    st = (tag >> 2) == epoch ? (tag & 3u) : 0u;
+                    v = (uint32_t)x;
+                }
+                if (__all(idx < 0 || st != 0)) break;
+                if (++spins > (1u << 22)) { timeout = true; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            const unsigned long long pm = __ballot(idx >= 0 && st == kPrefix);
+            const int stop = pm ? __builtin_ctzll(pm) : 64;
+            uint32_t x = (idx >= 0 && lane <= stop) ? v : 0u;
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off, 64);
+            prefix += x;
+            if (pm || timeout) break;
+        }
+        if (lane == 0) {
+            if (tile != 0) put_granule(g + tile, epoch, kPrefix, prefix + total);
+            s_x[2] = prefix;
+            s_x[3] = timeout ? 1u : 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t prefix = s_x[2];
+    if (ok && prefix + rank < f.J) f.assign[prefix + rank] = (int32_t)(a.leaf_base + l0 + tid);
+    if (tile + 1 == a.n_blocks) {
+        const uint32_t placed = prefix + total < f.J ? prefix + total : f.J;
+        for (uint32_t j = placed + tid; j < f.J; j += kTallyThreads) f.assign[j] = -1;
+        if (tid == 0 && f.stats) {
+            f.stats[0] = f.n_runs;
+            f.stats[1] = placed;
+            f.stats[2] = s_x[3];
+        }
+    }
 }
 
 // ----------------------------------------------------------------- A5 / A9 batch kernels
@@ -369,7 +584,6 @@ __device__ __forceinline__ int32_t row_domain(int32_t row, uint32_t level, uint3
                                               const uint32_t* leaf_start, uint32_t n_leaves,
                                               uint32_t leaf_base, const TopoDev& topo) {
     if (row < 0 || (uint32_t)row >= n_rows || level >= topo.K) return -1;
-    // leaf: last l with leaf_start[l] <= row (leaf_start has n_leaves+1 entries)
     const uint32_t l = upper_bound_u32(leaf_start, n_leaves + 1, (uint32_t)row) - 1 + leaf_base;
     if (level + 1 == topo.K) return (int32_t)l;
     return (int32_t)(upper_bound_u32(topo.fl[level], topo.D[level] + 1, l) - 1);
@@ -420,41 +634,68 @@ __global__ void patch_kernel(const uint32_t* __restrict__ rows, uint32_t n, uint
     if (dexcl) excl[row] = dexcl[i];
 }
 
-hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
-                        const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
-                        uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, n, npad, W, R, dlab, dtaint,
-                       dfree, dexcl, labels, taints, freer, excl);
-    return hipGetLastError();
-}
-
 // ----------------------------------------------------------------- launchers
 template <int W, int R>
 static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((tally_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads), 0, s, a.labels, a.taints,
-                       a.freer, a.excl, a.npad, a.leaf_start, a.blk_leaf, a.cls, a.c0, a.nc, a.do_occ,
-                       a.cap_out, a.occ_out, a.ld, a.leaf_base);
+    hipLaunchKernelGGL((tally_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
+                       sizeof(uint32_t) * tally_lds_words((int)a.nc + a.do_occ), s, a);
     return hipGetLastError();
 }
 
-template <int W>
-static hipError_t launch_tally_w(const TallyArgs& a, hipStream_t s) {
-    switch (a.R) {
-        case 1: return launch_tally_wr<W, 1>(a, s);
-        case 2: return launch_tally_wr<W, 2>(a, s);
-        case 3: return launch_tally_wr<W, 3>(a, s);
-        default: return launch_tally_wr<W, 4>(a, s);
-    }
+template <int W, int R>
+static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
+    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads), f.lds_bytes, s, a, f);
+    return hipGetLastError();
 }
 
-hipError_t launch_tally(const TallyArgs& a, hipStream_t s) {
-    switch (a.W) {
-        case 1: return launch_tally_w<1>(a, s);
-        case 2: return launch_tally_w<2>(a, s);
-        case 3: return launch_tally_w<3>(a, s);
-        default: return launch_tally_w<4>(a, s);
+template <int W, int R>
+static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
+    hipLaunchKernelGGL((place_compact_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
+                       compact_lds_bytes(), s, a, f);
+    return hipGetLastError();
+}
+
+#define JSP_DISPATCH_WR(FN, ...)              \
+    switch (a.W * 8 + a.R) {                  \
+        case 9: return FN<1, 1>(__VA_ARGS__); \
+        case 10: return FN<1, 2>(__VA_ARGS__); \
+        case 11: return FN<1, 3>(__VA_ARGS__); \
+        case 12: return FN<1, 4>(__VA_ARGS__); \
+        case 17: return FN<2, 1>(__VA_ARGS__); \
+        case 18: return FN<2, 2>(__VA_ARGS__); \
+        case 19: return FN<2, 3>(__VA_ARGS__); \
+        case 20: return FN<2, 4>(__VA_ARGS__); \
+        case 25: return FN<3, 1>(__VA_ARGS__); \
+        case 26: return FN<3, 2>(__VA_ARGS__); \
+        case 27: return FN<3, 3>(__VA_ARGS__); \
+        case 28: return FN<3, 4>(__VA_ARGS__); \
+        case 33: return FN<4, 1>(__VA_ARGS__); \
+        case 34: return FN<4, 2>(__VA_ARGS__); \
+        case 35: return FN<4, 3>(__VA_ARGS__); \
+        case 36: return FN<4, 4>(__VA_ARGS__); \
+        default: return hipErrorInvalidValue; \
     }
+
+hipError_t launch_tally(const TallyArgs& a, hipStream_t s) { JSP_DISPATCH_WR(launch_tally_wr, a, s) }
+
+hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_fused_wr, a, f, s)
+}
+
+hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_compact_wr, a, f, s)
+}
+
+size_t compact_lds_bytes() { return sizeof(uint32_t) * (tally_lds_words(2) + 4 + 2 * kTallyWaves + 8); }
+
+size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv) {
+    const size_t tail = (size_t)(t_words + feas_words) * 8 + sizeof(uint32_t) * assign_small_words(kTallyThreads);
+    const size_t head = sizeof(uint32_t) * (tally_lds_words((int)nv) + 4);
+    return ((tail > head ? tail : head) + 15) & ~size_t(15);
+}
+
+size_t assign_lds_bytes(uint32_t t_words) {
+    return (size_t)t_words * 8 + sizeof(uint32_t) * assign_small_words(kAssignThreads);
 }
 
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
@@ -467,10 +708,10 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
 }
 
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
-                         const TopoDev& topo, const uint32_t* t_off, uint32_t t_words, const uint32_t* job_class,
-                         uint32_t J, int32_t* assign, uint32_t* stats, hipStream_t s) {
-    hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), (size_t)t_words * 8, s, feas, word_off, cls,
-                       C, topo, t_off, job_class, J, assign, stats);
+                         const TopoDev& topo, uint32_t t_words, const uint32_t* run_class, const uint32_t* run_len,
+                         uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats, hipStream_t s) {
+    hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), assign_lds_bytes(t_words), s, feas, word_off,
+                       cls, C, topo, run_class, run_len, n_runs, J, assign, stats);
     return hipGetLastError();
 }
 
@@ -489,6 +730,15 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
     if (n_jobs == 0) return hipSuccess;
     hipLaunchKernelGGL(audit_kernel, dim3((n_jobs + 3) / 4), dim3(256), 0, s, leader_rows, levels, foff, fdom,
                        n_jobs, n_rows, leaf_start, n_leaves, leaf_base, topo, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
+                        const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
+                        uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, n, npad, W, R, dlab, dtaint,
+                       dfree, dexcl, labels, taints, freer, excl);
     return hipGetLastError();
 }
 

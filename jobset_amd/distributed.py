@@ -20,7 +20,7 @@ from typing import Callable, Optional
 
 import numpy as np
 
-from .snapshot import Problem, shard_problem
+from .snapshot import Problem, job_runs, shard_problem
 
 
 def barrier(world: int) -> None:
@@ -64,7 +64,10 @@ class ShardedPlacement:
         self.C, self.L = C, L
         self.local = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
         self.reduced = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
-        self.jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+        rc, rl = job_runs(p.job_class)
+        self.n_runs = int(rc.shape[0])
+        self.rc = torch.from_numpy(rc.astype(np.int32)).cuda()
+        self.rl = torch.from_numpy(rl.astype(np.int32)).cuda()
         self.out = torch.empty(max(p.n_jobs, 1), dtype=torch.int32, device="cuda")
         self._ev = []
 
@@ -72,7 +75,8 @@ class ShardedPlacement:
         import torch
         J = self.p.n_jobs
         if self.world == 1:
-            self.engine.place_device(self.jc.data_ptr(), J, self.out.data_ptr(), self.stream)
+            self.engine.place_device(self.rc.data_ptr(), self.rl.data_ptr(), self.n_runs, J, self.out.data_ptr(),
+                                     self.stream)
             return
         L = self.L
         self.engine.tally_device(self.local.data_ptr(), self.local[self.C].data_ptr(), L, self.stream)
@@ -84,8 +88,8 @@ class ShardedPlacement:
             self._ev.append((a, b))
         else:
             reduce_tallies(self.local, self.reduced, self.group)
-        self.engine.assign_device(self.reduced.data_ptr(), self.reduced[self.C].data_ptr(), L, self.jc.data_ptr(),
-                                  J, self.out.data_ptr(), self.stream)
+        self.engine.assign_device(self.reduced.data_ptr(), self.reduced[self.C].data_ptr(), L, self.rc.data_ptr(),
+                                  self.rl.data_ptr(), self.n_runs, J, self.out.data_ptr(), self.stream)
 
     def assign(self) -> np.ndarray:
         return self.out[:self.p.n_jobs].cpu().numpy()

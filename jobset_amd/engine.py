@@ -18,7 +18,7 @@ import numpy as np
 
 from . import native
 from .native import JspJobClass, JspNodes, JspStats, JspTiming, JspTopology, check
-from .snapshot import JobClass, Nodes, Problem, Topology
+from .snapshot import JobClass, Nodes, Problem, Topology, job_runs
 
 
 def _p(a: Optional[np.ndarray]) -> Optional[int]:
@@ -33,6 +33,7 @@ class PlaceResult:
     placed: int
     runs: int
     wall_us: float
+    fused: int = 0               # launch shape: 0 three launches, 1 fused tail, 2 one-class compaction
 
 
 class Engine:
@@ -131,28 +132,51 @@ class Engine:
         self.upload_classes(p.classes)
 
     # ---------------------------------------------------------------- placement
-    def place(self, job_class: np.ndarray, want_tally: bool = False) -> PlaceResult:
-        jc = np.ascontiguousarray(job_class, dtype=np.uint32)
-        J = jc.shape[0]
-        L = self.topology.n_leaves
+    def place_runs(self, run_class: np.ndarray, run_len: np.ndarray, want_tally: bool = False) -> PlaceResult:
+        """Jobs as replicated-job runs in global order: run i = run_len[i] jobs of
+        class run_class[i] (a ReplicatedJob's replicas share one template)."""
+        rc = np.ascontiguousarray(run_class, dtype=np.uint32)
+        rl = np.ascontiguousarray(run_len, dtype=np.uint32)
+        J = int(rl.astype(np.int64).sum())
+        L = self.topology.n_leaves if self.topology is not None else 0
         assign = np.empty(max(J, 1), dtype=np.int32)
         cap = np.empty((max(self.n_classes, 1), max(L, 1)), dtype=np.uint32) if want_tally else None
         occ = np.empty(max(L, 1), dtype=np.uint32) if want_tally else None
         st = JspStats()
-        check(self._lib.jsp_place(self._h, _p(jc), J, _p(assign), _p(cap), _p(occ), ctypes.byref(st)))
+        check(self._lib.jsp_place(self._h, _p(rc), _p(rl), rc.shape[0], _p(assign), _p(cap), _p(occ),
+                                  ctypes.byref(st)))
         return PlaceResult(assign=assign[:J], cap=None if cap is None else cap[:self.n_classes, :L],
                            occ=None if occ is None else occ[:L], placed=st.placed, runs=st.runs,
-                           wall_us=st.wall_us)
+                           wall_us=st.wall_us, fused=int(st.fused))
 
-    def place_device(self, d_job_class: int, n_jobs: int, d_assign: int, stream: Optional[int] = None) -> None:
-        check(self._lib.jsp_place_device(self._h, d_job_class, n_jobs, d_assign, stream))
+    def place(self, job_class: np.ndarray, want_tally: bool = False) -> PlaceResult:
+        """One class id per job (global order); run-length encoded in the library."""
+        jc = np.ascontiguousarray(job_class, dtype=np.uint32)
+        J = jc.shape[0]
+        L = self.topology.n_leaves if self.topology is not None else 0
+        assign = np.empty(max(J, 1), dtype=np.int32)
+        cap = np.empty((max(self.n_classes, 1), max(L, 1)), dtype=np.uint32) if want_tally else None
+        occ = np.empty(max(L, 1), dtype=np.uint32) if want_tally else None
+        st = JspStats()
+        check(self._lib.jsp_place_jobs(self._h, _p(jc), J, _p(assign), _p(cap), _p(occ), ctypes.byref(st)))
+        return PlaceResult(assign=assign[:J], cap=None if cap is None else cap[:self.n_classes, :L],
+                           occ=None if occ is None else occ[:L], placed=st.placed, runs=st.runs,
+                           wall_us=st.wall_us, fused=int(st.fused))
+
+    def place_device(self, d_run_class: int, d_run_len: int, n_runs: int, n_jobs: int, d_assign: int,
+                     stream: Optional[int] = None) -> None:
+        check(self._lib.jsp_place_device(self._h, d_run_class, d_run_len, n_runs, n_jobs, d_assign, stream))
 
     def tally_device(self, d_cap: int, d_occ: int, ld: int, stream: Optional[int] = None) -> None:
         check(self._lib.jsp_tally_device(self._h, d_cap, d_occ, ld, stream))
 
-    def assign_device(self, d_cap: int, d_occ: int, ld: int, d_job_class: int, n_jobs: int, d_assign: int,
-                      stream: Optional[int] = None) -> None:
-        check(self._lib.jsp_assign_device(self._h, d_cap, d_occ, ld, d_job_class, n_jobs, d_assign, stream))
+    def assign_device(self, d_cap: int, d_occ: int, ld: int, d_run_class: int, d_run_len: int, n_runs: int,
+                      n_jobs: int, d_assign: int, stream: Optional[int] = None) -> None:
+        check(self._lib.jsp_assign_device(self._h, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs,
+                                          d_assign, stream))
+
+    def set_fused(self, enable: bool) -> None:
+        check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
     # ---------------------------------------------------------------- webhook / reconciler batches
     def resolve_leader_domains(self, leader_rows: np.ndarray, levels: np.ndarray) -> np.ndarray:

@@ -37,12 +37,15 @@ class JspJobClass(ctypes.Structure):
 
 
 class JspStats(ctypes.Structure):
-    _fields_ = [("jobs", u32), ("placed", u32), ("runs", u32), ("reserved", u32), ("wall_us", ctypes.c_double)]
+    _fields_ = [("jobs", u32), ("placed", u32), ("runs", u32), ("fused", u32), ("wall_us", ctypes.c_double)]
 
 
 class JspTiming(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("tally_ms", ctypes.c_double), ("feas_ms", ctypes.c_double),
-                ("assign_ms", ctypes.c_double)]
+                ("assign_ms", ctypes.c_double), ("fused_ms", ctypes.c_double), ("fused_calls", ctypes.c_uint64)]
+
+
+JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
 
 
 # (name, restype, argtypes) — every entry point declared in include/jsplace.h
@@ -56,12 +59,14 @@ SIGNATURES = [
     ("jsp_snapshot_upload", ctypes.c_int, [vp, ctypes.POINTER(JspNodes)]),
     ("jsp_snapshot_patch", ctypes.c_int, [vp, vp, u32, vp, vp, vp, vp]),
     ("jsp_classes_upload", ctypes.c_int, [vp, ctypes.POINTER(JspJobClass), u32]),
-    ("jsp_place", ctypes.c_int, [vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
+    ("jsp_place", ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
+    ("jsp_place_jobs", ctypes.c_int, [vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
     ("jsp_tally_device", ctypes.c_int, [vp, vp, vp, u32, vp]),
-    ("jsp_assign_device", ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp]),
-    ("jsp_place_device", ctypes.c_int, [vp, vp, u32, vp, vp]),
+    ("jsp_assign_device", ctypes.c_int, [vp, vp, vp, u32, vp, vp, u32, u32, vp, vp]),
+    ("jsp_place_device", ctypes.c_int, [vp, vp, vp, u32, u32, vp, vp]),
     ("jsp_resolve_leader_domains", ctypes.c_int, [vp, vp, vp, u32, vp]),
     ("jsp_audit_placements", ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp]),
+    ("jsp_engine_set_fused", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
     ("jsp_engine_stream", vp, [vp]),

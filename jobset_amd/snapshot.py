@@ -190,6 +190,17 @@ class Dictionary:
         return words
 
 
+def job_runs(job_class: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Run-length encode a per-job class list into replicated-job runs
+    (run_class, run_len), preserving the global job order."""
+    jc = np.asarray(job_class, dtype=np.uint32)
+    if jc.shape[0] == 0:
+        return np.zeros(0, dtype=np.uint32), np.zeros(0, dtype=np.uint32)
+    starts = np.concatenate([[0], np.nonzero(jc[1:] != jc[:-1])[0] + 1])
+    lens = np.diff(np.concatenate([starts, [jc.shape[0]]]))
+    return jc[starts].astype(np.uint32), lens.astype(np.uint32)
+
+
 def shard_problem(p: Problem, rank: int, world: int) -> Nodes:
     """Domain-aligned node shard for `rank`: level-0 domains are
     split into `world` contiguous groups of about equal row count, so every

@@ -15,6 +15,15 @@ from oracle import oracle as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["fused", "three-launch"])
+def any_engine(request, engine):
+    """The session engine in both launch shapes (fused single launch where the
+    snapshot allows it, and tally -> feas -> assign)."""
+    engine.set_fused(request.param == "fused")
+    yield engine
+    engine.set_fused(True)
+
+
 def run_both(engine: Engine, p: Problem):
     engine.load(p)
     got = engine.place(p.job_class, want_tally=True)
@@ -30,9 +39,9 @@ def assert_same(got, a, cap, occ):
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3, 5])
-def test_config_parity(engine, cfg):
+def test_config_parity(any_engine, cfg):
     p = synth.CONFIGS[cfg]()
-    got, a, cap, occ = run_both(engine, p)
+    got, a, cap, occ = run_both(any_engine, p)
     assert_same(got, a, cap, occ)
     O.check_invariants(p, got.assign, got.cap, got.occ)
 
@@ -56,9 +65,9 @@ def test_config2_expected_shape(engine):
 
 
 @pytest.mark.parametrize("seed", range(120))
-def test_random_parity(engine, seed):
+def test_random_parity(any_engine, seed):
     p = synth.random_problem(seed)
-    got, a, cap, occ = run_both(engine, p)
+    got, a, cap, occ = run_both(any_engine, p)
     assert_same(got, a, cap, occ)
 
 
@@ -75,6 +84,46 @@ def test_trials_parity(engine):
         p = synth.config2(trial=t)
         got, a, cap, occ = run_both(engine, p)
         assert_same(got, a, cap, occ)
+        assert got.fused
+
+
+def test_fused_repeat_and_ticket(engine):
+    """The fused launch's last-arriver ticket survives many launches and
+    snapshot changes (block counts change between snapshots)."""
+    for cfg in (2, 1, 5, 2):
+        p = synth.CONFIGS[cfg]()
+        engine.load(p)
+        a = O.place_c(p)[0]
+        for _ in range(25):
+            got = engine.place(p.job_class)
+            np.testing.assert_array_equal(got.assign, a)
+            assert got.fused
+
+
+@pytest.mark.parametrize("jobs", [0, 1, 39_000, 60_000])
+def test_compaction_many_tiles(engine, jobs):
+    """One leaf-level class over 1M nodes: the single-launch compaction with a
+    look-back across ~1000 workgroups (multiple 64-tile windows), incl. more
+    jobs than feasible racks (the tail of assign[] must be -1)."""
+    p = synth.config4()
+    p.classes = [p.classes[0]]
+    p.job_class = np.zeros(jobs, dtype=np.uint32)
+    engine.load(p)
+    for _ in range(3):  # the epoch scheme across repeated launches
+        got = engine.place(p.job_class, want_tally=True)
+        assert got.fused == 2
+        a, cap, occ = O.place_c(p)
+        assert_same(got, a, cap, occ)
+
+
+def test_runs_api_equals_job_api(engine):
+    from jobset_amd.snapshot import job_runs
+    p = synth.config5()
+    engine.load(p)
+    rc, rl = job_runs(p.job_class)
+    got = engine.place_runs(rc, rl)
+    np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    assert got.runs == rc.shape[0]
 
 
 def _tiny(n_leaves=3, per=2, K=1):
@@ -210,11 +259,14 @@ def test_sharded_tally_allreduce_parity(engine):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(cap_sum.cpu().numpy().astype(np.uint32), cap_ref)
         np.testing.assert_array_equal(occ_sum.cpu().numpy().astype(np.uint32), occ_ref)
-        jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+        from jobset_amd.snapshot import job_runs
+        rc, rl = job_runs(p.job_class)
+        rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+        rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
         for e in engines:
             out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
-            e.assign_device(cap_sum.data_ptr(), occ_sum.data_ptr(), L, jc.data_ptr(), p.n_jobs, out.data_ptr(),
-                            torch.cuda.current_stream().cuda_stream)
+            e.assign_device(cap_sum.data_ptr(), occ_sum.data_ptr(), L, rct.data_ptr(), rlt.data_ptr(), rc.shape[0],
+                            p.n_jobs, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
             torch.cuda.synchronize()
             np.testing.assert_array_equal(out.cpu().numpy(), a_ref)
     finally:
@@ -226,9 +278,13 @@ def test_place_device_matches_host_api(engine):
     import torch
     p = synth.config3()
     engine.load(p)
-    jc = torch.from_numpy(p.job_class.astype(np.int32)).cuda()
+    from jobset_amd.snapshot import job_runs
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
     out = torch.full((p.n_jobs,), -7, dtype=torch.int32, device="cuda")
-    engine.place_device(jc.data_ptr(), p.n_jobs, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(out.cpu().numpy(), O.place_c(p)[0])
 
@@ -251,10 +307,12 @@ def test_resolve_and_audit(engine):
             leaf = leaf_of_row[r]
             exp.append(int(leaf) if k == 1 else int(zone_of_leaf[leaf]))
     np.testing.assert_array_equal(got, exp)
+    # followers per job: job0 3 matching; job1 none; job2 one wrong; job3 leader
+    # unknown; job4 none; job5 one matching + two wrong
     off = np.array([0, 3, 3, 5, 6, 6, 9], dtype=np.uint32)
-    fd = np.array([exp[0], exp[0], exp[0], 999, exp[2], 0, exp[4], 3, exp[4]], dtype=np.int32)
+    fd = np.array([exp[0], exp[0], exp[0], 999, exp[2], 0, exp[5], exp[5] + 1, -1], dtype=np.int32)
     bad = engine.audit_placements(rows, levels, off, fd)
-    np.testing.assert_array_equal(bad, [0, 0, 1, 0xFFFFFFFF, 0, 1])
+    np.testing.assert_array_equal(bad, [0, 0, 1, 0xFFFFFFFF, 0, 2])
 
 
 def test_error_paths(engine):
@@ -272,9 +330,15 @@ def test_error_paths(engine):
                        first_leaf=[np.array([0, 2, 3], dtype=np.uint32), np.arange(4, dtype=np.uint32)])
         bad.first_leaf[0] = np.array([0, 1, 3], dtype=np.uint32)
         e.upload_topology(bad)  # 1 and 3 are level-1 boundaries: nested, accepted
-        with pytest.raises(JspError) as ei:
-            e.upload_topology(Topology(level_keys=["a"], n_domains=[3],
-                                       first_leaf=[np.array([0, 2, 1, 3], dtype=np.uint32)]))
+        with pytest.raises(JspError) as ei:  # non-monotone coarse level
+            e.upload_topology(Topology(level_keys=["a", "b"], n_domains=[3, 3],
+                                       first_leaf=[np.array([0, 2, 1, 3], dtype=np.uint32),
+                                                   np.arange(4, dtype=np.uint32)]))
+        assert ei.value.code == JSP_EINVAL
+        with pytest.raises(JspError) as ei:  # level 0 boundary 2 is not a level-1 boundary
+            e.upload_topology(Topology(level_keys=["a", "b"], n_domains=[2, 2],
+                                       first_leaf=[np.array([0, 1, 4], dtype=np.uint32),
+                                                   np.array([0, 2, 4], dtype=np.uint32)]))
         assert ei.value.code == JSP_EINVAL
         with pytest.raises(JspError) as ei:
             e.upload_topology(Topology(level_keys=["a"], n_domains=[2_000_000],
