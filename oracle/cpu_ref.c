@@ -108,25 +108,23 @@ int jspo_tally(const jspo_problem* p, uint32_t* cap /*[C][L]*/, uint32_t* occ /*
     return 0;
 }
 
-/* Full placement. cap/occ may be NULL. Returns the number of placed jobs or
- * a negative value on allocation failure. */
-int jspo_place(const jspo_problem* p, int32_t* assign, uint32_t* cap_out, uint32_t* occ_out) {
+/* Assignment from per-(class, leaf) capacities and per-leaf occupancy (the
+ * multi-GPU path assigns from all-reduced tallies). Returns the number of
+ * placed jobs or a negative value on allocation failure. */
+int jspo_assign(const jspo_problem* p, const uint32_t* cap, const uint32_t* occ, int32_t* assign) {
     const uint32_t K = p->n_levels;
     const uint32_t L = p->n_domains[K - 1];
     const uint32_t C = p->n_classes;
-    uint32_t* cap = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)C * L + 1));
-    uint32_t* occ = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)L + 1));
     uint8_t* feas[64];
     uint8_t* taken[MAXL];
     uint32_t cursor[64];
     int placed = 0;
-    if (!cap || !occ) return -1;
-    jspo_tally(p, cap, occ);
     /* feasibility per class at its level */
     for (uint32_t c = 0; c < C; ++c) {
         uint32_t k = p->cls_level[c];
         uint32_t D = p->n_domains[k];
         feas[c] = (uint8_t*)calloc(D + 1, 1);
+        if (!feas[c]) return -1;
         cursor[c] = 0;
         for (uint32_t d = 0; d < D; ++d) {
             uint64_t cs = 0, os = 0;
@@ -137,7 +135,10 @@ int jspo_place(const jspo_problem* p, int32_t* assign, uint32_t* cap_out, uint32
             feas[c][d] = (cs >= p->cls_pods[c] && os == 0);
         }
     }
-    for (uint32_t k = 0; k < K; ++k) taken[k] = (uint8_t*)calloc(p->n_domains[k] + 1, 1);
+    for (uint32_t k = 0; k < K; ++k) {
+        taken[k] = (uint8_t*)calloc(p->n_domains[k] + 1, 1);
+        if (!taken[k]) return -1;
+    }
     /* Greedy in global job order. The per-class cursor only skips domains
      * that are infeasible for the class or already taken; both stay so for
      * the rest of the call, so the lowest available domain never lies behind
@@ -167,10 +168,24 @@ int jspo_place(const jspo_problem* p, int32_t* assign, uint32_t* cap_out, uint32
             }
         }
     }
-    if (cap_out) memcpy(cap_out, cap, sizeof(uint32_t) * (size_t)C * L);
-    if (occ_out) memcpy(occ_out, occ, sizeof(uint32_t) * L);
     for (uint32_t c = 0; c < C; ++c) free(feas[c]);
     for (uint32_t k = 0; k < K; ++k) free(taken[k]);
+    (void)L;
+    return placed;
+}
+
+/* Full placement. cap/occ may be NULL. Returns the number of placed jobs or
+ * a negative value on allocation failure. */
+int jspo_place(const jspo_problem* p, int32_t* assign, uint32_t* cap_out, uint32_t* occ_out) {
+    const uint32_t L = p->n_domains[p->n_levels - 1];
+    const uint32_t C = p->n_classes;
+    uint32_t* cap = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)C * L + 1));
+    uint32_t* occ = (uint32_t*)malloc(sizeof(uint32_t) * ((size_t)L + 1));
+    if (!cap || !occ) return -1;
+    jspo_tally(p, cap, occ);
+    int placed = jspo_assign(p, cap, occ, assign);
+    if (cap_out) memcpy(cap_out, cap, sizeof(uint32_t) * (size_t)C * L);
+    if (occ_out) memcpy(occ_out, occ, sizeof(uint32_t) * L);
     free(cap);
     free(occ);
     return placed;

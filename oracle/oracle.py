@@ -74,6 +74,8 @@ def lib():
         _lib.jspo_place.argtypes = [ctypes.POINTER(_Problem), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         _lib.jspo_tally.restype = ctypes.c_int
         _lib.jspo_tally.argtypes = [ctypes.POINTER(_Problem), ctypes.c_void_p, ctypes.c_void_p]
+        _lib.jspo_assign.restype = ctypes.c_int
+        _lib.jspo_assign.argtypes = [ctypes.POINTER(_Problem), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     return _lib
 
 
@@ -144,6 +146,34 @@ def place_c(p: Problem, packed: Optional[PackedProblem] = None) -> Tuple[np.ndar
     if rc < 0:
         raise MemoryError("oracle allocation failed")
     return assign[:pk.J], cap[:, :pk.L], occ[:pk.L]
+
+
+def tally_nodes(topology_leaves: int, nodes, classes) -> Tuple[np.ndarray, np.ndarray]:
+    """Per-(class, leaf) capacity and per-leaf occupancy of a (possibly
+    sharded) node set: the tally half of the rules, for the shard tests."""
+    from jobset_amd.snapshot import Problem, Topology
+    L = nodes.n_leaves
+    topo = Topology(level_keys=["leaf"], n_domains=[L], first_leaf=[np.arange(L + 1, dtype=np.uint32)])
+    flat = [type(c)(req_labels=c.req_labels, forbid_labels=c.forbid_labels, tolerated_taints=c.tolerated_taints,
+                    level=0, pods=c.pods, req_res=c.req_res) for c in classes]
+    from jobset_amd.snapshot import Nodes
+    n0 = Nodes(leaf_start=nodes.leaf_start, labels=nodes.labels, taints=nodes.taints, free=nodes.free,
+               excl=nodes.excl, leaf_begin=0)
+    pk = PackedProblem(Problem(topology=topo, nodes=n0, classes=flat, job_class=np.zeros(0, dtype=np.uint32)))
+    cap = np.empty((pk.C, max(L, 1)), dtype=np.uint32)
+    occ = np.empty(max(L, 1), dtype=np.uint32)
+    lib().jspo_tally(ctypes.byref(pk.st), _ptr(cap), _ptr(occ))
+    return cap[:, :L], occ[:L]
+
+
+def assign_from_tallies(p: Problem, cap: np.ndarray, occ: np.ndarray) -> np.ndarray:
+    pk = PackedProblem(p)
+    cap = np.ascontiguousarray(cap, dtype=np.uint32)
+    occ = np.ascontiguousarray(occ, dtype=np.uint32)
+    assign = np.empty(max(pk.J, 1), dtype=np.int32)
+    if lib().jspo_assign(ctypes.byref(pk.st), _ptr(cap), _ptr(occ), _ptr(assign)) < 0:
+        raise MemoryError("oracle allocation failed")
+    return assign[:pk.J]
 
 
 # ------------------------------------------------------------------ pure Python

@@ -346,3 +346,52 @@ def test_error_paths(engine):
         assert ei.value.code == JSP_ERANGE
     finally:
         e.close()
+
+
+def test_webhook_consults_engine_identically(engine):
+    """A5 rewired: with the cache bound to the engine, follower nodeSelector
+    values come from the resident snapshot (jsp_resolve_leader_domains) and
+    the mutation is identical to the reference's Node-Get path; the same for
+    the PodReconciler audit (A9)."""
+    from jobset_amd import host
+    p = synth.config5()
+    engine.load(p)
+    topo = p.topology
+    leaf_of_row = p.nodes.leaf_of_row()
+    zone_of_leaf = topo.parent_of_leaf(0)
+    names = [f"node-{r:05d}" for r in range(p.nodes.n_nodes)]
+    keys = topo.level_keys
+    plain, bound = host.Cache(), host.Cache()
+    for r in range(0, p.nodes.n_nodes, 97):
+        lf = int(leaf_of_row[r])
+        plain.add_node({"metadata": {"name": names[r], "labels": {
+            keys[0]: topo.domain_values[0][int(zone_of_leaf[lf])], keys[1]: topo.domain_values[1][lf]}}})
+    bound.bind_engine(engine, {n: i for i, n in enumerate(names)}, keys, topo.domain_values)
+    muts = []
+    for j, r in enumerate(range(0, p.nodes.n_nodes, 97 * 7)):
+        level_key = keys[j % 2]
+        js, rj = f"js{j}", "w"
+        key = host.jobHashKey("default", f"{js}-{rj}-0")
+        lab = {"jobset.sigs.k8s.io/jobset-name": js, "jobset.sigs.k8s.io/replicatedjob-name": rj,
+               "jobset.sigs.k8s.io/job-index": "0", "jobset.sigs.k8s.io/job-key": key}
+        ann = {**lab, "alpha.jobset.sigs.k8s.io/exclusive-topology": level_key}
+        own = [{"uid": f"u{j}", "kind": "Job", "controller": True}]
+        leader = {"metadata": {"name": f"{js}-{rj}-0-0-abcde", "namespace": "default", "labels": lab,
+                               "annotations": {**ann, "batch.kubernetes.io/job-completion-index": "0"},
+                               "ownerReferences": own}, "spec": {"nodeName": names[r]}}
+        follower = {"metadata": {"name": f"{js}-{rj}-0-1-fghij", "namespace": "default", "labels": lab,
+                                 "annotations": {**ann, "batch.kubernetes.io/job-completion-index": "1"},
+                                 "ownerReferences": own}, "spec": {}}
+        for c in (plain, bound):
+            c.add_pod(leader)
+        a, ea = plain.Default(follower)
+        b, eb = bound.Default(follower)
+        assert ea is None and eb is None and a == b
+        muts.append(a["spec"]["nodeSelector"])
+        for c in (plain, bound):
+            c.add_pod(a)
+        assert plain.Reconcile("default", leader["metadata"]["name"]) == bound.Reconcile(
+            "default", leader["metadata"]["name"]) is None
+    assert len({tuple(m.items()) for m in muts}) > 1
+    sb, sp = bound.stats(), plain.stats()
+    assert sb["nodeGets"] == 0 and sb["engineCalls"] > 0 and sp["nodeGets"] > 0
