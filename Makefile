@@ -31,8 +31,19 @@ $(LIB): $(OBJ)
 oracle:
 	$(MAKE) -s -C oracle
 
+# diagnostic build with in-kernel phase stamps (tools/stamps.py); never the product library
+diag: tools/diag/libjsplace.so tools/diag/dispatch_probe
+tools/diag/dispatch_probe: tools/dispatch_probe.hip
+	@mkdir -p tools/diag
+	$(HIPCC) --offload-arch=gfx950 -O3 -o $@ $<
+tools/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip jobset_amd/csrc/jsp_engine.cc $(HOST_SRC) $(HDR) $(HOST_HDR)
+	@mkdir -p build/diag tools/diag
+	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -c -o build/diag/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -x hip -c -o build/diag/e.o jobset_amd/csrc/jsp_engine.cc
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag/k.o build/diag/e.o $(HOST_OBJ)
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean diag

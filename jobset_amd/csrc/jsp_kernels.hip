@@ -26,6 +26,21 @@
 
 namespace jsp {
 
+// Diagnostic build only (-DJSP_STAMPS, tools/stamps.py): per-workgroup phase
+// timestamps of the constant 100 MHz clock, for finding where a launch's
+// time goes. The product library is built without it.
+#ifdef JSP_STAMPS
+__device__ unsigned long long jsp_dbg[4096 * 8];
+#define JSP_STAMP(blk, i)                                                                 \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && (blk) < 4096) jsp_dbg[(blk) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define JSP_STAMP(blk, i) \
+    do {                  \
+    } while (0)
+#endif
+
 // ----------------------------------------------------------------- helpers
 // Inclusive wave64 prefix sum on the VALU with DPP (no LDS traffic):
 // row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry the
@@ -140,6 +155,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) valid[i] = any && (row + i >= r0) && (row + i < r1);
         __syncthreads();  // s_cls / s_ls / s_acc ready (first chunk); previous leaf pass done (later ones)
+        JSP_STAMP(blk, 1);
 
         // ---- row pass: per value, evaluate 4 rows, scan, store row prefixes
         for (int c = 0; c < nv; ++c) {
@@ -171,6 +187,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
             if (lane == 63) s_wsum[c * kTallyWaves + wid] = incl;
         }
         __syncthreads();
+        JSP_STAMP(blk, 6);
 
         // ---- leaf pass: one thread per leaf folds its rows of this chunk
         for (uint32_t li = tid; li < nl; li += kTallyThreads) {
@@ -195,6 +212,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
         }
     }
     __syncthreads();
+    JSP_STAMP(blk, 7);
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
         const uint32_t leaf = a.leaf_base + l0 + li;
         for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * kMaxBlkLeaves + li];
@@ -515,7 +533,9 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
         __syncthreads();
         tile = s_x[0];
     }
+    JSP_STAMP(tile, 0);
     tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+    JSP_STAMP(tile, 2);
 
     const uint32_t* s_acc = lds + tally_acc_off();
     const uint4 bt = a.blk[tile];
@@ -523,6 +543,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     const bool ok = (uint32_t)tid < nl && s_acc[tid] >= f.pods && s_acc[kMaxBlkLeaves + tid] == 0;
     uint32_t total;
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
+    JSP_STAMP(tile, 3);
     unsigned long long* g = f.granules;
     if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total);
     if (tid < 64) {  // wave 0: look back
@@ -556,6 +577,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
         }
     }
     __syncthreads();
+    JSP_STAMP(tile, 4);
     const uint32_t prefix = s_x[2];
     if (ok && prefix + rank < f.J) f.assign[prefix + rank] = (int32_t)(a.leaf_base + l0 + tid);
     if (tile + 1 == a.n_blocks) {
@@ -567,6 +589,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
             f.stats[2] = s_x[3];
         }
     }
+    JSP_STAMP(tile, 5);
 }
 
 // ----------------------------------------------------------------- A5 / A9 batch kernels
@@ -743,3 +766,14 @@ hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_
 }
 
 }  // namespace jsp
+
+#ifdef JSP_STAMPS
+extern "C" int jsp_debug_stamps(unsigned long long* out, unsigned n) {
+    if (n > 4096 * 8) n = 4096 * 8;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(jsp::jsp_dbg), n * sizeof(unsigned long long)) == hipSuccess ? 0 : -2;
+}
+extern "C" int jsp_debug_clear() {
+    static unsigned long long zero[4096 * 8];
+    return hipMemcpyToSymbol(HIP_SYMBOL(jsp::jsp_dbg), zero, sizeof zero) == hipSuccess ? 0 : -2;
+}
+#endif

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libjsplace.so")
+# JSP_LIB_PATH selects another build of the same library (tools/stamps.py
+# loads the -DJSP_STAMPS diagnostic build); the default is the in-tree product.
+LIB_PATH = os.environ.get("JSP_LIB_PATH") or os.path.join(_HERE, "libjsplace.so")
 
 JSP_OK, JSP_EINVAL, JSP_EHIP, JSP_ENOMEM, JSP_ESTATE, JSP_ERANGE = 0, -1, -2, -3, -4, -5
 ERROR_NAMES = {JSP_EINVAL: "JSP_EINVAL", JSP_EHIP: "JSP_EHIP", JSP_ENOMEM: "JSP_ENOMEM",
