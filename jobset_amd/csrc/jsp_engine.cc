@@ -95,7 +95,7 @@ struct jsp_engine {
     uint32_t feas_words = 0;
 
     // scratch
-    DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+    DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, recs, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
     int fused_mode = JSP_FUSED_AUTO;
     uint32_t last_shape = 0;  // 0 three launches, 1 fused tail, 2 single-class compaction
 
@@ -227,9 +227,12 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
                              e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
     ev_end(p, s);
     p = ev_begin(e, 2, s);
+    if (e->recs.reserve(sizeof(jsp::AssignRec) * (size_t)std::max<uint32_t>(J, 1)) != hipSuccess)
+        return set_err(JSP_ENOMEM, "assignment records (%u jobs)", J);
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
-                               e->C, e->topo, e->t_off_h[e->K], d_run_class, d_run_len, n_runs, J, d_assign,
-                               e->stats.as<uint32_t>(), s));
+                               e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
+                               d_assign,
+                               e->stats.as<uint32_t>(), e->recs.as<jsp::AssignRec>(), s));
     ev_end(p, s);
     return JSP_OK;
 }
@@ -292,7 +295,10 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     f.J = J;
     f.assign = d_assign;
     f.stats = e->stats.as<uint32_t>();
-    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc + a.do_occ);
+    const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
+    f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
+    f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
+    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc + a.do_occ, f.topo_in_lds ? topo_words : 0u);
     EvPair* p = ev_begin(e, 3, s);
     HIP_TRY(jsp::launch_fused(a, f, s));
     ev_end(p, s);

@@ -34,6 +34,15 @@ struct alignas(16) DevClass {
 };
 constexpr uint32_t kDivIdentity = 0xFFFFFFFFu;
 
+// A long run's step gives away the taken bits of a window word: one record per
+// such word (assign_kernel), expanded to assign[] by expand_kernel. Each taken
+// domain is in exactly one record, so J records always suffice.
+struct alignas(16) AssignRec {
+    uint32_t dom0;   // domain of bit 0 of the word
+    uint32_t base;   // job of the lowest taken bit
+    uint64_t took;   // taken bits
+};
+
 // Domain hierarchy on the device (passed by value).
 struct TopoDev {
     uint32_t K;
@@ -77,6 +86,8 @@ struct FusedArgs {
     int32_t* assign;
     uint32_t* stats;
     size_t lds_bytes;
+    uint32_t topo_in_lds;        // hierarchy tables staged in LDS for the tail
+    uint32_t topo_lds_words;     // their size (0 when not staged)
 };
 
 // Single-class leaf-level placement as one compaction pass (decoupled look-back).
@@ -92,21 +103,50 @@ struct CompactArgs {
     uint32_t coresident;           // 1: every workgroup is resident at once, tile = blockIdx.x
 };
 
-constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 8 + 2 * nt; }
+constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt; }
 constexpr uint32_t kFusedMaxWords = 6144;  // taken + feasibility words the fused tail keeps in LDS (48 KiB)
+constexpr uint32_t kFusedStage = 2048;     // ranks the fused tail stages per long-run step (8 KiB)
+constexpr uint32_t kMinStage = 4096;       // assign_kernel stages the bitmaps in LDS only if this much stage remains
+constexpr uint32_t kMaxStage = 32768;
+constexpr uint32_t kFusedTopoMax = 8192;   // hierarchy-table words the fused tail stages in LDS (32 KiB)
+constexpr size_t kLdsBytes = 160 * 1024;   // gfx950 LDS per workgroup
+// window of a long-run step: NT u64 words + NT u32 ranks, in u64 units
+constexpr uint32_t kAssignWinWords64 = kAssignThreads + kAssignThreads / 2;
+constexpr uint32_t kFusedWinWords64 = kTallyThreads + kTallyThreads / 2;
+
+// Words of the LDS copy of the hierarchy tables (parent[k] for k >= 1,
+// child_start[k] for k < K-1), in the order stage_meta numbers them.
+__host__ __device__ inline uint32_t topo_table_words(uint32_t K, const uint32_t* D) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < K; ++k) {
+        if (k >= 1) t += D[k];
+        if (k + 1 < K) t += D[k] + 1;
+    }
+    return t;
+}
+
+// LDS plan of assign_kernel: the hierarchy tables, then the feasibility
+// bitmaps, are staged in LDS when they fit beside the taken bitmaps.
+struct AssignPlan {
+    uint32_t feas_in_lds;
+    uint32_t topo_in_lds;
+    uint32_t stage_cap;  // ranks per long-run step
+    size_t lds_bytes;    // 0: does not fit
+};
+AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_words);
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
 size_t compact_lds_bytes();
-size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv);
-size_t assign_lds_bytes(uint32_t t_words);
+size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv, uint32_t topo_words);
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s);
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
-                         const TopoDev& topo, uint32_t t_words, const uint32_t* run_class, const uint32_t* run_len,
-                         uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats, hipStream_t s);
+                         const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
+                         const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
+                         AssignRec* recs, hipStream_t s);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

@@ -189,24 +189,26 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
         __syncthreads();
         JSP_STAMP(blk, 6);
 
-        // ---- leaf pass: one thread per leaf folds its rows of this chunk
+        // ---- leaf pass: one thread per leaf folds its rows of this chunk.
+        // Chunk prefix at row x = wave-local prefix + the totals of the waves
+        // before x's wave; every LDS read of a value is independent (one
+        // round trip), the wave offsets come from one 16-B read.
+        static_assert(kTallyWaves == 4, "wave-offset select assumes 4 waves");
         for (uint32_t li = tid; li < nl; li += kTallyThreads) {
             const uint32_t s = s_ls[li], e = s_ls[li + 1];
             const uint32_t lo = s > base ? s : base;
             const uint32_t hi = e < base + kChunkRows ? e : base + kChunkRows;
             if (lo >= hi) continue;
-            const uint32_t xl = lo - base, xh = hi - 1 - base;  // chunk-local first / last row
-            const uint32_t wl = xl >> 8, wh = xh >> 8;           // their waves (256 rows per wave)
+            const uint32_t xh = hi - 1 - base;                       // chunk-local last row
+            const uint32_t xb = lo > base ? lo - 1 - base : 0u;      // row before the first (if any)
+            const bool has_lo = lo > base;
+            const uint32_t wh = xh >> 8, wb = xb >> 8;               // their waves (256 rows per wave)
             for (int c = 0; c < nv; ++c) {
                 const uint32_t* pre = s_pre + c * kChunkRows;
-                const uint32_t* ws = s_wsum + c * kTallyWaves;
-                uint32_t hi_p = pre[xh], lo_p = xl > 0 ? pre[xl - 1] : 0u;
-                for (uint32_t w = 0; w < wh; ++w) hi_p += ws[w];
-                if (xl > 0) {
-                    const uint32_t wlo = (xl - 1) >> 8;
-                    for (uint32_t w = 0; w < wlo; ++w) lo_p += ws[w];
-                }
-                (void)wl;
+                const uint4 ws = reinterpret_cast<const uint4*>(s_wsum)[c];
+                const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
+                const uint32_t hi_p = pre[xh] + (wh == 0 ? 0u : wh == 1 ? e1 : wh == 2 ? e2 : e3);
+                const uint32_t lo_p = has_lo ? pre[xb] + (wb == 0 ? 0u : wb == 1 ? e1 : wb == 2 ? e2 : e3) : 0u;
                 s_acc[c * kMaxBlkLeaves + li] += hi_p - lo_p;
             }
         }
@@ -223,7 +225,9 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void tally_kernel(TallyArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    JSP_STAMP(blockIdx.x, 0);
     tally_block<W, R>(a, blockIdx.x, lds);
+    JSP_STAMP(blockIdx.x, 5);
 }
 
 // ----------------------------------------------------------------- feasibility
@@ -303,8 +307,12 @@ struct AssignMeta {
     uint32_t* s_pods;    // kMaxClasses
     uint32_t* s_woff;    // kMaxClasses + 1
     uint32_t* s_toff;    // 8
+    uint32_t* s_D;       // 8: domains per level
+    uint32_t* s_poff;    // 8: parent[k] offset in the LDS topology tables
+    uint32_t* s_coff;    // 8: child_start[k] offset in the LDS topology tables
     uint32_t* s_rc;      // NT run classes (tile)
     uint32_t* s_ro;      // NT run job offsets (tile)
+    uint32_t* s_long;    // NT indices of the tile's long runs
 };
 
 template <int NT>
@@ -318,8 +326,12 @@ __device__ __forceinline__ AssignMeta carve_meta(uint32_t* s_small) {
     m.s_pods = m.s_lvl + kMaxClasses;
     m.s_woff = m.s_pods + kMaxClasses;
     m.s_toff = m.s_woff + kMaxClasses + 1;
-    m.s_rc = m.s_toff + 8;
+    m.s_D = m.s_toff + 8;
+    m.s_poff = m.s_D + 8;
+    m.s_coff = m.s_poff + 8;
+    m.s_rc = m.s_coff + 8;
     m.s_ro = m.s_rc + NT;
+    m.s_long = m.s_ro + NT;
     return m;
 }
 
@@ -336,12 +348,31 @@ __device__ __forceinline__ void stage_meta(const AssignMeta& m, const DevClass* 
     }
     for (uint32_t i = tid; i <= C; i += NT) m.s_woff[i] = word_off[i];
     if (tid == 0) {
-        uint32_t off = 0;
+        uint32_t off = 0, t = 0;
         for (uint32_t k = 0; k < topo.K; ++k) {
             m.s_toff[k] = off;
+            m.s_D[k] = topo.D[k];
             off += (topo.D[k] + 63) >> 6;
+            if (k >= 1) { m.s_poff[k] = t; t += topo.D[k]; }
+            if (k + 1 < topo.K) { m.s_coff[k] = t; t += topo.D[k] + 1; }
         }
         m.s_toff[topo.K] = off;
+    }
+}
+
+// Copy the hierarchy tables into LDS (no barrier inside).
+template <int NT>
+__device__ __forceinline__ void stage_topo(uint32_t* s_topo, const TopoDev& topo) {
+    uint32_t t = 0;
+    for (uint32_t k = 0; k < topo.K; ++k) {
+        if (k >= 1) {
+            for (uint32_t i = threadIdx.x; i < topo.D[k]; i += NT) s_topo[t + i] = (uint32_t)topo.par[k][i];
+            t += topo.D[k];
+        }
+        if (k + 1 < topo.K) {
+            for (uint32_t i = threadIdx.x; i <= topo.D[k]; i += NT) s_topo[t + i] = topo.cs[k][i];
+            t += topo.D[k] + 1;
+        }
     }
 }
 
@@ -351,106 +382,354 @@ __device__ __forceinline__ uint32_t taken_words(const TopoDev& topo) {
     return off;
 }
 
-// Runs walk. Requires stage_meta + a barrier first, and s_taken zeroed.
-template <int NT>
+// Taking domain d at level lvl also takes, at every other level, each domain
+// whose leaf range intersects d's: its ancestors (one bit per level) and its
+// descendants (a bit range per level). LDS atomics: other lanes may mark the
+// same words. The hierarchy tables are read from LDS when staged there.
+template <bool TOPO_LDS>
+__device__ __forceinline__ void mark_other_levels(uint32_t d, uint32_t lvl, uint32_t K, const TopoDev& topo,
+                                                  uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo) {
+    uint32_t dd = d;  // ancestors
+    for (int kk = (int)lvl - 1; kk >= 0; --kk) {
+        if constexpr (TOPO_LDS) dd = s_topo[m.s_poff[kk + 1] + dd];
+        else dd = (uint32_t)topo.par[kk + 1][dd];
+        lds_set_bit(s_taken + m.s_toff[kk], dd);
+    }
+    uint32_t lo = d, hi = d + 1;  // descendants
+    for (uint32_t kk = lvl + 1; kk < K; ++kk) {
+        if constexpr (TOPO_LDS) {
+            const uint32_t* cs = s_topo + m.s_coff[kk - 1];
+            lo = cs[lo];
+            hi = cs[hi];
+        } else {
+            lo = topo.cs[kk - 1][lo];
+            hi = topo.cs[kk - 1][hi];
+        }
+        lds_set_range(s_taken + m.s_toff[kk], lo, hi);
+    }
+}
+
+// Position of the r-th (0-based) set bit of x; r < popcount(x).
+__device__ __forceinline__ uint32_t select_bit(uint64_t x, uint32_t r) {
+    uint32_t pos = 0;
+    uint32_t c = (uint32_t)__popc((uint32_t)x);
+    if (r >= c) { r -= c; x >>= 32; pos += 32; }
+    c = (uint32_t)__popc((uint32_t)x & 0xFFFFu);
+    if (r >= c) { r -= c; x >>= 16; pos += 16; }
+    c = (uint32_t)__popc((uint32_t)x & 0xFFu);
+    if (r >= c) { r -= c; x >>= 8; pos += 8; }
+    c = (uint32_t)__popc((uint32_t)x & 0xFu);
+    if (r >= c) { r -= c; x >>= 4; pos += 4; }
+    c = (uint32_t)__popc((uint32_t)x & 0x3u);
+    if (r >= c) { r -= c; x >>= 2; pos += 2; }
+    c = (uint32_t)(x & 1u);
+    if (r >= c) pos += 1;
+    return pos;
+}
+
+// Runs with at most this many jobs are placed by wave 0 alone: no workgroup
+// barrier, a 64-word (4096-domain) window per step, per-class state in wave
+// 0's registers (lane c holds class c). Longer runs use the whole workgroup on
+// an NT-word window per step.
+constexpr uint32_t kWaveRunMax = 64;
+
+// One long run (jobs [j0, jend) of class c), executed by every wave of the
+// workgroup. Per step: a block scan gives each window word its first rank;
+// each word's owner marks what the step takes from it; every thread then
+// emits an equal share of the step's ranks (merge-path split: binary search
+// of its first rank over the word ranks, select of the bit, then a walk)
+// into LDS in rank order; the ranks leave for assign[] in coalesced stores.
+// Returns the class's new cursor.
+template <int NT, bool TOPO_LDS>
+__device__ uint32_t long_run(uint32_t c, uint32_t j0, uint32_t jend, const uint64_t* __restrict__ feas,
+                             const TopoDev& topo, int32_t* __restrict__ assign, uint64_t* s_taken,
+                             const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win, uint32_t* s_stage,
+                             uint32_t stage_cap, AssignRec* __restrict__ recs, uint32_t& placed) {
+    const int tid = threadIdx.x;
+    const uint32_t K = topo.K;
+    uint32_t* s_wpre = reinterpret_cast<uint32_t*>(s_win + NT);
+    __syncthreads();  // wave 0's short-run state (taken words, cursors) visible
+    JSP_STAMP(4001u + (c & 7u), 0);
+    const uint32_t lvl = m.s_lvl[c];
+    const uint32_t D = m.s_D[lvl];
+    const uint32_t nw = (D + 63) >> 6;
+    uint64_t* Tk = s_taken + m.s_toff[lvl];
+    const uint64_t* F = feas + m.s_woff[c];
+    uint32_t cur = m.s_cursor[c];
+    uint32_t need = jend - j0, jpos = j0;
+    while (need > 0 && cur < D) {
+        const uint32_t cap = (recs != nullptr || need < stage_cap) ? need : stage_cap;
+        const uint32_t wb0 = cur >> 6;
+        const uint32_t w = wb0 + tid;
+        uint64_t bits = 0;
+        if (w < nw) {
+            bits = F[w] & ~Tk[w];
+            if (w == wb0) bits &= ~0ull << (cur & 63);
+        }
+        const uint32_t cnt = (uint32_t)__popcll(bits);
+        uint32_t total;
+        const uint32_t pre = block_excl_scan<NT>(cnt, m.s_w, &total);
+        JSP_STAMP(4001u + (c & 7u), 1);
+        const uint32_t used = total < cap ? total : cap;
+        // the owner of each word marks the ranks [pre, min(pre + cnt, used)) taken
+        uint64_t took = 0;
+        if (cnt != 0 && pre < used) {
+            took = pre + cnt <= used ? bits : bits & ((1ull << select_bit(bits, used - pre)) - 1ull);
+            Tk[w] |= took;
+        }
+        if (recs != nullptr) {
+            // record mode: one {word, first job, taken bits} record per word that
+            // gives domains away; expand_kernel turns them into assign[] with the
+            // whole GPU. Slots from an LDS counter (one add per wave).
+            const uint64_t has = __ballot(took != 0);
+            uint32_t slot0 = 0;
+            if ((tid & 63) == 0 && has != 0) slot0 = atomicAdd(&m.s_misc[1], (uint32_t)__popcll(has));
+            slot0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot0);
+            if (took != 0) {
+                const uint32_t slot = slot0 + (uint32_t)__popcll(has & ((1ull << (tid & 63)) - 1ull));
+                AssignRec r;
+                r.dom0 = w * 64;
+                r.base = jpos + pre;
+                r.took = took;
+                recs[slot] = r;
+                if (K > 1) {
+                    uint64_t x = took;
+                    while (x) {
+                        mark_other_levels<TOPO_LDS>(w * 64 + (uint32_t)__builtin_ctzll(x), lvl, K, topo, s_taken, m,
+                                                    s_topo);
+                        x &= x - 1;
+                    }
+                }
+                if (pre + cnt >= used) m.s_misc[0] = w * 64 + 64 - (uint32_t)__builtin_clzll(took);  // last taken + 1
+            }
+            __syncthreads();
+            cur = total >= cap ? m.s_misc[0] : (wb0 + NT) * 64u;
+            need -= used;
+            jpos += used;
+            placed += used;
+            continue;  // the next step's scan barriers order s_misc[0] reuse
+        }
+        s_win[tid] = bits;
+        s_wpre[tid] = pre;
+        __syncthreads();
+        JSP_STAMP(4001u + (c & 7u), 2);
+        // this thread's share of the ranks: [i0, i1)
+        const uint32_t i0 = (uint32_t)(((uint64_t)tid * used) / NT);
+        const uint32_t i1 = (uint32_t)(((uint64_t)(tid + 1) * used) / NT);
+        if (i0 < i1) {
+            uint32_t lo = 0, hi = NT;  // last word k with s_wpre[k] <= i0: it holds rank i0
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_wpre[mid] <= i0) lo = mid; else hi = mid;
+            }
+            uint32_t k = lo;
+            uint64_t x = s_win[k];
+            x &= ~0ull << select_bit(x, i0 - s_wpre[k]);
+            for (uint32_t i = i0; i < i1; ++i) {
+                while (x == 0) x = s_win[++k];
+                const uint32_t d = (wb0 + k) * 64 + (uint32_t)__builtin_ctzll(x);
+                x &= x - 1;
+                s_stage[i] = d;
+                if (K > 1) mark_other_levels<TOPO_LDS>(d, lvl, K, topo, s_taken, m, s_topo);
+                if (i + 1 == used) m.s_misc[0] = d + 1;
+            }
+        }
+        __syncthreads();
+        JSP_STAMP(4001u + (c & 7u), 3);
+        for (uint32_t i = tid; i < used; i += NT) assign[jpos + i] = (int32_t)s_stage[i];
+        cur = total >= cap ? m.s_misc[0] : (wb0 + NT) * 64u;
+        need -= used;
+        jpos += used;
+        placed += used;
+        __syncthreads();  // window, stage and s_misc free again
+        JSP_STAMP(4001u + (c & 7u), 4);
+    }
+    for (uint32_t j = jpos + tid; j < jend; j += NT) assign[j] = -1;
+    JSP_STAMP(4001u + (c & 7u), 5);
+    return cur < D ? cur : D;
+}
+
+// Runs walk (A7). Requires stage_meta (+ stage_topo when TOPO_LDS) and a
+// barrier first, s_taken zeroed, and `feas` holding every class's bitmap words
+// (LDS or global). Jobs are taken in global order, run by run; a run of class
+// c takes the lowest free feasible domains at c's level from c's cursor on
+// (domains below the cursor are taken or infeasible: the cursor only grows).
+// Wave 0 walks every run; the other waves only join the long ones.
+template <int NT, bool TOPO_LDS>
 __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, const TopoDev& topo,
                              const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
-                             uint64_t* s_taken, const AssignMeta& m) {
-    const int tid = threadIdx.x;
+                             uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
+                             uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t K = topo.K;
+    // wave 0: class state in registers, lane c = class c (C <= kMaxClasses = 64)
+    uint32_t my_cur = 0, my_lvl = 0, my_woff = 0, my_D = 0, my_toff = 0;
+    if (wid == 0 && (uint32_t)lane < C) {
+        my_lvl = m.s_lvl[lane];
+        my_woff = m.s_woff[lane];
+        my_D = m.s_D[my_lvl];
+        my_toff = m.s_toff[my_lvl];
+        my_cur = m.s_cursor[lane];
+    }
     uint32_t placed = 0, jbase = 0;
     for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
-        // ---- a tile of runs and their job offsets (block scan of run lengths)
+        // ---- a tile of runs: job offsets (block scan of run lengths) and the long-run list
         const uint32_t ri = r0 + tid;
         const uint32_t len = ri < n_runs ? run_len[ri] : 0u;
-        m.s_rc[tid] = ri < n_runs ? run_class[ri] : 0u;
-        uint32_t tile_total;
+        const uint32_t rc = ri < n_runs ? run_class[ri] : 0u;
+        m.s_rc[tid] = rc;
+        uint32_t tile_total, n_long;
         const uint32_t off = block_excl_scan<NT>(len, m.s_w, &tile_total);
         m.s_ro[tid] = off;
+        const bool is_long = len > kWaveRunMax && rc < C;
+        const uint32_t lrank = block_excl_scan<NT>(is_long ? 1u : 0u, m.s_w, &n_long);
+        if (is_long) m.s_long[lrank] = (uint32_t)tid;
         __syncthreads();
         const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
-        for (uint32_t t = 0; t < nr; ++t) {
-            const uint32_t c = m.s_rc[t];
-            const uint32_t j0 = jbase + m.s_ro[t];
-            uint32_t jend = (t + 1 < nr) ? jbase + m.s_ro[t + 1] : jbase + tile_total;
-            if (jend > J) jend = J;
-            if (j0 >= jend) continue;
-            if (c >= C) {  // malformed run: its jobs are unplaceable
-                for (uint32_t j = j0 + tid; j < jend; j += NT) assign[j] = -1;
-                continue;
-            }
-            const uint32_t lvl = m.s_lvl[c];
-            const uint32_t D = topo.D[lvl];
-            const uint32_t nw = (D + 63) >> 6;
-            uint64_t* Tk = s_taken + m.s_toff[lvl];
-            const uint64_t* F = feas + m.s_woff[c];
-            uint32_t need = jend - j0, jpos = j0;
-            uint32_t cur = m.s_cursor[c];
-            while (need > 0 && cur < D) {
-                const uint32_t w = (cur >> 6) + tid;
-                uint64_t bits = 0;
-                if (w < nw) {
-                    bits = F[w] & ~Tk[w];
-                    if (w == (cur >> 6)) bits &= ~0ull << (cur & 63);
-                }
-                uint32_t total;
-                const uint32_t pre = block_excl_scan<NT>((uint32_t)__popcll(bits), m.s_w, &total);
-                if (tid == 0) m.s_misc[0] = ((cur >> 6) + NT) * 64u;
-                __syncthreads();
-                if (bits && pre < need) {
-                    uint32_t r = pre;
-                    uint64_t took = 0;
-                    while (bits && r < need) {
-                        const uint32_t b = __builtin_ctzll(bits);
-                        bits &= bits - 1;
-                        const uint32_t d = w * 64 + b;
-                        assign[jpos + r] = (int32_t)d;
-                        took |= 1ull << b;
-                        uint32_t dd = d;  // ancestors
-                        for (int kk = (int)lvl - 1; kk >= 0; --kk) {
-                            dd = (uint32_t)topo.par[kk + 1][dd];
-                            lds_set_bit(s_taken + m.s_toff[kk], dd);
-                        }
-                        uint32_t lo = d, hi = d + 1;  // descendants
-                        for (uint32_t kk = lvl + 1; kk < topo.K; ++kk) {
-                            lo = topo.cs[kk - 1][lo];
-                            hi = topo.cs[kk - 1][hi];
-                            lds_set_range(s_taken + m.s_toff[kk], lo, hi);
-                        }
-                        ++r;
-                        if (r == need) m.s_misc[0] = d + 1;
+        if (wid == 0) {
+            for (uint32_t t0 = 0; t0 < nr; t0 += 64) {
+                const uint32_t tl = t0 + (uint32_t)lane;
+                const uint32_t rc_l = tl < nr ? m.s_rc[tl] : 0u;
+                const uint32_t ro_l = tl < nr ? m.s_ro[tl] : 0u;
+                const uint32_t rn_l = tl + 1 < nr ? m.s_ro[tl + 1] : tile_total;
+                const uint32_t nb = (nr - t0) < 64u ? (nr - t0) : 64u;
+                for (uint32_t q = 0; q < nb; ++q) {
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
+                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)ro_l, (int)q);
+                    const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)rn_l, (int)q);
+                    const uint32_t j0 = jbase + o0;
+                    const uint32_t jend = jbase + o1 < J ? jbase + o1 : J;
+                    if (j0 >= jend) continue;
+                    if (c >= C) {  // malformed run: its jobs are unplaceable
+                        for (uint32_t j = j0 + lane; j < jend; j += 64) assign[j] = -1;
+                        continue;
                     }
-                    atomicOr(reinterpret_cast<unsigned long long*>(&Tk[w]), (unsigned long long)took);
+                    if (o1 - o0 > kWaveRunMax) {  // long run: publish the cursors, join the workgroup
+                        if ((uint32_t)lane < C) m.s_cursor[lane] = my_cur;
+                        const uint32_t nc = long_run<NT, TOPO_LDS>(c, j0, jend, feas, topo, assign, s_taken, m, s_topo,
+                                                                   s_win, s_stage, stage_cap, recs, placed);
+                        if ((uint32_t)lane == c) my_cur = nc;
+                        continue;
+                    }
+                    // ---- short run, wave 0 alone
+                    const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
+                    const uint32_t D = (uint32_t)__builtin_amdgcn_readlane((int)my_D, (int)c);
+                    const uint32_t nw = (D + 63) >> 6;
+                    uint64_t* Tk = s_taken + (uint32_t)__builtin_amdgcn_readlane((int)my_toff, (int)c);
+                    const uint64_t* F = feas + (uint32_t)__builtin_amdgcn_readlane((int)my_woff, (int)c);
+                    uint32_t cur = (uint32_t)__builtin_amdgcn_readlane((int)my_cur, (int)c);
+                    uint32_t need = jend - j0, jpos = j0;
+                    while (need > 0 && cur < D) {
+                        const uint32_t w = (cur >> 6) + lane;
+                        uint64_t bits = 0;
+                        if (w < nw) {
+                            bits = F[w] & ~Tk[w];
+                            if (w == (cur >> 6)) bits &= ~0ull << (cur & 63);
+                        }
+                        const uint32_t cnt = (uint32_t)__popcll(bits);
+                        const uint32_t incl = wave_incl_scan(cnt, lane);
+                        const uint32_t pre = incl - cnt;
+                        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                        uint32_t last = 0;
+                        if (bits && pre < need) {
+                            uint32_t r = pre;
+                            uint64_t took = 0;
+                            while (bits && r < need) {
+                                const uint32_t b = __builtin_ctzll(bits);
+                                bits &= bits - 1;
+                                const uint32_t d = w * 64 + b;
+                                assign[jpos + r] = (int32_t)d;
+                                took |= 1ull << b;
+                                if (K > 1) mark_other_levels<TOPO_LDS>(d, lvl, K, topo, s_taken, m, s_topo);
+                                last = d;
+                                ++r;
+                            }
+                            Tk[w] |= took;
+                        }
+                        if (total >= need) {  // the lane holding rank need-1 names the next cursor
+                            const uint64_t hit = __ballot(cnt != 0 && pre < need && pre + cnt >= need);
+                            cur = (uint32_t)__builtin_amdgcn_readlane((int)last, __builtin_ctzll(hit)) + 1;
+                        } else {
+                            cur = ((cur >> 6) + 64) * 64;
+                        }
+                        const uint32_t used = total < need ? total : need;
+                        need -= used;
+                        jpos += used;
+                        placed += used;
+                    }
+                    for (uint32_t j = jpos + lane; j < jend; j += 64) assign[j] = -1;
+                    if ((uint32_t)lane == c) my_cur = cur < D ? cur : D;
                 }
-                __syncthreads();
-                const uint32_t used = total < need ? total : need;
-                need -= used;
-                jpos += used;
-                placed += used;
-                cur = m.s_misc[0] < D ? m.s_misc[0] : D;
-                __syncthreads();
             }
-            for (uint32_t j = jpos + tid; j < jend; j += NT) assign[j] = -1;
-            if (tid == 0) m.s_cursor[c] = cur;
-            __syncthreads();
+        } else {
+            for (uint32_t q = 0; q < n_long; ++q) {
+                const uint32_t t = m.s_long[q];
+                const uint32_t j0 = jbase + m.s_ro[t];
+                uint32_t jend = (t + 1 < nr) ? jbase + m.s_ro[t + 1] : jbase + tile_total;
+                if (jend > J) jend = J;
+                if (j0 >= jend) continue;
+                long_run<NT, TOPO_LDS>(m.s_rc[t], j0, jend, feas, topo, assign, s_taken, m, s_topo, s_win, s_stage,
+                                       stage_cap, recs, placed);
+            }
         }
         jbase += tile_total;
-        __syncthreads();
+        __syncthreads();  // tile tables free again; short-run state visible
     }
-    if (tid == 0 && stats != nullptr) { stats[0] = n_runs; stats[1] = placed; }
+    if (tid == 0 && stats != nullptr) {
+        stats[0] = n_runs;
+        stats[1] = placed;
+        stats[3] = m.s_misc[1];  // records for expand_kernel
+    }
+    JSP_STAMP(4000u, 7);
 }
 
+// LDS: [taken t_words u64][window NT u64 + NT u32][feasibility feas_words u64, when staged]
+//      [small tables][hierarchy tables, when staged][stage stage_cap u32]
 __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     const uint64_t* __restrict__ feas, const uint32_t* __restrict__ word_off, const DevClass* __restrict__ cls,
     uint32_t C, TopoDev topo, const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
-    uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];  // [taken][small]
+    uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats, uint32_t feas_words,
+    uint32_t feas_in_lds, uint32_t topo_in_lds, uint32_t topo_words, uint32_t stage_cap, AssignRec* __restrict__ recs) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const uint32_t tw = taken_words(topo);
-    const AssignMeta m = carve_meta<kAssignThreads>(reinterpret_cast<uint32_t*>(s_dyn + tw));
+    uint64_t* s_win = s_dyn + tw;
+    uint64_t* s_feas = s_win + kAssignWinWords64;
+    const uint32_t fw = feas_in_lds ? feas_words : 0u;
+    uint32_t* s_small = reinterpret_cast<uint32_t*>(s_feas + fw);
+    const AssignMeta m = carve_meta<kAssignThreads>(s_small);
+    uint32_t* s_topo = s_small + assign_small_words(kAssignThreads);
+    uint32_t* s_stage = s_topo + (topo_in_lds ? topo_words : 0u);
+    JSP_STAMP(4000u, 0);
     stage_meta<kAssignThreads>(m, cls, C, word_off, topo);
+    if (threadIdx.x == 0) m.s_misc[1] = 0;
+    if (topo_in_lds) stage_topo<kAssignThreads>(s_topo, topo);
     for (uint32_t i = threadIdx.x; i < tw; i += kAssignThreads) s_dyn[i] = 0;
+    for (uint32_t i = threadIdx.x; i < fw; i += kAssignThreads) s_feas[i] = feas[i];
     __syncthreads();
-    assign_block<kAssignThreads>(feas, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m);
+    JSP_STAMP(4000u, 1);
+    const uint64_t* F = feas_in_lds ? s_feas : feas;
+    if (topo_in_lds)
+        assign_block<kAssignThreads, true>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m, s_topo,
+                                           s_win, s_stage, stage_cap, recs);
+    else
+        assign_block<kAssignThreads, false>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m,
+                                            s_topo, s_win, s_stage, stage_cap, recs);
+}
+
+// Expansion of assign_kernel's records (grid-stride, one wave per record):
+// lane b of a record with bit b taken writes job base + (taken bits below b).
+// Each record's jobs are consecutive, so a wave's stores are one run.
+__global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict__ recs,
+                                                     const uint32_t* __restrict__ stats, int32_t* __restrict__ assign) {
+    const uint32_t n = stats[3];
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
+    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
+        const AssignRec x = recs[r];
+        if ((x.took >> lane) & 1ull)
+            assign[x.base + (uint32_t)__popcll(x.took & ((1ull << lane) - 1ull))] = (int32_t)(x.dom0 + lane);
+    }
 }
 
 // ----------------------------------------------------------------- fused small-snapshot placement
@@ -481,9 +760,15 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     if (*s_flag == 0) return;
     // the tail: small tables first (independent of the other workgroups' sums)
     uint64_t* s_taken = reinterpret_cast<uint64_t*>(lds);
-    uint64_t* s_feas = s_taken + f.t_words;
-    const AssignMeta m = carve_meta<kTallyThreads>(reinterpret_cast<uint32_t*>(s_feas + f.feas_words));
+    uint64_t* s_win = s_taken + f.t_words;
+    uint64_t* s_feas = s_win + kFusedWinWords64;
+    uint32_t* s_small = reinterpret_cast<uint32_t*>(s_feas + f.feas_words);
+    const AssignMeta m = carve_meta<kTallyThreads>(s_small);
+    uint32_t* s_topo = s_small + assign_small_words(kTallyThreads);
+    uint32_t* s_stage = s_topo + f.topo_lds_words;
     stage_meta<kTallyThreads>(m, a.cls, f.C, f.word_off, f.topo);
+    if (threadIdx.x == 0) m.s_misc[1] = 0;
+    if (f.topo_in_lds) stage_topo<kTallyThreads>(s_topo, f.topo);
     for (uint32_t i = threadIdx.x; i < f.t_words; i += kTallyThreads) s_taken[i] = 0;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -500,8 +785,12 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
         if (lane == 0) s_feas[gw] = word;
     }
     __syncthreads();
-    assign_block<kTallyThreads>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign, f.stats,
-                                s_taken, m);
+    if (f.topo_in_lds)
+        assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
+                                          f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr);
+    else
+        assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
+                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr);
 }
 
 // ----------------------------------------------------------------- single-class compaction
@@ -711,14 +1000,32 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 
 size_t compact_lds_bytes() { return sizeof(uint32_t) * (tally_lds_words(2) + 4 + 2 * kTallyWaves + 8); }
 
-size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv) {
-    const size_t tail = (size_t)(t_words + feas_words) * 8 + sizeof(uint32_t) * assign_small_words(kTallyThreads);
+size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv, uint32_t topo_words) {
+    const size_t tail = (size_t)(t_words + kFusedWinWords64 + feas_words) * 8 +
+                        sizeof(uint32_t) * (assign_small_words(kTallyThreads) + topo_words + kFusedStage);
     const size_t head = sizeof(uint32_t) * (tally_lds_words((int)nv) + 4);
     return ((tail > head ? tail : head) + 15) & ~size_t(15);
 }
 
-size_t assign_lds_bytes(uint32_t t_words) {
-    return (size_t)t_words * 8 + sizeof(uint32_t) * assign_small_words(kAssignThreads);
+AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_words) {
+    AssignPlan p{};
+    size_t used = (size_t)(t_words + kAssignWinWords64) * 8 + sizeof(uint32_t) * assign_small_words(kAssignThreads);
+    if (used > kLdsBytes) return p;  // lds_bytes 0: does not fit
+    if (topo_words > 0 && used + sizeof(uint32_t) * topo_words <= kLdsBytes) {
+        p.topo_in_lds = 1;
+        used += sizeof(uint32_t) * topo_words;
+    }
+    if (used + (size_t)feas_words * 8 + sizeof(uint32_t) * kMinStage <= kLdsBytes) {
+        p.feas_in_lds = 1;
+        used += (size_t)feas_words * 8;
+    }
+    size_t st = (kLdsBytes - used) / sizeof(uint32_t);
+    if (st > kMaxStage) st = kMaxStage;
+    st &= ~size_t(63);
+    if (st < 64) return AssignPlan{};
+    p.stage_cap = (uint32_t)st;
+    p.lds_bytes = used + sizeof(uint32_t) * st;
+    return p;
 }
 
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
@@ -731,10 +1038,19 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
 }
 
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
-                         const TopoDev& topo, uint32_t t_words, const uint32_t* run_class, const uint32_t* run_len,
-                         uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats, hipStream_t s) {
-    hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), assign_lds_bytes(t_words), s, feas, word_off,
-                       cls, C, topo, run_class, run_len, n_runs, J, assign, stats);
+                         const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
+                         const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
+                         AssignRec* recs, hipStream_t s) {
+    const uint32_t topo_words = topo.K > 1 ? topo_table_words(topo.K, topo.D) : 0u;
+    const AssignPlan p = plan_assign(t_words, feas_words, topo_words);
+    if (p.lds_bytes == 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
+                       run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
+                       topo_words, p.stage_cap, recs);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
+    // records never outnumber the placed jobs (each taken domain is in one record)
+    const uint32_t waves = J < 8192u ? J : 8192u;
+    hipLaunchKernelGGL(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, stats, assign);
     return hipGetLastError();
 }
 

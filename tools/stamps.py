@@ -23,6 +23,7 @@ def main():
     from jobset_amd.snapshot import job_runs
     cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 50
+    b2b = int(sys.argv[3]) if len(sys.argv) > 3 else 1  # launches per sample: >1 = back-to-back (GPU busy)
     lib = native.lib()
     lib.jsp_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     p = synth.CONFIGS[cfg]()
@@ -36,7 +37,9 @@ def main():
     rows = []
     for i in range(reps):
         lib.jsp_debug_clear()
-        eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 0)
+        torch.cuda.synchronize()
+        for _ in range(b2b):  # the stamps keep the last launch's times
+            eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 0)
         torch.cuda.synchronize()
         lib.jsp_debug_stamps(buf.ctypes.data, buf.shape[0])
         st = buf.reshape(4096, 8)
@@ -46,7 +49,7 @@ def main():
         rows.append(((st[:, :8] - t0) * 10))  # ns
     arr = np.stack(rows[5:])  # [reps, blocks, 6]
     med = np.median(arr, axis=0)
-    print(f"cfg{cfg}: {med.shape[0]} workgroups; phase start (ns, median over {arr.shape[0]} launches)")
+    print(f"cfg{cfg} ({b2b} back-to-back launches per sample): {med.shape[0]} workgroups; phase start (ns, median over {arr.shape[0]} launches)")
     cols = [0, 1, 6, 7, 2, 3, 4, 5]
     print("phase:          entry  barrier1  rowpass  leafpass  tallied  scanned  lookback  end")
     for b in range(min(med.shape[0], 24)):
