@@ -5,8 +5,8 @@ Metric (BASELINE.json): exclusive-topology placements/sec at 15k nodes; p99
 recovery placement latency. Workload (`value`): config 2 — a 15,000-node /
 1,000-rack post-delete snapshot and a full-JobSet recovery of 990 jobs x 15
 pods — resident in HBM; one step = one placement of all 990
-jobs (tally kernel + feasibility-bitmap kernel + assignment kernel) from the
-resident snapshot and job list to assign[] in HBM.
+jobs (tally + feasibility + lowest-index assignment) from the resident
+snapshot and run list to assign[] in HBM.
 
 `--gpus N` (torchrun, one rank per GPU): config 2 has ~0.4 MB of rows and does
 not shard usefully, so ranks run independent replicas (weak scaling, no
@@ -15,14 +15,23 @@ placements / max-over-ranks time. The sharded path of config 4 (1M nodes,
 node dimension split over the ranks, per-leaf tallies SUM-all-reduced by RCCL)
 is reported beside it under "cfg4_1M".
 
+Roofline: the dominant kernel's average duration comes from two HIP events
+recorded on the launch stream around K back-to-back launches (no per-launch
+events, which would add their own overhead to every launch); its algorithmic
+bytes are DESIGN.md §4's. `traffic` is the PMC-measured HBM bytes per launch
+of the same kernel from the committed rocprofv3 passes under profiles/
+(FETCH_SIZE x 2 for gfx950's wide-load halving + WRITE_SIZE, per
+MI355X_MICROARCH.md "HBM"), or null when no pass for it is committed.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
 import argparse
+import csv
+import glob
 import json
 import os
-import statistics
 import sys
 import time
 
@@ -32,16 +41,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
+SHAPES = {0: "three launches (tally -> feas -> assign + expand)", 1: "fused single launch",
+          2: "single-class compaction, one launch"}
+KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel"}
 
 
 def tally_bytes(p) -> int:
     """Algorithmic bytes of one tally launch: every node row read once
-    (labels 8W + taints 4 + free 4R + excl 4 B), leaf offsets and block table
-    read, per-(class, leaf) capacities and per-leaf occupancy written once."""
+    (labels 8W + taints 4 + free 4R + excl 4 B), leaf offsets read,
+    per-(class, leaf) capacities and per-leaf occupancy written once."""
     n = p.nodes
     row = 8 * n.n_label_words + 4 + 4 * n.n_res + 4
     L = n.n_leaves
     return n.n_nodes * row + 4 * (L + 1) + 4 * len(p.classes) * L + 4 * L
+
+
+def compact_bytes(p) -> int:
+    """Algorithmic bytes of one compaction launch (one leaf-level class): the
+    rows and leaf offsets read once, assign[] written once (the per-leaf
+    tallies stay in LDS)."""
+    n = p.nodes
+    row = 8 * n.n_label_words + 4 + 4 * n.n_res + 4
+    return n.n_nodes * row + 4 * (n.n_leaves + 1) + 4 * p.n_jobs
 
 
 def placement_tail_bytes(p) -> int:
@@ -55,6 +76,40 @@ def placement_tail_bytes(p) -> int:
     return 4 * (C + 1) * L + 8 * words + 8 * n_runs + 4 * p.n_jobs
 
 
+def pmc_traffic(kernel: str, cfg: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (latest round under profiles/): FETCH_SIZE (KiB, x2 on gfx950) +
+    WRITE_SIZE (KiB), averaged over that kernel's dispatches."""
+    def avg(path):
+        vals = []
+        with open(path, newline="") as f:
+            for row in csv.DictReader(f):
+                if row["Kernel_Name"].startswith(kernel):
+                    vals.append(float(row["Counter_Value"]))
+        return sum(vals) / len(vals) if vals else None
+    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        fp, wp = os.path.join(d, f"pmc_fetch_cfg{cfg}.csv"), os.path.join(d, f"pmc_write_cfg{cfg}.csv")
+        if os.path.exists(fp) and os.path.exists(wp):
+            fa, wa = avg(fp), avg(wp)
+            if fa is not None and wa is not None:
+                return {"bytes": round((2 * fa + wa) * 1024), "source": os.path.relpath(d, ROOT)}
+    return None
+
+
+def event_loop_us(fn, k: int, stream) -> float:
+    """Average µs per call of `fn` over k back-to-back calls, HIP events on
+    the launch stream around the whole loop."""
+    import torch
+    s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.default_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(s)
+    for _ in range(k):
+        fn()
+    b.record(s)
+    b.synchronize()
+    return a.elapsed_time(b) * 1e3 / k
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -63,6 +118,7 @@ def main() -> None:
     ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the 1M-node sharded leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the per-config (1, 3, 5) lines")
     args = ap.parse_args()
 
     import torch
@@ -84,19 +140,22 @@ def main() -> None:
     stream = torch.cuda.current_stream().cuda_stream
     eng = Engine(local)
 
+    def device_step(p):
+        rc_np, rl_np = job_runs(p.job_class)
+        rc = torch.from_numpy(rc_np.astype(np.int32)).cuda()
+        rl = torch.from_numpy(rl_np.astype(np.int32)).cuda()
+        out = torch.empty(max(p.n_jobs, 1), dtype=torch.int32, device="cuda")
+
+        def step():
+            eng.place_device(rc.data_ptr(), rl.data_ptr(), rc_np.shape[0], p.n_jobs, out.data_ptr(), stream)
+        return step, out
+
     # ------------------------------------------------ config 2 (value)
     p = synth.config2()
     eng.load(p)
     J = p.n_jobs
-    # the JobSet spec: one replicatedJob "workers" x 990 replicas = one run of class 0
-    rc_np, rl_np = job_runs(p.job_class)
-    rc = torch.from_numpy(rc_np.astype(np.int32)).cuda()
-    rl = torch.from_numpy(rl_np.astype(np.int32)).cuda()
-    out = torch.empty(J, dtype=torch.int32, device="cuda")
-
-    def step():
-        eng.place_device(rc.data_ptr(), rl.data_ptr(), rc_np.shape[0], J, out.data_ptr(), stream)
-
+    shape = eng.place(p.job_class).fused
+    step, out = device_step(p)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -109,29 +168,20 @@ def main() -> None:
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    placed = int((out.cpu().numpy() >= 0).sum())
-    total_placements = placed * args.steps * world
-    value = total_placements / elapsed
+    placed = int((out[:J].cpu().numpy() >= 0).sum())
+    value = placed * args.steps * world / elapsed
 
-    # kernel durations by HIP events on the launch stream (same steps again)
-    eng.set_timing(True)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    tm = eng.timing(reset=True)
-    eng.set_timing(False)
-    tally_us = tm.tally_ms * 1e3 / max(tm.calls, 1)
-    feas_us = tm.feas_ms * 1e3 / max(tm.calls, 1)
-    assign_us = tm.assign_ms * 1e3 / max(tm.calls, 1)
-    fused_us = tm.fused_ms * 1e3 / max(tm.fused_calls, 1) if tm.fused_calls else None
-    # dominant kernel: the fused single-launch placement when it ran, else the tally
-    if fused_us is not None:
-        dom_kernel, dom_us = "place_fused_kernel", fused_us
-        tb = tally_bytes(p) + placement_tail_bytes(p)
+    # dominant kernel: the step's single launch (compaction / fused), else the tally
+    if shape in (1, 2):
+        dom_us = event_loop_us(step, args.steps, stream)
+        tb = compact_bytes(p) if shape == 2 else tally_bytes(p) + placement_tail_bytes(p)
     else:
-        dom_kernel, dom_us = "tally_kernel", tally_us
+        cap = torch.empty((len(p.classes) + 1, p.topology.n_leaves), dtype=torch.int32, device="cuda")
+        dom_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
+                                                        stream), args.steps, stream)
         tb = tally_bytes(p)
     achieved = tb / (dom_us * 1e-6) / 1e9
+    traffic = pmc_traffic(KERNEL[shape], 2)
 
     # ------------------------------------------------ p99 recovery latency (host API, trial snapshots)
     lat = []
@@ -163,6 +213,34 @@ def main() -> None:
                "sample": f"config 2 placed {n} times in {dt:.1f} s by oracle/cpu_ref.c (1 thread, -O2), "
                          f"same snapshot and rules"}
 
+    # ------------------------------------------------ configs 1, 3, 5 (one GPU, device-resident)
+    configs = None
+    if rank == 0 and not args.no_configs:
+        configs = {}
+        for cfg in (1, 3, 5):
+            pc = synth.CONFIGS[cfg]()
+            eng.load(pc)
+            r = eng.place(pc.job_class)
+            st, _ = device_step(pc)
+            for _ in range(5):
+                st()
+            us = event_loop_us(st, 50, stream)
+            line = {"nodes": pc.nodes.n_nodes, "jobs": pc.n_jobs, "classes": len(pc.classes),
+                    "levels": pc.topology.n_levels, "placed": r.placed, "shape": SHAPES[r.fused],
+                    "us_per_placement": round(us, 2), "placements_per_s": round(r.placed / (us * 1e-6), 1),
+                    "host_api_us": round(r.wall_us, 1)}
+            if world == 1 and args.cpu_seconds > 0:
+                from oracle import oracle as O
+                pk = O.PackedProblem(pc)
+                O.place_c(pc, pk)
+                n, t0c = 0, time.perf_counter()
+                while time.perf_counter() - t0c < min(1.0, args.cpu_seconds / 5):
+                    O.place_c(pc, pk)
+                    n += 1
+                line["cpu_port_us_per_placement"] = round((time.perf_counter() - t0c) * 1e6 / n, 1)
+            configs[f"cfg{cfg}"] = line
+        eng.load(p)
+
     # ------------------------------------------------ config 4: 1M nodes, sharded over the ranks
     cfg4 = None
     if not args.no_cfg4:
@@ -186,15 +264,21 @@ def main() -> None:
         torch.cuda.synchronize()
         t4 = sp.engine.timing(reset=True)
         sp.engine.set_timing(False)
-        t4_us = t4.tally_ms * 1e3 / max(t4.calls - t4.fused_calls, 1) if t4.calls > t4.fused_calls else float("nan")
+        n4 = max(t4.calls - t4.fused_calls, 1)
+        # tally alone, back to back, events around the loop
+        C4, L4 = len(p4.classes), p4.topology.n_leaves
+        cap4 = torch.zeros((C4 + 1, L4), dtype=torch.int32, device="cuda")
+        tally_us = event_loop_us(lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream),
+                                 steps4, stream)
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
                 "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
-                "placed": placed4, "tally_us": round(t4_us, 2),
-                "tally_gbs": round(tb4 / (t4_us * 1e-6) / 1e9, 1),
-                "tally_frac": round(tb4 / (t4_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "feas_us": round(t4.feas_ms * 1e3 / max(t4.calls, 1), 2),
-                "assign_us": round(t4.assign_ms * 1e3 / max(t4.calls, 1), 2),
+                "placed": placed4, "tally_us": round(tally_us, 2),
+                "tally_gbs": round(tb4 / (tally_us * 1e-6) / 1e9, 1),
+                "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "tally_traffic": pmc_traffic("tally_kernel", 4) if world == 1 else None,
+                "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
+                "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
                 "allreduce_us": sp.allreduce_us(), "shards": world}
 
     if rank == 0:
@@ -214,16 +298,18 @@ def main() -> None:
             "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery",
                        "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J,
                        "pods_per_job": p.classes[0].pods, "classes": len(p.classes),
-                       "parallelism": f"replicas{world}"},
+                       "shape": SHAPES[shape], "parallelism": f"replicas{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
-                         "kernel": dom_kernel, "bytes_per_launch": tb, "avg_us": round(dom_us, 3)},
-            "kernels_us": {"fused": round(fused_us, 3) if fused_us else None, "tally": round(tally_us, 3),
-                           "feas": round(feas_us, 3), "assign": round(assign_us, 3)},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5),
+                         "traffic": traffic["bytes"] if traffic else None,
+                         "traffic_source": traffic["source"] if traffic else None,
+                         "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
+                         "note": "latency-bound: one launch moving 0.44 MB; see DESIGN.md §8"},
             "p50_recovery_us": round(pct(0.50), 1) if lat else None,
             "p99_recovery_us": round(pct(0.99), 1) if lat else None,
             "recovery_trials": len(lat),
             "cpu_baseline": cpu,
+            "configs": configs,
             "cfg4_1M": cfg4,
         }
         print(json.dumps(line), flush=True)

@@ -58,6 +58,29 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(p); }
 };
 
+// Pinned, device-mapped host memory: the host placement path hands run lists
+// to the kernels and takes assign[] back through it without DMA copies
+// (kernels read and write it over the host link directly).
+struct HostBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    ~HostBuf() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t reserve(size_t n) {
+        if (n <= bytes && p) return hipSuccess;
+        release();
+        hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) bytes = n ? n : 16;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
     int tag = 0;  // 0 tally, 1 feas, 2 assign, 3 fused
@@ -96,6 +119,8 @@ struct jsp_engine {
 
     // scratch
     DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, recs, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+    HostBuf h_runs, h_assign, h_stats;  // zero-copy staging of the host placement path
+    uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
     int fused_mode = JSP_FUSED_AUTO;
     uint32_t last_shape = 0;  // 0 three launches, 1 fused tail, 2 single-class compaction
 
@@ -219,6 +244,8 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
     return JSP_OK;
 }
 
+uint32_t* stats_ptr(jsp_engine* e) { return e->stats_override ? e->stats_override : e->stats.as<uint32_t>(); }
+
 int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
                 const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
                 int32_t* d_assign, hipStream_t s) {
@@ -232,7 +259,7 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
                                e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
                                d_assign,
-                               e->stats.as<uint32_t>(), e->recs.as<jsp::AssignRec>(), s));
+                               stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(), s));
     ev_end(p, s);
     return JSP_OK;
 }
@@ -265,7 +292,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
         f.n_runs = n_runs;
         f.J = J;
         f.assign = d_assign;
-        f.stats = e->stats.as<uint32_t>();
+        f.stats = stats_ptr(e);
         e->epoch = e->epoch % 0x3FFFFFFFu + 1u;
         f.epoch = e->epoch;
         f.coresident = e->n_blocks <= kCoresidentBlocks ? 1u : 0u;
@@ -294,7 +321,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     f.n_runs = n_runs;
     f.J = J;
     f.assign = d_assign;
-    f.stats = e->stats.as<uint32_t>();
+    f.stats = stats_ptr(e);
     const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
     f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
     f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
@@ -676,19 +703,28 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     hipStream_t s = e->stream;
-    HIP_TRY(upload(e->run_class, run_class, n_runs, s));
-    HIP_TRY(upload(e->run_len, run_len, n_runs, s));
-    HIP_TRY(e->assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
-    if (int rc = place_impl(e, e->run_class.as<uint32_t>(), e->run_len.as<uint32_t>(), n_runs, J,
-                            e->assign.as<int32_t>(), s))
-        return rc;
-    uint32_t st[3] = {0, 0, 0};
-    if (J > 0) HIP_TRY(hipMemcpyAsync(assign_out, e->assign.p, (size_t)J * 4, hipMemcpyDeviceToHost, s));
+    // runs in, assign[] and stats out through pinned mapped host memory: one
+    // launch sequence and one synchronize, no DMA round trips
+    HIP_TRY(e->h_runs.reserve((size_t)std::max<uint32_t>(n_runs, 1) * 8));
+    HIP_TRY(e->h_assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
+    HIP_TRY(e->h_stats.reserve(16));
+    uint32_t* h_rc = e->h_runs.as<uint32_t>();
+    uint32_t* h_rl = h_rc + std::max<uint32_t>(n_runs, 1);
+    if (n_runs > 0) {
+        std::memcpy(h_rc, run_class, (size_t)n_runs * 4);
+        std::memcpy(h_rl, run_len, (size_t)n_runs * 4);
+    }
+    e->stats_override = e->h_stats.as<uint32_t>();
+    const int prc = place_impl(e, h_rc, h_rl, n_runs, J, e->h_assign.as<int32_t>(), s);
+    e->stats_override = nullptr;
+    if (prc) return prc;
     if (tally_out && e->C > 0)
         HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
     if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(st, e->stats.p, sizeof st, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    if (J > 0) std::memcpy(assign_out, e->h_assign.p, (size_t)J * 4);
+    uint32_t st[3];
+    std::memcpy(st, e->h_stats.p, sizeof st);
     if (e->last_shape == 2 && st[2] != 0)
         return set_err(JSP_EHIP, "compaction look-back timed out (a workgroup never published its count)");
     if (stats) {

@@ -560,7 +560,8 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                              const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
                              uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
-                             uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs) {
+                             uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs,
+                             uint32_t* __restrict__ rec_count) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t K = topo.K;
     // wave 0: class state in registers, lane c = class c (C <= kMaxClasses = 64)
@@ -631,28 +632,30 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                         const uint32_t incl = wave_incl_scan(cnt, lane);
                         const uint32_t pre = incl - cnt;
                         const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                        uint32_t last = 0;
-                        if (bits && pre < need) {
-                            uint32_t r = pre;
-                            uint64_t took = 0;
-                            while (bits && r < need) {
-                                const uint32_t b = __builtin_ctzll(bits);
-                                bits &= bits - 1;
-                                const uint32_t d = w * 64 + b;
-                                assign[jpos + r] = (int32_t)d;
-                                took |= 1ull << b;
+                        // emission, one useful word at a time, its bits across the
+                        // lanes: lane b takes bit b at rank pre_k + (bits below b)
+                        uint64_t todo = __ballot(cnt != 0 && pre < need);
+                        uint32_t next = ((cur >> 6) + 64) * 64;
+                        while (todo) {
+                            const int k = __builtin_ctzll(todo);
+                            todo &= todo - 1;
+                            const uint32_t blo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, k);
+                            const uint32_t bhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), k);
+                            const uint64_t wbits = ((uint64_t)bhi << 32) | blo;
+                            const uint32_t rank = (uint32_t)__builtin_amdgcn_readlane((int)pre, k) +
+                                                  (uint32_t)__popcll(wbits & ((1ull << lane) - 1ull));
+                            const bool take = ((wbits >> lane) & 1ull) && rank < need;
+                            const uint32_t d = ((cur >> 6) + (uint32_t)k) * 64 + (uint32_t)lane;
+                            if (take) {
+                                assign[jpos + rank] = (int32_t)d;
                                 if (K > 1) mark_other_levels<TOPO_LDS>(d, lvl, K, topo, s_taken, m, s_topo);
-                                last = d;
-                                ++r;
                             }
-                            Tk[w] |= took;
+                            const uint64_t took = __ballot(take);
+                            if (lane == k) Tk[w] |= took;  // lane k owns word k of the window
+                            const uint64_t lastm = __ballot(take && rank + 1 == need);
+                            if (lastm) next = (uint32_t)__builtin_amdgcn_readlane((int)d, __builtin_ctzll(lastm)) + 1;
                         }
-                        if (total >= need) {  // the lane holding rank need-1 names the next cursor
-                            const uint64_t hit = __ballot(cnt != 0 && pre < need && pre + cnt >= need);
-                            cur = (uint32_t)__builtin_amdgcn_readlane((int)last, __builtin_ctzll(hit)) + 1;
-                        } else {
-                            cur = ((cur >> 6) + 64) * 64;
-                        }
+                        cur = next;
                         const uint32_t used = total < need ? total : need;
                         need -= used;
                         jpos += used;
@@ -679,8 +682,8 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
     if (tid == 0 && stats != nullptr) {
         stats[0] = n_runs;
         stats[1] = placed;
-        stats[3] = m.s_misc[1];  // records for expand_kernel
     }
+    if (tid == 0 && rec_count != nullptr) *rec_count = m.s_misc[1];  // records for expand_kernel
     JSP_STAMP(4000u, 7);
 }
 
@@ -690,7 +693,8 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     const uint64_t* __restrict__ feas, const uint32_t* __restrict__ word_off, const DevClass* __restrict__ cls,
     uint32_t C, TopoDev topo, const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
     uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats, uint32_t feas_words,
-    uint32_t feas_in_lds, uint32_t topo_in_lds, uint32_t topo_words, uint32_t stage_cap, AssignRec* __restrict__ recs) {
+    uint32_t feas_in_lds, uint32_t topo_in_lds, uint32_t topo_words, uint32_t stage_cap, AssignRec* __restrict__ recs,
+    uint32_t* __restrict__ rec_count) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const uint32_t tw = taken_words(topo);
     uint64_t* s_win = s_dyn + tw;
@@ -711,18 +715,19 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     const uint64_t* F = feas_in_lds ? s_feas : feas;
     if (topo_in_lds)
         assign_block<kAssignThreads, true>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m, s_topo,
-                                           s_win, s_stage, stage_cap, recs);
+                                           s_win, s_stage, stage_cap, recs, rec_count);
     else
         assign_block<kAssignThreads, false>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m,
-                                            s_topo, s_win, s_stage, stage_cap, recs);
+                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count);
 }
 
 // Expansion of assign_kernel's records (grid-stride, one wave per record):
 // lane b of a record with bit b taken writes job base + (taken bits below b).
 // Each record's jobs are consecutive, so a wave's stores are one run.
 __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict__ recs,
-                                                     const uint32_t* __restrict__ stats, int32_t* __restrict__ assign) {
-    const uint32_t n = stats[3];
+                                                     const uint32_t* __restrict__ rec_count,
+                                                     int32_t* __restrict__ assign) {
+    const uint32_t n = *rec_count;
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t waves = gridDim.x * (blockDim.x >> 6);
     for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
@@ -787,10 +792,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     __syncthreads();
     if (f.topo_in_lds)
         assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
-                                          f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr);
+                                          f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
     else
         assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
-                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr);
+                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
 }
 
 // ----------------------------------------------------------------- single-class compaction
@@ -1040,17 +1045,17 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                         AssignRec* recs, hipStream_t s) {
+                         uint32_t* rec_count, AssignRec* recs, hipStream_t s) {
     const uint32_t topo_words = topo.K > 1 ? topo_table_words(topo.K, topo.D) : 0u;
     const AssignPlan p = plan_assign(t_words, feas_words, topo_words);
     if (p.lds_bytes == 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
                        run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
-                       topo_words, p.stage_cap, recs);
+                       topo_words, p.stage_cap, recs, rec_count);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
     // records never outnumber the placed jobs (each taken domain is in one record)
     const uint32_t waves = J < 8192u ? J : 8192u;
-    hipLaunchKernelGGL(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, stats, assign);
+    hipLaunchKernelGGL(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, assign);
     return hipGetLastError();
 }
 
