@@ -15,6 +15,7 @@ constexpr int kTallyClasses = 16;                  // classes per tally pass
 constexpr int kAssignThreads = 1024;               // 16 waves, one workgroup
 constexpr int kAssignWaves = kAssignThreads / 64;
 constexpr int kMaxClasses = 64;
+constexpr uint32_t kMaxLevels = 4;                 // JSP_MAX_LEVELS
 constexpr uint32_t kMaxTakenWords = 16384;         // 128 KiB of LDS: 1M domain bits over all levels
 
 // Device copy of a jsp_job_class, pre-digested for the tally's inner loop:

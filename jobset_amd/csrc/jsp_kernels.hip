@@ -249,6 +249,102 @@ __device__ __forceinline__ uint64_t feas_word(const uint32_t* __restrict__ cap, 
     return __ballot(ok);
 }
 
+// Inclusive wave64 prefix sum of a 64-bit value: the DPP steps of
+// wave_incl_scan on both halves, carry propagated from the low half.
+__device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
+    uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+#define JSP_SCAN64_STEP(CTRL, RM)                                                              \
+    {                                                                                          \
+        const uint32_t a = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, CTRL, RM, 0xf, false); \
+        const uint32_t b = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, CTRL, RM, 0xf, false); \
+        const uint32_t n = lo + a;                                                             \
+        hi += b + (n < lo ? 1u : 0u);                                                          \
+        lo = n;                                                                                \
+    }
+    JSP_SCAN64_STEP(0x111, 0xf)
+    JSP_SCAN64_STEP(0x112, 0xf)
+    JSP_SCAN64_STEP(0x114, 0xf)
+    JSP_SCAN64_STEP(0x118, 0xf)
+    JSP_SCAN64_STEP(0x142, 0xa)
+    JSP_SCAN64_STEP(0x143, 0xc)
+#undef JSP_SCAN64_STEP
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// Feasibility word w of class c at a level above the leaves. Lane i owns
+// domain 64w + i with leaves [lo_i, hi_i); the word's leaves [A, B) are one
+// contiguous range, which the wave streams in coalesced 64-leaf chunks
+// (kUpperBatch chunks of loads in flight at once). A 64-bit running prefix of
+// min(cap, pods) — the clamp keeps `capsum >= pods` exact — and a 32-bit one of
+// occ give each lane P(hi_i) when hi_i falls in a chunk; P(lo_i) is the
+// previous lane's P(hi). One pass, no per-domain serial loops, so a zone of
+// thousands of racks costs ~(leaves / 512) memory round trips, not one per leaf.
+constexpr int kUpperBatch = 8;
+__device__ uint64_t feas_word_upper(const uint32_t* __restrict__ cap, const uint32_t* __restrict__ occ, uint32_t ld,
+                                    uint32_t lvl, uint32_t pods, uint32_t c, uint32_t w, const TopoDev& topo,
+                                    int lane) {
+    const uint32_t D = topo.D[lvl];
+    const uint32_t d0 = w * 64;
+    const uint32_t nd = (D - d0) < 64u ? (D - d0) : 64u;
+    const uint32_t* fl = topo.fl[lvl];
+    const uint32_t hi_i = (uint32_t)lane < nd ? fl[d0 + lane + 1] : 0u;
+    const uint32_t A = fl[d0];
+    const uint32_t B = (uint32_t)__builtin_amdgcn_readlane((int)hi_i, (int)nd - 1);
+    const uint32_t* cp = cap + (size_t)c * ld;
+    uint64_t carry = 0, p_hi = 0;
+    uint32_t ocarry = 0, o_hi = 0;
+    for (uint32_t base = A; base < B; base += 64u * kUpperBatch) {
+        uint32_t v[kUpperBatch], o[kUpperBatch];
+#pragma unroll
+        for (int u = 0; u < kUpperBatch; ++u) {
+            const uint32_t leaf = base + 64u * u + (uint32_t)lane;
+            v[u] = 0;
+            o[u] = 0;
+            if (leaf < B) {
+                const uint32_t x = cp[leaf];
+                v[u] = x < pods ? x : pods;
+                o[u] = occ[leaf];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUpperBatch; ++u) {
+            const uint32_t sb = base + 64u * u;
+            if (sb >= B) break;  // wave-uniform
+            const uint64_t s = wave_incl_scan64(v[u]);
+            const uint32_t os = wave_incl_scan(o[u], lane);
+            // P(hi_i) = carry + s[hi_i - 1 - sb] when hi_i in (sb, sb + 64]
+            const bool mine = hi_i > sb && hi_i <= sb + 64u;
+            const int src = mine ? (int)(hi_i - 1 - sb) : 0;
+            const uint32_t slo = (uint32_t)__shfl((int)(uint32_t)s, src, 64);
+            const uint32_t shi = (uint32_t)__shfl((int)(uint32_t)(s >> 32), src, 64);
+            const uint32_t so = (uint32_t)__shfl((int)os, src, 64);
+            if (mine) {
+                p_hi = carry + (((uint64_t)shi << 32) | slo);
+                o_hi = ocarry + so;
+            }
+            carry += ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(s >> 32), 63) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)s, 63);
+            ocarry += (uint32_t)__builtin_amdgcn_readlane((int)os, 63);
+        }
+    }
+    // P(lo_i) = P(hi_{i-1}); P(A) = 0. Empty domains read equal prefixes.
+    const uint32_t plo_l = (uint32_t)__shfl_up((int)(uint32_t)p_hi, 1, 64);
+    const uint32_t plo_h = (uint32_t)__shfl_up((int)(uint32_t)(p_hi >> 32), 1, 64);
+    const uint32_t olo_s = (uint32_t)__shfl_up((int)o_hi, 1, 64);
+    const uint64_t p_lo = lane == 0 ? 0ull : (((uint64_t)plo_h << 32) | plo_l);
+    const uint32_t o_lo = lane == 0 ? 0u : olo_s;
+    const bool ok = (uint32_t)lane < nd && (p_hi - p_lo) >= pods && (o_hi - o_lo) == 0u;
+    return __ballot(ok);
+}
+
+// Word w of class c at its level, leaves or above.
+__device__ __forceinline__ uint64_t feas_word_any(const uint32_t* __restrict__ cap, const uint32_t* __restrict__ occ,
+                                                  uint32_t ld, uint32_t lvl, uint32_t pods, uint32_t c, uint32_t w,
+                                                  const TopoDev& topo, int lane) {
+    if (lvl + 1 < topo.K) return feas_word_upper(cap, occ, ld, lvl, pods, c, w, topo, lane);
+    return feas_word(cap, occ, ld, lvl, pods, c, w, topo, lane);
+}
+
 __global__ __launch_bounds__(256) void feas_kernel(const uint32_t* __restrict__ cap,
                                                    const uint32_t* __restrict__ occ, uint32_t ld,
                                                    const DevClass* __restrict__ cls, uint32_t C,
@@ -259,7 +355,7 @@ __global__ __launch_bounds__(256) void feas_kernel(const uint32_t* __restrict__ 
     if (gw >= word_off[C]) return;
     uint32_t c = 0;
     while (word_off[c + 1] <= gw) ++c;  // wave-uniform, C <= 64
-    const uint64_t word = feas_word(cap, occ, ld, cls[c].level, cls[c].pods, c, gw - word_off[c], topo, lane);
+    const uint64_t word = feas_word_any(cap, occ, ld, cls[c].level, cls[c].pods, c, gw - word_off[c], topo, lane);
     if (lane == 0) feas[gw] = word;
 }
 
@@ -549,6 +645,124 @@ __device__ uint32_t long_run(uint32_t c, uint32_t j0, uint32_t jend, const uint6
     return cur < D ? cur : D;
 }
 
+// ---- register-resident walker for small hierarchies: when the taken
+// bitmaps of all levels together are <= 64 words (s_taken's layout: level k at
+// words [toff_k, toff_k + nw_k)), wave 0 keeps them in one register, lane w =
+// word w, so a short run touches no LDS state. The only memory access per job
+// is its class's feasibility word, loaded one run ahead. Taking a domain marks
+// its descendants at once (ranges from the child_start tables); its ancestors
+// are marked lazily: taken bits below level 0 stay pending until a job at a
+// coarser level, or a long run, needs them, and are then folded upwards (one
+// parent lookup per distinct parent per word) through the LDS image s_taken.
+constexpr uint32_t kRegMaxWords = 64;
+
+struct RegState {
+    uint64_t T;  // taken (lane w: word w of the concatenated level bitmaps)
+    uint64_t P;  // taken directly at a level >= 1, ancestors not yet marked
+    int pend;    // highest level with pending bits, -1 none (wave-uniform)
+};
+
+// bits of [lo, hi) in word `wi` (domains [64 wi, 64 wi + 64))
+__device__ __forceinline__ uint64_t range_word(uint32_t wi, uint32_t lo, uint32_t hi) {
+    const uint32_t w0 = wi * 64, a = lo > w0 ? lo : w0, b = hi < w0 + 64 ? hi : w0 + 64;
+    if (a >= b) return 0ull;
+    const uint32_t n = b - a;
+    return (n == 64 ? ~0ull : ((1ull << n) - 1ull)) << (a - w0);
+}
+
+template <bool TOPO_LDS>
+__device__ __forceinline__ uint32_t topo_cs(const TopoDev& topo, const uint32_t* s_topo, const AssignMeta& m,
+                                            uint32_t k, uint32_t i) {
+    if constexpr (TOPO_LDS) return s_topo[m.s_coff[k] + i];
+    else return topo.cs[k][i];
+}
+
+template <bool TOPO_LDS>
+__device__ __forceinline__ uint32_t topo_par(const TopoDev& topo, const uint32_t* s_topo, const AssignMeta& m,
+                                             uint32_t k, uint32_t i) {
+    if constexpr (TOPO_LDS) return s_topo[m.s_poff[k] + i];
+    else return (uint32_t)topo.par[k][i];
+}
+
+__device__ __forceinline__ uint64_t reg_load_f(const uint64_t* __restrict__ feas, uint32_t rc_l, uint32_t q, uint32_t C,
+                                               uint32_t my_toff, uint32_t my_woff, uint32_t my_nw, int lane) {
+    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
+    if (c >= C) return 0ull;
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)my_toff, (int)c);
+    const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)my_nw, (int)c);
+    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)my_woff, (int)c);
+    const uint32_t wi = (uint32_t)lane - t0;  // wraps for lanes below the level
+    return wi < nw ? feas[wo + wi] : 0ull;
+}
+
+// Mark the descendants of every taken bit of `took` (level lvl, its words at
+// lanes [t0, ...)) at all finer levels: contiguous taken bits of one word are
+// one domain range, whose descendants are one range per level.
+template <bool TOPO_LDS>
+__device__ void reg_mark_desc(RegState& s, uint64_t took, uint32_t lvl, uint32_t t0, uint32_t K, const TopoDev& topo,
+                              const uint32_t* s_topo, const AssignMeta& m, int lane) {
+    uint64_t lanes = __ballot(took != 0);
+    while (lanes) {
+        const int k = __builtin_ctzll(lanes);
+        lanes &= lanes - 1;
+        uint64_t word = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(took >> 32), k) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)took, k);
+        while (word) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(word);
+            const uint64_t sh = word >> b;
+            const uint32_t len = ~sh == 0ull ? 64u - b : (uint32_t)__builtin_ctzll(~sh);
+            word &= len >= 64u ? 0ull : ~(((1ull << len) - 1ull) << b);
+            uint32_t lo = ((uint32_t)k - t0) * 64 + b, hi = lo + len;
+            for (uint32_t kk = lvl + 1; kk < K; ++kk) {
+                lo = topo_cs<TOPO_LDS>(topo, s_topo, m, kk - 1, lo);
+                hi = topo_cs<TOPO_LDS>(topo, s_topo, m, kk - 1, hi);
+                const uint32_t tk = m.s_toff[kk], nwk = (m.s_D[kk] + 63) >> 6;
+                const uint32_t wi = (uint32_t)lane - tk;
+                if (wi < nwk) s.T |= range_word(wi, lo, hi);
+            }
+        }
+    }
+}
+
+// Fold the pending bits into their ancestors, finest level first, so marks
+// made at level k-1 propagate further up. Lanes scatter the ancestor bits
+// into other lanes' words with LDS atomics on the image s_taken (written from
+// the register first, read back after); one parent lookup per distinct parent
+// per word (parents are monotone: skip the bits below the next parent's first
+// child).
+template <bool TOPO_LDS>
+__device__ void reg_flush(RegState& s, uint32_t K, const TopoDev& topo, uint64_t* s_taken, uint32_t t_words,
+                          const uint32_t* s_topo, const AssignMeta& m, int lane) {
+    if ((uint32_t)lane < t_words) s_taken[lane] = s.T;
+    for (uint32_t kk = K - 1; kk >= 1; --kk) {
+        const uint32_t tk = m.s_toff[kk], nwk = (m.s_D[kk] + 63) >> 6;
+        const uint32_t wi = (uint32_t)lane - tk;
+        uint64_t pb = wi < nwk ? s.P : 0ull;
+        if (__ballot(pb != 0) == 0) continue;
+        const uint32_t tu = m.s_toff[kk - 1], nwu = (m.s_D[kk - 1] + 63) >> 6;
+        const uint64_t before = s.T;
+        while (__ballot(pb != 0)) {
+            if (pb) {
+                const uint32_t d = wi * 64 + (uint32_t)__builtin_ctzll(pb);
+                const uint32_t p = topo_par<TOPO_LDS>(topo, s_topo, m, kk, d);
+                lds_set_bit(s_taken + tu, p);
+                const uint32_t end = topo_cs<TOPO_LDS>(topo, s_topo, m, kk - 1, p + 1);  // p's children end
+                const uint32_t w0 = wi * 64;
+                pb = end >= w0 + 64 ? 0ull : pb & (~0ull << (end - w0));
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if ((uint32_t)lane < t_words) s.T = s_taken[lane];
+        if (wi < nwk) s.P = 0;  // level kk done
+        const uint32_t wu = (uint32_t)lane - tu;
+        if (kk - 1 >= 1 && wu < nwu) s.P |= s.T & ~before;  // new marks propagate further up
+        if (kk == 1) break;
+    }
+    s.pend = -1;
+}
+
 // Runs walk (A7). Requires stage_meta (+ stage_topo when TOPO_LDS) and a
 // barrier first, s_taken zeroed, and `feas` holding every class's bitmap words
 // (LDS or global). Jobs are taken in global order, run by run; a run of class
@@ -574,6 +788,14 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
         my_cur = m.s_cursor[lane];
     }
     uint32_t placed = 0, jbase = 0;
+    // register mode: the taken bitmaps of all levels fit one word per lane
+    const uint32_t t_words = m.s_toff[K];
+    const bool regmode = t_words <= kRegMaxWords;
+    RegState rs;
+    rs.T = rs.P = 0;  // s_taken starts zeroed
+    rs.pend = -1;
+    uint32_t my_nw = 0;  // wave 0, lane c: bitmap words of class c's level
+    if (wid == 0 && (uint32_t)lane < C) my_nw = (my_D + 63) >> 6;
     for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
         // ---- a tile of runs: job offsets (block scan of run lengths) and the long-run list
         const uint32_t ri = r0 + tid;
@@ -588,7 +810,89 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
         if (is_long) m.s_long[lrank] = (uint32_t)tid;
         __syncthreads();
         const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
-        if (wid == 0) {
+        if (wid == 0 && regmode) {
+            for (uint32_t t0 = 0; t0 < nr; t0 += 64) {
+                const uint32_t tl = t0 + (uint32_t)lane;
+                const uint32_t rc_l = tl < nr ? m.s_rc[tl] : 0u;
+                const uint32_t ro_l = tl < nr ? m.s_ro[tl] : 0u;
+                const uint32_t rn_l = tl + 1 < nr ? m.s_ro[tl + 1] : tile_total;
+                const uint32_t nb = (nr - t0) < 64u ? (nr - t0) : 64u;
+                // feasibility word of run q's class for this lane (0 outside its level),
+                // loaded one run ahead so it is in flight while the previous run is placed
+                JSP_STAMP(4010u + t0 / 64, 0);
+                uint64_t f_next = reg_load_f(feas, rc_l, 0, C, my_toff, my_woff, my_nw, lane);
+                for (uint32_t q = 0; q < nb; ++q) {
+                    const uint64_t f = f_next;
+                    if (q + 1 < nb) f_next = reg_load_f(feas, rc_l, q + 1, C, my_toff, my_woff, my_nw, lane);
+                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
+                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)ro_l, (int)q);
+                    const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)rn_l, (int)q);
+                    const uint32_t j0 = jbase + o0;
+                    const uint32_t jend = jbase + o1 < J ? jbase + o1 : J;
+                    if (j0 >= jend) continue;
+                    if (c >= C) {  // malformed run: its jobs are unplaceable
+                        for (uint32_t j = j0 + lane; j < jend; j += 64) assign[j] = -1;
+                        continue;
+                    }
+                    const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
+                    const uint32_t t0l = (uint32_t)__builtin_amdgcn_readlane((int)my_toff, (int)c);
+                    if (o1 - o0 > kWaveRunMax) {
+                        // long run: fold pending ancestors, publish the bitmaps, join the
+                        // workgroup (cursor 0: the whole level is one window), reload
+                        if (rs.pend >= 1) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
+                        if ((uint32_t)lane < t_words) s_taken[lane] = rs.T;
+                        if (lane == 0) m.s_cursor[c] = 0;
+                        long_run<NT, TOPO_LDS>(c, j0, jend, feas, topo, assign, s_taken, m, s_topo, s_win, s_stage,
+                                               stage_cap, recs, placed);
+                        if ((uint32_t)lane < t_words) rs.T = s_taken[lane];
+                        continue;
+                    }
+                    if (rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
+                    const uint64_t avail = f & ~rs.T;
+                    const uint32_t n = jend - j0;
+                    uint64_t took = 0;
+                    if (n == 1) {
+                        const uint64_t nz = __ballot(avail != 0);
+                        if (nz == 0) {
+                            if (lane == 0) assign[j0] = -1;
+                        } else {
+                            const int k = __builtin_ctzll(nz);
+                            const uint64_t word =
+                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(avail >> 32), k) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)avail, k);
+                            const uint32_t b = (uint32_t)__builtin_ctzll(word);
+                            if (lane == 0) assign[j0] = (int32_t)(((uint32_t)k - t0l) * 64 + b);
+                            took = lane == k ? (1ull << b) : 0ull;
+                            placed += 1;
+                        }
+                    } else {
+                        const uint32_t cnt = (uint32_t)__popcll(avail);
+                        const uint32_t incl = wave_incl_scan(cnt, lane);
+                        const uint32_t pre = incl - cnt;
+                        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                        const uint32_t used = total < n ? total : n;
+                        if (cnt != 0 && pre < used)
+                            took = pre + cnt <= used ? avail : avail & ((1ull << select_bit(avail, used - pre)) - 1ull);
+                        uint64_t x = took;
+                        uint32_t r = j0 + pre;
+                        while (x) {
+                            assign[r++] = (int32_t)(((uint32_t)lane - t0l) * 64 + (uint32_t)__builtin_ctzll(x));
+                            x &= x - 1;
+                        }
+                        for (uint32_t j = j0 + used + lane; j < jend; j += 64) assign[j] = -1;
+                        placed += used;
+                    }
+                    rs.T |= took;
+                    if (lvl >= 1) {
+                        rs.P |= took;
+                        rs.pend = rs.pend > (int)lvl ? rs.pend : (int)lvl;
+                    }
+                    if (lvl + 1 < K) reg_mark_desc<TOPO_LDS>(rs, took, lvl, t0l, K, topo, s_topo, m, lane);
+                    if (q == 15 || q == 31 || q == 47) JSP_STAMP(4010u + t0 / 64, 1 + q / 16);
+                }
+                JSP_STAMP(4010u + t0 / 64, 4);
+            }
+        } else if (wid == 0) {
             for (uint32_t t0 = 0; t0 < nr; t0 += 64) {
                 const uint32_t tl = t0 + (uint32_t)lane;
                 const uint32_t rc_l = tl < nr ? m.s_rc[tl] : 0u;
@@ -780,14 +1084,43 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
-    // feasibility bitmaps of every class into LDS
+    // feasibility bitmaps of every class into LDS. The tallies were written by
+    // other workgroups (after the acquire every load misses to HBM/MALL), so a
+    // wave issues the loads of kTailBatch leaf-level words before it uses any.
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (uint32_t gw = wid; gw < f.feas_words; gw += kTallyWaves) {
-        uint32_t c = 0;
-        while (m.s_woff[c + 1] <= gw) ++c;
-        const uint64_t word = feas_word(a.cap_out, a.occ_out, a.ld, m.s_lvl[c], m.s_pods[c], c, gw - m.s_woff[c],
-                                        f.topo, lane);
-        if (lane == 0) s_feas[gw] = word;
+    constexpr int kTailBatch = 8;
+    const uint32_t Kt = f.topo.K;
+    for (uint32_t g0 = wid; g0 < f.feas_words; g0 += kTallyWaves * kTailBatch) {
+        uint32_t cv[kTailBatch], ov[kTailBatch], cc[kTailBatch];
+#pragma unroll
+        for (int u = 0; u < kTailBatch; ++u) {
+            const uint32_t gw = g0 + (uint32_t)u * kTallyWaves;
+            cv[u] = 0;
+            ov[u] = 1;
+            cc[u] = 0;
+            if (gw < f.feas_words) {
+                uint32_t c = 0;
+                while (m.s_woff[c + 1] <= gw) ++c;
+                cc[u] = c;
+                const uint32_t lvl = m.s_lvl[c];
+                const uint32_t d = (gw - m.s_woff[c]) * 64 + (uint32_t)lane;
+                if (lvl + 1 == Kt && d < f.topo.D[lvl]) {
+                    cv[u] = a.cap_out[(size_t)c * a.ld + d];
+                    ov[u] = a.occ_out[d];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kTailBatch; ++u) {
+            const uint32_t gw = g0 + (uint32_t)u * kTallyWaves;
+            if (gw >= f.feas_words) break;
+            const uint32_t c = cc[u], lvl = m.s_lvl[c];
+            const uint64_t word =
+                lvl + 1 == Kt ? __ballot(cv[u] >= m.s_pods[c] && ov[u] == 0)
+                              : feas_word_upper(a.cap_out, a.occ_out, a.ld, lvl, m.s_pods[c], c, gw - m.s_woff[c],
+                                                f.topo, lane);
+            if (lane == 0) s_feas[gw] = word;
+        }
     }
     __syncthreads();
     if (f.topo_in_lds)
