@@ -7,6 +7,7 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -142,7 +143,21 @@ struct jsp_engine {
 
 namespace {
 
-constexpr uint32_t kTargetBlockRows = jsp::kChunkRows - 4;  // one chunk even when unaligned
+constexpr uint32_t kMaxBlockChunks = 8;
+
+// 1024-row chunks per tally workgroup. One: measured on MI355X (cfg4, 1M rows,
+// C=4) the tally takes 14.2 / 18.9 / 23.2 / 28.4 / 39.2 us at 1/2/3/4/8 chunks
+// per workgroup -- the chunk's row/leaf passes, not its HBM loads, set a
+// workgroup's time, and more, smaller-grid workgroups hide each other's
+// latency better than a next-chunk prefetch does. JSP_BLOCK_CHUNKS overrides
+// it (tuning experiments; the parity tests cover 2, 3 and 8).
+uint32_t block_chunks(uint32_t /*N*/) {
+    if (const char* v = std::getenv("JSP_BLOCK_CHUNKS")) {
+        const long x = std::strtol(v, nullptr, 10);
+        if (x >= 1 && x <= (long)kMaxBlockChunks) return (uint32_t)x;
+    }
+    return 1;
+}
 constexpr size_t kMaxEvents = 3 * 4096;
 // Above this many tally workgroups the three-launch shape wins: the fused tail
 // runs feasibility + assignment on one 256-thread workgroup.
@@ -523,13 +538,17 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
         if (ls[l] > ls[l + 1]) return set_err(JSP_EINVAL, "leaf_start not monotone at %u", l);
         max_rows = std::max(max_rows, ls[l + 1] - ls[l]);
     }
-    // workgroup partition: whole leaves, ~one 1024-row chunk and <= 256 leaves each
+    // workgroup partition: whole leaves, <= 256 leaves each, block_chunks()
+    // 1024-row chunks each (a workgroup with several prefetches its next
+    // chunk's rows while it evaluates one)
+    const uint32_t chunks = block_chunks(N);
+    const uint32_t target_rows = chunks * (uint32_t)jsp::kChunkRows - 4;  // fits even when unaligned
     std::vector<uint32_t> blk{0};
     {
         uint32_t rows = 0, leaves = 0;
         for (uint32_t l = 0; l < NL; ++l) {
             const uint32_t r = ls[l + 1] - ls[l];
-            if (leaves > 0 && (rows + r > kTargetBlockRows || leaves == (uint32_t)jsp::kMaxBlkLeaves)) {
+            if (leaves > 0 && (rows + r > target_rows || leaves == (uint32_t)jsp::kMaxBlkLeaves)) {
                 blk.push_back(l);
                 rows = 0;
                 leaves = 0;

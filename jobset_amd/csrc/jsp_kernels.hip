@@ -95,6 +95,45 @@ __host__ __device__ constexpr int tally_lds_words(int nv) { return tally_pre_off
 // prefix(last row in chunk) - prefix(row before first in chunk) of its leaf
 // (plus the earlier waves' totals) to acc[v][leaf]; the leaf is owned by that
 // thread, so no atomics.
+// One thread's 4 consecutive rows of every column (16-B loads).
+template <int W, int R>
+struct RowRegs {
+    uint64_t lab[W][4];
+    uint32_t tn[4], fr[R][4];
+    int32_t ex[4];
+};
+
+template <int W, int R>
+__device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool any, RowRegs<W, R>& x) {
+    if (any) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const ulonglong2* p = reinterpret_cast<const ulonglong2*>(a.labels + (size_t)w * a.npad + row);
+            const ulonglong2 u = p[0], v = p[1];
+            x.lab[w][0] = u.x; x.lab[w][1] = u.y; x.lab[w][2] = v.x; x.lab[w][3] = v.y;
+        }
+        const uint4 t4 = *reinterpret_cast<const uint4*>(a.taints + row);
+        x.tn[0] = t4.x; x.tn[1] = t4.y; x.tn[2] = t4.z; x.tn[3] = t4.w;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint4 f4 = *reinterpret_cast<const uint4*>(a.freer + (size_t)r * a.npad + row);
+            x.fr[r][0] = f4.x; x.fr[r][1] = f4.y; x.fr[r][2] = f4.z; x.fr[r][3] = f4.w;
+        }
+        const int4 e4 = *reinterpret_cast<const int4*>(a.excl + row);
+        x.ex[0] = e4.x; x.ex[1] = e4.y; x.ex[2] = e4.z; x.ex[3] = e4.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+            for (int w = 0; w < W; ++w) x.lab[w][i] = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) x.fr[r][i] = 0;
+            x.tn[i] = 0;
+            x.ex[i] = -1;
+        }
+    }
+}
+
 template <int W, int R>
 __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
     const int nc = (int)a.nc;
@@ -117,45 +156,33 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
         for (int i = tid; i < nc * (int)(sizeof(DevClass) / 16); i += kTallyThreads) dst[i] = src[i];
     }
 
-    for (uint32_t base = r0 & ~3u; base < r1; base += kChunkRows) {
-        // ---- issue this chunk's row loads before any barrier
+    // A workgroup of a large snapshot owns several chunks: the next chunk's rows
+    // are loaded (into a second register set) before this chunk is evaluated,
+    // so its HBM latency hides behind the row and leaf passes.
+    const uint32_t base0 = r0 & ~3u;
+    RowRegs<W, R> cur;
+    {
+        const uint32_t row = base0 + 4u * tid;
+        load_rows<W, R>(a, row, (row < r1) && (row + 3 >= r0), cur);
+    }
+    for (uint32_t base = base0; base < r1; base += kChunkRows) {
         const uint32_t row = base + 4u * tid;
         const bool any = (row < r1) && (row + 3 >= r0);
-        uint64_t lab[W][4];
-        uint32_t tn[4], fr[R][4];
-        int32_t ex[4];
-        if (any) {
-#pragma unroll
-            for (int w = 0; w < W; ++w) {
-                const ulonglong2* p = reinterpret_cast<const ulonglong2*>(a.labels + (size_t)w * a.npad + row);
-                const ulonglong2 x = p[0], y = p[1];
-                lab[w][0] = x.x; lab[w][1] = x.y; lab[w][2] = y.x; lab[w][3] = y.y;
-            }
-            const uint4 t4 = *reinterpret_cast<const uint4*>(a.taints + row);
-            tn[0] = t4.x; tn[1] = t4.y; tn[2] = t4.z; tn[3] = t4.w;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const uint4 f4 = *reinterpret_cast<const uint4*>(a.freer + (size_t)r * a.npad + row);
-                fr[r][0] = f4.x; fr[r][1] = f4.y; fr[r][2] = f4.z; fr[r][3] = f4.w;
-            }
-            const int4 e4 = *reinterpret_cast<const int4*>(a.excl + row);
-            ex[0] = e4.x; ex[1] = e4.y; ex[2] = e4.z; ex[3] = e4.w;
-        } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-#pragma unroll
-                for (int w = 0; w < W; ++w) lab[w][i] = 0;
-#pragma unroll
-                for (int r = 0; r < R; ++r) fr[r][i] = 0;
-                tn[i] = 0;
-                ex[i] = -1;
-            }
-        }
         bool valid[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) valid[i] = any && (row + i >= r0) && (row + i < r1);
         __syncthreads();  // s_cls / s_ls / s_acc ready (first chunk); previous leaf pass done (later ones)
         JSP_STAMP(blk, 1);
+        const bool more = base + kChunkRows < r1;  // workgroup-uniform
+        RowRegs<W, R> nxt;
+        if (more) {
+            const uint32_t nrow = row + kChunkRows;
+            load_rows<W, R>(a, nrow, (nrow < r1) && (nrow + 3 >= r0), nxt);
+        }
+        const auto& lab = cur.lab;
+        const auto& tn = cur.tn;
+        const auto& fr = cur.fr;
+        const auto& ex = cur.ex;
 
         // ---- row pass: per value, evaluate 4 rows, scan, store row prefixes
         for (int c = 0; c < nv; ++c) {
@@ -212,6 +239,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
                 s_acc[c * kMaxBlkLeaves + li] += hi_p - lo_p;
             }
         }
+        if (more) cur = nxt;
     }
     __syncthreads();
     JSP_STAMP(blk, 7);

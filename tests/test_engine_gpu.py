@@ -78,6 +78,35 @@ def test_random_parity_large(engine, seed):
     assert_same(got, a, cap, occ)
 
 
+@pytest.mark.parametrize("chunks", [2, 3, 8])
+@pytest.mark.parametrize("seed", range(6))
+def test_multichunk_workgroups_parity(any_engine, monkeypatch, chunks, seed):
+    """Workgroups owning several 1024-row chunks (the next chunk's rows are
+    prefetched while one is evaluated): ragged leaves straddle chunk borders;
+    every launch shape, incl. the fused tail and the single-class compaction."""
+    monkeypatch.setenv("JSP_BLOCK_CHUNKS", str(chunks))
+    p = synth.random_problem(3000 + seed, max_nodes=60_000, max_leaves=3000)
+    got, a, cap, occ = run_both(any_engine, p)
+    assert_same(got, a, cap, occ)
+    p.classes = [p.classes[0]]
+    p.classes[0].level = p.topology.n_levels - 1
+    p.job_class = np.zeros(min(p.n_jobs, 500), dtype=np.uint32)
+    got, a, cap, occ = run_both(any_engine, p)
+    assert_same(got, a, cap, occ)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_deep_interleaved_walk_parity(any_engine, seed):
+    """Up to 4 nested levels, many interleaved short runs and some long ones:
+    the register-resident walker's lazy ancestor marking (flushed when a
+    coarser job or a long run needs it) must equal the eager rule."""
+    p = synth.random_problem(5000 + seed, max_nodes=20_000, max_levels=4, max_leaves=1500,
+                             max_jobs=1200)
+    got, a, cap, occ = run_both(any_engine, p)
+    assert_same(got, a, cap, occ)
+    O.check_invariants(p, got.assign, got.cap, got.occ)
+
+
 def test_trials_parity(engine):
     """Recovery trials (seed = 2*1000 + trial) as timed by bench.py's p99 leg."""
     for t in range(20):
