@@ -84,7 +84,12 @@ def pmc_traffic(kernel: str, cfg: int):
         vals = []
         with open(path, newline="") as f:
             for row in csv.DictReader(f):
-                if row["Kernel_Name"].startswith(kernel):
+                name = row["Kernel_Name"]
+                if name.startswith("void "):
+                    name = name[5:]
+                if name.startswith("jsp::"):
+                    name = name[5:]
+                if name.startswith(kernel):
                     vals.append(float(row["Counter_Value"]))
         return sum(vals) / len(vals) if vals else None
     for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):

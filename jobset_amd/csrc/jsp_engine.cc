@@ -107,6 +107,7 @@ struct jsp_engine {
     // snapshot
     bool have_snap = false;
     uint32_t N = 0, npad = 0, W = 0, R = 0, leaf_begin = 0, n_leaves = 0, max_leaf_rows = 0;
+    uint32_t blk_leaves = 4;  // most leaves any tally workgroup owns, rounded up to 4 (LDS tally stride)
     DevBuf labels, taints, freer, excl, leaf_start, blk;
     uint32_t n_blocks = 0;
     uint32_t epoch = 0;  // compaction launches so far (granule tags)
@@ -230,6 +231,7 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
     a.leaf_start = e->leaf_start.as<uint32_t>();
     a.blk = e->blk.as<uint4>();
     a.n_blocks = e->n_blocks;
+    a.la = e->blk_leaves;
     a.cls = e->cls.as<jsp::DevClass>();
     a.cap_out = d_cap;
     a.occ_out = d_occ;
@@ -340,7 +342,8 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
     f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
     f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
-    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc + a.do_occ, f.topo_in_lds ? topo_words : 0u);
+    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
+                                       f.topo_in_lds ? topo_words : 0u);
     EvPair* p = ev_begin(e, 3, s);
     HIP_TRY(jsp::launch_fused(a, f, s));
     ev_end(p, s);
@@ -595,6 +598,11 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     e->n_leaves = NL;
     e->max_leaf_rows = max_rows;
     e->n_blocks = (uint32_t)blk.size() - 1;
+    {
+        uint32_t most = 1;
+        for (size_t b = 0; b + 1 < blk.size(); ++b) most = std::max(most, blk[b + 1] - blk[b]);
+        e->blk_leaves = (most + 3) & ~3u;
+    }
     e->have_snap = true;
     if (e->have_cls) {
         for (auto& c : e->cls_h)

@@ -62,6 +62,7 @@ struct TallyArgs {
     const uint32_t* leaf_start;
     const uint4* blk;           // per workgroup {first leaf, end leaf, first row, end row}
     uint32_t n_blocks;
+    uint32_t la;                // leaf stride of the LDS tallies: max leaves of a block, rounded up to 4
     const DevClass* cls;
     uint32_t c0, nc;
     int do_occ;
@@ -139,8 +140,9 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
-size_t compact_lds_bytes();
-size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv, uint32_t topo_words);
+size_t compact_lds_bytes(uint32_t la);
+size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
+                       uint32_t topo_words);
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s);

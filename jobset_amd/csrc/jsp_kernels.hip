@@ -75,17 +75,25 @@ __device__ __forceinline__ uint32_t leaf_search(const uint32_t* ls, uint32_t n, 
 
 // ----------------------------------------------------------------- A8 tally (one workgroup)
 // LDS carve (uint32 words), sized per launch by nv = classes in this pass + 1:
-//   [classes kTallyClasses x DevClass][acc nv x kMaxBlkLeaves][wsum nv x 4]
-//   [leaf starts kMaxBlkLeaves+1 (+3 pad)][row prefixes nv x kChunkRows]
+//   [classes nc x DevClass][acc nv x la][wsum nv x 4]
+//   [leaf starts la+1 (+3 pad)][row prefixes nv x kChunkRows]
 // Class records are staged in LDS once per workgroup (read per row from global
 // memory they were re-fetched by vector loads: a generic pointer may alias
 // LDS, and SGPRs are too few to hold them).
-constexpr int kClsWords = kTallyClasses * (int)(sizeof(DevClass) / 4);
-__host__ __device__ constexpr int tally_acc_off() { return kClsWords; }
-__host__ __device__ constexpr int tally_wsum_off(int nv) { return kClsWords + nv * kMaxBlkLeaves; }
-__host__ __device__ constexpr int tally_ls_off(int nv) { return tally_wsum_off(nv) + nv * kTallyWaves; }
-__host__ __device__ constexpr int tally_pre_off(int nv) { return tally_ls_off(nv) + kMaxBlkLeaves + 4; }
-__host__ __device__ constexpr int tally_lds_words(int nv) { return tally_pre_off(nv) + nv * kChunkRows; }
+// Sized per launch: nc classes, nv values, la = the leaf stride of acc (the
+// most leaves any workgroup of the snapshot owns, rounded up to 4), so a
+// snapshot of small racks does not reserve 256 leaves' worth per value --
+// LDS per workgroup decides how many tally workgroups a CU holds at once.
+__host__ __device__ constexpr int tally_acc_off(int nc) { return nc * (int)(sizeof(DevClass) / 4); }
+__host__ __device__ constexpr int tally_wsum_off(int nc, int nv, int la) { return tally_acc_off(nc) + nv * la; }
+__host__ __device__ constexpr int tally_ls_off(int nc, int nv, int la) { return tally_wsum_off(nc, nv, la) + nv * kTallyWaves; }
+__host__ __device__ constexpr int tally_pre_off(int nc, int nv, int la) { return tally_ls_off(nc, nv, la) + la + 4; }
+__host__ __device__ constexpr int tally_lds_words(int nc, int nv, int la) {
+    return tally_pre_off(nc, nv, la) + nv * kChunkRows;
+}
+__host__ __device__ inline int tally_lds_words(const TallyArgs& a) {
+    return tally_lds_words((int)a.nc, (int)a.nc + a.do_occ, (int)a.la);
+}
 
 // Rows of the workgroup: [r0, r1) = leaves [l0, l1). Per chunk of 1024 rows
 // each thread holds 4 consecutive rows (16-B column loads: a wave streams
@@ -134,27 +142,70 @@ __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool
     }
 }
 
+// The fields of one class the row pass reads, moved to SGPRs: every lane
+// reads the same LDS words, so readfirstlane is exact, and the row pass then
+// takes them as scalar operands and branches on them without exec masking
+// (read as VGPRs, each use waited on its own LDS round trip).
+template <int W, int R>
+struct ClassRegs {
+    uint64_t req[W], mask[W];
+    uint32_t tol_inv, pods, res[R], magic[R], shift[R];
+};
+
+__device__ __forceinline__ uint32_t to_sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t to_sgpr64(uint64_t x) {
+    return ((uint64_t)to_sgpr((uint32_t)(x >> 32)) << 32) | to_sgpr((uint32_t)x);
+}
+
+template <int W, int R>
+__device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
+    ClassRegs<W, R> k;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        k.req[w] = to_sgpr64(d.req[w]);
+        k.mask[w] = to_sgpr64(d.mask[w]);
+    }
+    k.tol_inv = to_sgpr(d.tol_inv);
+    k.pods = to_sgpr(d.pods);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        k.res[r] = to_sgpr(d.res[r]);
+        k.magic[r] = to_sgpr(d.magic[r]);
+        k.shift[r] = to_sgpr(d.shift[r]);
+    }
+    return k;
+}
+
 template <int W, int R>
 __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
     DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
-    uint32_t* s_acc = lds + tally_acc_off();
-    uint32_t* s_wsum = lds + tally_wsum_off(nv);
-    uint32_t* s_ls = lds + tally_ls_off(nv);
-    uint32_t* s_pre = lds + tally_pre_off(nv);
+    const int la = (int)a.la;
+    uint32_t* s_acc = lds + tally_acc_off(nc);
+    uint32_t* s_wsum = lds + tally_wsum_off(nc, nv, la);
+    uint32_t* s_ls = lds + tally_ls_off(nc, nv, la);
+    uint32_t* s_pre = lds + tally_pre_off(nc, nv, la);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint4 bt = a.blk[blk];  // {first leaf, end leaf, first row, end row}
     const uint32_t l0 = bt.x, nl = bt.y - bt.x, r0 = bt.z, r1 = bt.w;
 
-    for (uint32_t i = tid; i <= nl; i += kTallyThreads) s_ls[i] = a.leaf_start[l0 + i];
-    for (int i = tid; i < nv * kMaxBlkLeaves; i += kTallyThreads) s_acc[i] = 0;
-    {
-        const uint4* src = reinterpret_cast<const uint4*>(a.cls + a.c0);
-        uint4* dst = reinterpret_cast<uint4*>(s_cls);
-        for (int i = tid; i < nc * (int)(sizeof(DevClass) / 16); i += kTallyThreads) dst[i] = src[i];
-    }
+    // Every global load a workgroup needs before its first barrier is issued
+    // back to back -- staging words (class records, leaf starts) first, then
+    // the first chunk's rows -- and only then are the staging words written to
+    // LDS, so the wait for them (vmcnt counts in issue order) leaves the row
+    // loads in flight: one memory round trip before the row pass, not two.
+    constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
+    static_assert(kTallyClasses * kClsVec <= kTallyThreads, "one class vector per thread");
+    static_assert(kMaxBlkLeaves + 1 <= 2 * kTallyThreads, "two leaf starts per thread");
+    const bool st_cls = tid < nc * kClsVec;
+    const bool st_ls0 = (uint32_t)tid <= nl, st_ls1 = (uint32_t)tid + kTallyThreads <= nl;
+    uint4 cls_v = make_uint4(0, 0, 0, 0);
+    uint32_t ls0 = 0, ls1 = 0;
+    if (st_cls) cls_v = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
+    if (st_ls0) ls0 = a.leaf_start[l0 + tid];
+    if (st_ls1) ls1 = a.leaf_start[l0 + tid + kTallyThreads];
 
     // A workgroup of a large snapshot owns several chunks: the next chunk's rows
     // are loaded (into a second register set) before this chunk is evaluated,
@@ -165,6 +216,10 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
         const uint32_t row = base0 + 4u * tid;
         load_rows<W, R>(a, row, (row < r1) && (row + 3 >= r0), cur);
     }
+    for (int i = tid; i < nv * la; i += kTallyThreads) s_acc[i] = 0;
+    if (st_cls) reinterpret_cast<uint4*>(s_cls)[tid] = cls_v;
+    if (st_ls0) s_ls[tid] = ls0;
+    if (st_ls1) s_ls[tid + kTallyThreads] = ls1;
     for (uint32_t base = base0; base < r1; base += kChunkRows) {
         const uint32_t row = base + 4u * tid;
         const bool any = (row < r1) && (row + 3 >= r0);
@@ -188,20 +243,28 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
         for (int c = 0; c < nv; ++c) {
             uint32_t v[4];
             if (c < nc) {
-                const DevClass& k = s_cls[c];
+                const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
+                uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (k.res[r] == 0) continue;  // scalar branches (SGPR operands), once per 4 rows
+                    if (k.shift[r] == kDivIdentity) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], fr[r][i]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t n = fr[r][i], h = __umulhi(n, k.magic[r]);
+                            cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
+                        }
+                    }
+                }
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     bool ok = valid[i] & ((tn[i] & k.tol_inv) == 0);
 #pragma unroll
                     for (int w = 0; w < W; ++w) ok = ok & ((lab[w][i] & k.mask[w]) == k.req[w]);
-                    uint32_t cap = k.pods;
-#pragma unroll
-                    for (int r = 0; r < R; ++r)
-                        if (k.res[r] != 0) {  // wave-uniform
-                            const uint32_t q = div_invariant(fr[r][i], k.magic[r], k.shift[r]);
-                            cap = q < cap ? q : cap;
-                        }
-                    v[i] = ok ? cap : 0u;
+                    v[i] = ok ? cap[i] : 0u;
                 }
             } else {
 #pragma unroll
@@ -236,7 +299,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
                 const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
                 const uint32_t hi_p = pre[xh] + (wh == 0 ? 0u : wh == 1 ? e1 : wh == 2 ? e2 : e3);
                 const uint32_t lo_p = has_lo ? pre[xb] + (wb == 0 ? 0u : wb == 1 ? e1 : wb == 2 ? e2 : e3) : 0u;
-                s_acc[c * kMaxBlkLeaves + li] += hi_p - lo_p;
+                s_acc[c * la + li] += hi_p - lo_p;
             }
         }
         if (more) cur = nxt;
@@ -245,8 +308,8 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
     JSP_STAMP(blk, 7);
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
         const uint32_t leaf = a.leaf_base + l0 + li;
-        for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * kMaxBlkLeaves + li];
-        if (a.do_occ) a.occ_out[leaf] = s_acc[nc * kMaxBlkLeaves + li];
+        for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * la + li];
+        if (a.do_occ) a.occ_out[leaf] = s_acc[nc * la + li];
     }
 }
 
@@ -1085,7 +1148,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     // publish
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    uint32_t* s_flag = lds + tally_lds_words((int)a.nc + a.do_occ);
+    uint32_t* s_flag = lds + tally_lds_words(a);
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1177,7 +1240,7 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoc
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs a, CompactArgs f) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* s_x = lds + tally_lds_words(2);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
+    uint32_t* s_x = lds + tally_lds_words(a);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t epoch = f.epoch;  // host launch counter, 30-bit, never 0
     uint32_t tile = blockIdx.x;
@@ -1192,10 +1255,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     JSP_STAMP(tile, 2);
 
-    const uint32_t* s_acc = lds + tally_acc_off();
+    const uint32_t* s_acc = lds + tally_acc_off(1);
     const uint4 bt = a.blk[tile];
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
-    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= f.pods && s_acc[kMaxBlkLeaves + tid] == 0;
+    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= f.pods && s_acc[a.la + tid] == 0;
     uint32_t total;
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
     JSP_STAMP(tile, 3);
@@ -1316,7 +1379,7 @@ __global__ void patch_kernel(const uint32_t* __restrict__ rows, uint32_t n, uint
 template <int W, int R>
 static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((tally_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
-                       sizeof(uint32_t) * tally_lds_words((int)a.nc + a.do_occ), s, a);
+                       sizeof(uint32_t) * tally_lds_words(a), s, a);
     return hipGetLastError();
 }
 
@@ -1329,7 +1392,7 @@ static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStr
 template <int W, int R>
 static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
     hipLaunchKernelGGL((place_compact_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
-                       compact_lds_bytes(), s, a, f);
+                       compact_lds_bytes(a.la), s, a, f);
     return hipGetLastError();
 }
 
@@ -1364,12 +1427,13 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
     JSP_DISPATCH_WR(launch_compact_wr, a, f, s)
 }
 
-size_t compact_lds_bytes() { return sizeof(uint32_t) * (tally_lds_words(2) + 4 + 2 * kTallyWaves + 8); }
+size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }
 
-size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nv, uint32_t topo_words) {
+size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
+                       uint32_t topo_words) {
     const size_t tail = (size_t)(t_words + kFusedWinWords64 + feas_words) * 8 +
                         sizeof(uint32_t) * (assign_small_words(kTallyThreads) + topo_words + kFusedStage);
-    const size_t head = sizeof(uint32_t) * (tally_lds_words((int)nv) + 4);
+    const size_t head = sizeof(uint32_t) * (tally_lds_words((int)nc, (int)nv, (int)la) + 4);
     return ((tail > head ? tail : head) + 15) & ~size_t(15);
 }
 

@@ -55,6 +55,16 @@ def main():
     for b in range(min(med.shape[0], 24)):
         print(f"  wg {b:4d}: " + "  ".join(f"{med[b][c]:8.0f}" for c in cols))
     print("  max     : " + "  ".join(f"{med.max(axis=0)[c]:8.0f}" for c in cols))
+    for q in (10, 50, 90):
+        print(f"  p{q:<2d} wgs : " + "  ".join(f"{np.percentile(med[:, c], q):8.0f}" for c in cols))
+    late = np.nonzero(med[:, 0] > 2000)[0]
+    print(f"  {late.size} workgroups enter > 2 us after the first: {late[:40].tolist()}")
+    if late.size:
+        print(f"  their entry (ns): {med[late[:40], 0].astype(int).tolist()}")
+    # per-workgroup phase durations (tally launch: entry -> barrier1 -> rowpass -> leafpass -> end)
+    d = lambda a, b: np.median(med[:, b] - med[:, a])
+    print(f"  median wg durations (ns): to-barrier1 {d(0, 1):.0f}  rowpass {d(1, 6):.0f}  "
+          f"leafpass {d(6, 7):.0f}  write-out {d(7, 5):.0f}  total {d(0, 5):.0f}")
 
 
 if __name__ == "__main__":
