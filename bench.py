@@ -115,6 +115,25 @@ def event_loop_us(fn, k: int, stream) -> float:
     return a.elapsed_time(b) * 1e3 / k
 
 
+def cold_us(fn, k: int, stream, scrub) -> float:
+    """Median µs of one call of `fn` with cold caches: before each call a
+    512 MiB buffer is read and written on the same stream, which evicts the
+    256 MiB Infinity Cache and every XCD's L2; HIP events bracket the call."""
+    import torch
+    s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.default_stream()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ts = []
+    with torch.cuda.stream(s):
+        for _ in range(k):
+            scrub.add_(1)
+            a.record(s)
+            fn()
+            b.record(s)
+            b.synchronize()
+            ts.append(a.elapsed_time(b) * 1e3)
+    return float(np.median(ts))
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -276,11 +295,17 @@ def main() -> None:
         tally_us = event_loop_us(lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream),
                                  steps4, stream)
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
+        scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
+        tally_cold = cold_us(lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream),
+                             20, stream, scrub)
+        del scrub
         cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
                 "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
                 "placed": placed4, "tally_us": round(tally_us, 2),
                 "tally_gbs": round(tb4 / (tally_us * 1e-6) / 1e9, 1),
                 "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "tally_cold_us": round(tally_cold, 2),
+                "tally_cold_gbs": round(tb4 / (tally_cold * 1e-6) / 1e9, 1),
                 "tally_traffic": pmc_traffic("tally_kernel", 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
                 "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
