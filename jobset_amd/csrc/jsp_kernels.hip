@@ -776,12 +776,14 @@ __device__ __forceinline__ uint32_t topo_par(const TopoDev& topo, const uint32_t
 }
 
 __device__ __forceinline__ uint64_t reg_load_f(const uint64_t* __restrict__ feas, uint32_t rc_l, uint32_t q, uint32_t C,
-                                               uint32_t my_toff, uint32_t my_woff, uint32_t my_nw, int lane) {
+                                               uint32_t g_toff, uint32_t g_woff, uint32_t g_nw, int lane) {
+    // g_*: run q's class fields, gathered per lane (lane = run), so every readlane
+    // here is indexed by q alone and none waits on another
     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
+    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)g_toff, (int)q);
+    const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)g_nw, (int)q);
+    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)g_woff, (int)q);
     if (c >= C) return 0ull;
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)my_toff, (int)c);
-    const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)my_nw, (int)c);
-    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)my_woff, (int)c);
     const uint32_t wi = (uint32_t)lane - t0;  // wraps for lanes below the level
     return wi < nw ? feas[wo + wi] : 0ull;
 }
@@ -911,10 +913,16 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                 // feasibility word of run q's class for this lane (0 outside its level),
                 // loaded one run ahead so it is in flight while the previous run is placed
                 JSP_STAMP(4010u + t0 / 64, 0);
-                uint64_t f_next = reg_load_f(feas, rc_l, 0, C, my_toff, my_woff, my_nw, lane);
+                // class fields of each lane's run (lane = run t0 + lane), one gather per 64 runs
+                const int cc = (int)(rc_l < C ? rc_l : 0u);
+                const uint32_t g_toff = (uint32_t)__shfl((int)my_toff, cc);
+                const uint32_t g_woff = (uint32_t)__shfl((int)my_woff, cc);
+                const uint32_t g_nw = (uint32_t)__shfl((int)my_nw, cc);
+                const uint32_t g_lvl = (uint32_t)__shfl((int)my_lvl, cc);
+                uint64_t f_next = reg_load_f(feas, rc_l, 0, C, g_toff, g_woff, g_nw, lane);
                 for (uint32_t q = 0; q < nb; ++q) {
                     const uint64_t f = f_next;
-                    if (q + 1 < nb) f_next = reg_load_f(feas, rc_l, q + 1, C, my_toff, my_woff, my_nw, lane);
+                    if (q + 1 < nb) f_next = reg_load_f(feas, rc_l, q + 1, C, g_toff, g_woff, g_nw, lane);
                     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
                     const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)ro_l, (int)q);
                     const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)rn_l, (int)q);
@@ -925,8 +933,8 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                         for (uint32_t j = j0 + lane; j < jend; j += 64) assign[j] = -1;
                         continue;
                     }
-                    const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
-                    const uint32_t t0l = (uint32_t)__builtin_amdgcn_readlane((int)my_toff, (int)c);
+                    const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)g_lvl, (int)q);
+                    const uint32_t t0l = (uint32_t)__builtin_amdgcn_readlane((int)g_toff, (int)q);
                     if (o1 - o0 > kWaveRunMax) {
                         // long run: fold pending ancestors, publish the bitmaps, join the
                         // workgroup (cursor 0: the whole level is one window), reload
