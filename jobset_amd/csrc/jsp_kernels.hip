@@ -921,8 +921,10 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                 const uint32_t g_lvl = (uint32_t)__shfl((int)my_lvl, cc);
                 uint64_t f_next = reg_load_f(feas, rc_l, 0, C, g_toff, g_woff, g_nw, lane);
                 for (uint32_t q = 0; q < nb; ++q) {
+                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 0);
                     const uint64_t f = f_next;
                     if (q + 1 < nb) f_next = reg_load_f(feas, rc_l, q + 1, C, g_toff, g_woff, g_nw, lane);
+                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 1);
                     const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
                     const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)ro_l, (int)q);
                     const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)rn_l, (int)q);
@@ -947,6 +949,7 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                         continue;
                     }
                     if (rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
+                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 2);
                     const uint64_t avail = f & ~rs.T;
                     const uint32_t n = jend - j0;
                     uint64_t took = 0;
@@ -986,7 +989,9 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
                         rs.P |= took;
                         rs.pend = rs.pend > (int)lvl ? rs.pend : (int)lvl;
                     }
+                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 3);
                     if (lvl + 1 < K) reg_mark_desc<TOPO_LDS>(rs, took, lvl, t0l, K, topo, s_topo, m, lane);
+                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 4);
                     if (q == 15 || q == 31 || q == 47) JSP_STAMP(4010u + t0 / 64, 1 + q / 16);
                 }
                 JSP_STAMP(4010u + t0 / 64, 4);

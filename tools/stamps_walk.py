@@ -44,11 +44,11 @@ def main():
         st = buf.reshape(4096, 8).astype(np.int64)
         nz = st[st != 0]
         t0 = nz.min() if nz.size else 0
-        sel = st[4000:4030]
+        sel = st[4000:4050]
         rows.append(np.where(sel != 0, (sel - t0) * 10, -1))
     med = np.median(np.stack(rows[3:]), axis=0)
     print(f"cfg{cfg} fused={fused} runs={rc.shape[0]}: ns from the launch's first stamp")
-    for r in range(30):
+    for r in range(50):
         if (med[r] >= 0).any():
             print(f"  row {4000 + r}: " + "  ".join(f"{x:8.0f}" for x in med[r]))
 
