@@ -2,11 +2,16 @@
 """Benchmark of the MI355X exclusive-topology placement engine.
 
 Metric (BASELINE.json): exclusive-topology placements/sec at 15k nodes; p99
-recovery placement latency. Workload (`value`): config 2 — a 15,000-node /
+recovery placement latency. Workload (`value`): config 2 -- a 15,000-node /
 1,000-rack post-delete snapshot and a full-JobSet recovery of 990 jobs x 15
-pods — resident in HBM; one step = one placement of all 990
-jobs (tally + feasibility + lowest-index assignment) from the resident
-snapshot and run list to assign[] in HBM.
+pods. One step = one `jsp_place` call through the C ABI, as
+the recovery path makes it: the run list goes host -> device, the engine
+tallies, decides feasibility and assigns all 990 jobs, and assign[] comes
+back to the caller's host buffer (placements/sec = J_placed /
+wall time of jsp_place including H2D and D2H). The snapshot is resident (its
+upload is the "post-delete snapshot ready" point and is not timed).
+`kernel_only_*` is the same placement from device-resident runs to a
+device-resident assign[] (no host round trip).
 
 `--gpus N` (torchrun, one rank per GPU): config 2 has ~0.4 MB of rows and does
 not shard usefully, so ranks run independent replicas (weak scaling, no
@@ -16,12 +21,15 @@ node dimension split over the ranks, per-leaf tallies SUM-all-reduced by RCCL)
 is reported beside it under "cfg4_1M".
 
 Roofline: the dominant kernel's average duration comes from two HIP events
-recorded on the launch stream around K back-to-back launches (no per-launch
-events, which would add their own overhead to every launch); its algorithmic
+recorded on the launch stream around K back-to-back launches; its algorithmic
 bytes are DESIGN.md §4's. `traffic` is the PMC-measured HBM bytes per launch
 of the same kernel from the committed rocprofv3 passes under profiles/
 (FETCH_SIZE x 2 for gfx950's wide-load halving + WRITE_SIZE, per
 MI355X_MICROARCH.md "HBM"), or null when no pass for it is committed.
+
+CPU baseline: oracle/cpu_fast.c, an optimized threaded evaluator of the same
+rules (bit-exact with the oracle), timed on this host at 1 thread, 2 threads
+(the reference manager's 2-CPU limit) and every core of the box's share.
 
 Prints ONE JSON line on rank 0.
 """
@@ -134,13 +142,62 @@ def cold_us(fn, k: int, stream, scrub) -> float:
     return float(np.median(ts))
 
 
+def cpu_threads() -> int:
+    """Threads of this host's share: OMP_NUM_THREADS (the GPU box sets it to
+    its per-GPU CPU share; os.cpu_count() there reports the whole machine),
+    bounded by the affinity mask."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return max(1, min(aff, int(omp))) if omp and omp.isdigit() else aff
+
+
+def time_cpu(fc, seconds: float):
+    """µs per placement of the prepared FastCPU over a bounded sample."""
+    fc.run()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        fc.run()
+        n += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return dt * 1e6 / n, n, dt
+
+
+def host_api_latency(eng, p, trials: int, trial_fn=None):
+    """Host-API wall of jsp_place (µs): over `trials` seeded trial snapshots
+    when trial_fn is given (upload untimed: "post-delete snapshot ready" ->
+    "assign[] returned"), else repeated calls on the resident snapshot."""
+    from jobset_amd.snapshot import job_runs
+    lat = []
+    if trial_fn is not None:
+        for t in range(trials):
+            pt = trial_fn(t)
+            eng.upload_snapshot(pt.nodes)
+            call = eng.host_placer(*job_runs(pt.job_class))
+            t0 = time.perf_counter()
+            call()
+            lat.append((time.perf_counter() - t0) * 1e6)
+        eng.upload_snapshot(p.nodes)
+    else:
+        call = eng.host_placer(*job_runs(p.job_class))
+        for _ in range(10):
+            call()
+        for _ in range(trials):
+            t0 = time.perf_counter()
+            call()
+            lat.append((time.perf_counter() - t0) * 1e6)
+    lat.sort()
+    pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 1)  # noqa: E731
+    return {"p50_us": pct(0.50), "p99_us": pct(0.99), "n": len(lat)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample")
+    ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99) on config 2")
+    ap.add_argument("--cpu-seconds", type=float, default=9.0, help="bounded CPU-baseline sample (all legs)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the 1M-node sharded leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the per-config (1, 3, 5) lines")
     args = ap.parse_args()
@@ -174,26 +231,40 @@ def main() -> None:
             eng.place_device(rc.data_ptr(), rl.data_ptr(), rc_np.shape[0], p.n_jobs, out.data_ptr(), stream)
         return step, out
 
-    # ------------------------------------------------ config 2 (value)
+    # ------------------------------------------------ config 2: host-API placements/s (value)
     p = synth.config2()
     eng.load(p)
     J = p.n_jobs
     shape = eng.place(p.job_class).fused
-    step, out = device_step(p)
+    call = eng.host_placer(*job_runs(p.job_class))
     for _ in range(args.warmup):
-        step()
+        call()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        call()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
-    placed = int((out[:J].cpu().numpy() >= 0).sum())
+    placed = int((call.assign >= 0).sum())
     value = placed * args.steps * world / elapsed
+
+    # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
+    step, out = device_step(p)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    barrier(world)
+    el_dev = max_over_ranks(time.perf_counter() - t0, world)
+    assert int((out[:J].cpu().numpy() >= 0).sum()) == placed
 
     # dominant kernel: the step's single launch (compaction / fused), else the tally
     if shape in (1, 2):
@@ -204,40 +275,37 @@ def main() -> None:
         dom_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
                                                         stream), args.steps, stream)
         tb = tally_bytes(p)
+    eng.check()
     achieved = tb / (dom_us * 1e-6) / 1e9
     traffic = pmc_traffic(KERNEL[shape], 2)
 
-    # ------------------------------------------------ p99 recovery latency (host API, trial snapshots)
-    lat = []
-    if rank == 0 and args.trials > 0:
-        for t in range(args.trials):
-            pt = synth.config2(trial=t)
-            eng.upload_snapshot(pt.nodes)           # post-delete snapshot ready (untimed)
-            r = eng.place(pt.job_class)             # restart triggered -> assign[] returned
-            lat.append(r.wall_us)
-        eng.upload_snapshot(p.nodes)
-    lat_sorted = sorted(lat)
+    # ------------------------------------------------ p50/p99 recovery latency (host API, trial snapshots)
+    lat2 = host_api_latency(eng, p, args.trials, synth.config2) if rank == 0 and args.trials > 0 else None
 
-    def pct(q):
-        return lat_sorted[min(len(lat_sorted) - 1, int(q * len(lat_sorted)))] if lat_sorted else None
-
-    # ------------------------------------------------ CPU baseline (rank 0, N=1 only)
+    # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
     cpu = None
+    T = cpu_threads()
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle import oracle as O
-        pk = O.PackedProblem(p)
-        O.place_c(p, pk)
-        n, t0c = 0, time.perf_counter()
-        while time.perf_counter() - t0c < args.cpu_seconds:
-            a, _, _ = O.place_c(p, pk)
-            n += 1
-        dt = time.perf_counter() - t0c
-        cpu = {"value": round(int((a >= 0).sum()) * n / dt, 1), "unit": "placements/s", "cores": 1,
-               "kind": "port",
-               "sample": f"config 2 placed {n} times in {dt:.1f} s by oracle/cpu_ref.c (1 thread, -O2), "
-                         f"same snapshot and rules"}
+        legs = []
+        for th in sorted({1, 2, T}):
+            fc = O.FastCPU(th)
+            fc.prepare(p)
+            a, _, _, pl = fc.run()
+            assert np.array_equal(a, call.assign), "CPU evaluator differs from the engine"
+            us, n, dt = time_cpu(fc, args.cpu_seconds / 3)
+            fc.close()
+            legs.append({"threads": th, "us_per_placement": round(us, 2),
+                         "placements_per_s": round(pl / (us * 1e-6), 1), "runs": n, "seconds": round(dt, 2)})
+        best = legs[-1]
+        cpu = {"value": best["placements_per_s"], "unit": "placements/s", "cores": best["threads"], "kind": "port",
+               "nproc": os.cpu_count(), "threads_share": T,
+               "sample": f"config 2 placed {best['runs']} times in {best['seconds']} s by oracle/cpu_fast.c "
+                         f"({best['threads']} threads, -O3 AVX2, same snapshot and rules, bit-exact with the "
+                         f"engine); legs at 1/2/{T} threads below",
+               "legs": legs}
 
-    # ------------------------------------------------ configs 1, 3, 5 (one GPU, device-resident)
+    # ------------------------------------------------ configs 1, 3, 5 (one GPU)
     configs = None
     if rank == 0 and not args.no_configs:
         configs = {}
@@ -249,19 +317,22 @@ def main() -> None:
             for _ in range(5):
                 st()
             us = event_loop_us(st, 50, stream)
+            eng.check()
             line = {"nodes": pc.nodes.n_nodes, "jobs": pc.n_jobs, "classes": len(pc.classes),
                     "levels": pc.topology.n_levels, "placed": r.placed, "shape": SHAPES[r.fused],
-                    "us_per_placement": round(us, 2), "placements_per_s": round(r.placed / (us * 1e-6), 1),
-                    "host_api_us": round(r.wall_us, 1)}
+                    "kernel_us_per_placement": round(us, 2),
+                    "kernel_placements_per_s": round(r.placed / (us * 1e-6), 1),
+                    "host_api_resident": host_api_latency(eng, pc, 200)}
+            if cfg in (3, 5):
+                line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
             if world == 1 and args.cpu_seconds > 0:
                 from oracle import oracle as O
-                pk = O.PackedProblem(pc)
-                O.place_c(pc, pk)
-                n, t0c = 0, time.perf_counter()
-                while time.perf_counter() - t0c < min(1.0, args.cpu_seconds / 5):
-                    O.place_c(pc, pk)
-                    n += 1
-                line["cpu_port_us_per_placement"] = round((time.perf_counter() - t0c) * 1e6 / n, 1)
+                for th in sorted({1, T}):
+                    fc = O.FastCPU(th)
+                    fc.prepare(pc)
+                    us_c, _, _ = time_cpu(fc, min(0.5, args.cpu_seconds / 10))
+                    fc.close()
+                    line[f"cpu_fast_{th}t_us_per_placement"] = round(us_c, 1)
             configs[f"cfg{cfg}"] = line
         eng.load(p)
 
@@ -298,7 +369,16 @@ def main() -> None:
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
         tally_cold = cold_us(lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream),
                              20, stream, scrub)
+        copy_ceiling = None
+        if world == 1:  # achievable streaming rate: a cold copy of the same byte count
+            src = torch.empty(tb4 // 2 // 16 * 4, dtype=torch.int32, device="cuda").fill_(1)
+            dst = torch.empty_like(src)
+            cu = cold_us(lambda: dst.copy_(src), 20, stream, scrub)
+            copy_ceiling = {"bytes": 2 * src.numel() * 4, "cold_us": round(cu, 2),
+                            "cold_gbs": round(2 * src.numel() * 4 / (cu * 1e-6) / 1e9, 1)}
+            del src, dst
         del scrub
+        sp.engine.check()
         cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
                 "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
                 "placed": placed4, "tally_us": round(tally_us, 2),
@@ -306,6 +386,8 @@ def main() -> None:
                 "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "tally_cold_us": round(tally_cold, 2),
                 "tally_cold_gbs": round(tb4 / (tally_cold * 1e-6) / 1e9, 1),
+                "tally_cold_frac": round(tb4 / (tally_cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "copy_ceiling_same_bytes": copy_ceiling,
                 "tally_traffic": pmc_traffic("tally_kernel", 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
                 "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
@@ -325,19 +407,22 @@ def main() -> None:
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic",
-            "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery",
+            "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery; one step "
+                                   "= one host-API jsp_place (runs H2D, assign[] D2H)",
                        "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J,
                        "pods_per_job": p.classes[0].pods, "classes": len(p.classes),
                        "shape": SHAPES[shape], "parallelism": f"replicas{world}"},
+            "kernel_only_placements_per_s": round(placed * args.steps * world / el_dev, 1),
+            "kernel_only_us_per_step": round(el_dev * 1e6 / args.steps, 3),
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
-                         "note": "latency-bound: one launch moving 0.44 MB; see DESIGN.md §8"},
-            "p50_recovery_us": round(pct(0.50), 1) if lat else None,
-            "p99_recovery_us": round(pct(0.99), 1) if lat else None,
-            "recovery_trials": len(lat),
+                         "note": "latency-bound: one launch moving 0.43 MB; see DESIGN.md §8"},
+            "p50_recovery_us": lat2["p50_us"] if lat2 else None,
+            "p99_recovery_us": lat2["p99_us"] if lat2 else None,
+            "recovery_trials": lat2["n"] if lat2 else 0,
             "cpu_baseline": cpu,
             "configs": configs,
             "cfg4_1M": cfg4,

@@ -39,6 +39,19 @@
  *
  * Threading: one engine is not re-entrant; calls on one engine are
  * serialised by an internal mutex (the Go wrapper also holds one).
+ *
+ * Stream ordering: uploads, patches, jsp_place and the webhook batches run on
+ * the engine's own stream and return after it has finished; the *_device
+ * entry points enqueue on the caller's stream and return at once. Every call
+ * is ordered after all work the engine enqueued earlier, on whatever stream
+ * (the first call on a different stream waits on an event of the previous
+ * one), so a patch after a jsp_place_device never races its tally.
+ *
+ * Kernel-side failures: the single-class compaction's look-back has a bounded
+ * spin. A launch that exceeds it writes its launch number to an error word
+ * and leaves that launch's assign[] invalid. jsp_place reports it before it
+ * returns; the device path reports it from jsp_engine_check (which waits for
+ * the engine's work) or, once visible, from the next call on the engine.
  */
 #ifndef JSPLACE_H
 #define JSPLACE_H
@@ -50,7 +63,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 1
+#define JSP_ABI_VERSION 2
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -118,6 +131,12 @@ typedef struct jsp_timing {
     double assign_ms;          /* summed HIP-event time of the assignment kernel */
     double fused_ms;           /* summed HIP-event time of single-launch placements (fused / compaction) */
     uint64_t fused_calls;      /* placements that ran as a single launch */
+    /* host-API placements (jsp_place), host wall clock, always accumulated */
+    uint64_t host_calls;
+    double host_prep_us;       /* entry to launch: checks, run list into the pinned staging buffer */
+    double host_launch_us;     /* the kernel launch call(s) */
+    double host_wait_us;       /* launch return to completion seen (completion words or stream sync) */
+    double host_post_us;       /* assign[] (and tallies) out, stats */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */
@@ -193,6 +212,9 @@ int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);
 int jsp_engine_sync(jsp_engine* e);
+/* Waits for every launch the engine has enqueued (on any stream) and returns
+ * JSP_EHIP if one of them failed on the device (see "Kernel-side failures"). */
+int jsp_engine_check(jsp_engine* e);
 
 #ifdef __cplusplus
 }

@@ -122,9 +122,24 @@ struct jsp_engine {
     // scratch
     DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, recs, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
     HostBuf h_runs, h_assign, h_stats;  // zero-copy staging of the host placement path
+    HostBuf h_done;                     // [n_blocks] completion words of the host placement path
+    HostBuf h_err;                      // [1] error word: a failed launch writes its epoch (sticky)
+    uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
     int fused_mode = JSP_FUSED_AUTO;
     uint32_t last_shape = 0;  // 0 three launches, 1 fused tail, 2 single-class compaction
+    // draws on the single-launch kernels' tickets so far (DevBuf ticket [0]
+    // tiles, [1] finished tiles): every launch adds its grid / tile count
+    unsigned long long tile_draws = 0, done_draws = 0;
+    // test hook, read at snapshot upload: JSP_LOOKBACK_SPINS (look-back polls
+    // before a compaction tile gives up)
+    uint32_t spin_limit = 1u << 22;
+
+    // stream ordering: work is enqueued on the engine stream or a caller's;
+    // the first call on a different stream waits for the previous one
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
+    hipEvent_t ev_switch = nullptr;
 
     // timing
     bool timing = false;
@@ -138,6 +153,7 @@ struct jsp_engine {
             if (p.a) (void)hipEventDestroy(p.a);
             if (p.b) (void)hipEventDestroy(p.b);
         }
+        if (ev_switch) (void)hipEventDestroy(ev_switch);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -162,11 +178,56 @@ uint32_t block_chunks(uint32_t /*N*/) {
 constexpr size_t kMaxEvents = 3 * 4096;
 // Above this many tally workgroups the three-launch shape wins: the fused tail
 // runs feasibility + assignment on one 256-thread workgroup.
-constexpr uint32_t kFusedMaxBlocks = 64;
-// Compaction workgroups resident at once without doubt: 256 CUs x 4 (LDS and
-// VGPRs admit more). Up to this grid the tile is blockIdx.x; above it tiles
-// are taken from a ticket so a workgroup only waits on started ones.
-constexpr uint32_t kCoresidentBlocks = 1024;
+constexpr uint32_t kFusedMaxBlocks = 256;
+
+// Order work on stream s after everything the engine enqueued before on
+// another stream (uploads and jsp_place use the engine stream, the device
+// entry points the caller's): the first call on a new stream records an event
+// on the previous one and makes s wait for it. Calls on one stream cost nothing.
+int enter_stream(jsp_engine* e, hipStream_t s) {
+    if (e->have_last && e->last_stream != s) {
+        if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_switch, 0));
+    }
+    e->last_stream = s;
+    e->have_last = true;
+    return JSP_OK;
+}
+
+// Non-blocking: a compaction launch whose look-back timed out has written its
+// epoch to the host-mapped error word. Reported once, by the next call.
+int check_launch_error(jsp_engine* e) {
+    const uint32_t w = __atomic_load_n(e->h_err.as<uint32_t>(), __ATOMIC_ACQUIRE);
+    if (w != e->err_ack) {
+        e->err_ack = w;
+        return set_err(JSP_EHIP, "placement launch %u failed: the compaction look-back timed out (a workgroup "
+                                 "never published its count); that launch's assign[] is invalid", w);
+    }
+    return JSP_OK;
+}
+
+// Host placement path: wait for the kernel's completion words (one per
+// signalling workgroup) instead of the kernel-end signal. A finished stream
+// whose words are missing, or a failed stream, is an error.
+int wait_done(jsp_engine* e, hipStream_t s, uint32_t n, uint32_t epoch) {
+    const uint32_t* words = e->h_done.as<uint32_t>();
+    uint32_t i = 0;
+    for (uint64_t spins = 1;; ++spins) {
+        while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == epoch) ++i;
+        if (i == n) return JSP_OK;
+        if ((spins & 255) == 0) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) {
+                for (; i < n; ++i)
+                    if (__atomic_load_n(words + i, __ATOMIC_ACQUIRE) != epoch)
+                        return set_err(JSP_EHIP, "placement kernel ended without completion word %u", i);
+                return JSP_OK;
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement kernel failed: %s", hipGetErrorString(q));
+        }
+    }
+}
 
 int resolve_timing(jsp_engine* e) {
     if (e->ev_used == 0) return JSP_OK;
@@ -296,26 +357,36 @@ bool compact_ok(jsp_engine* e) {
 
 // Whole placement on the engine's own tally buffers: one compaction launch for
 // a single leaf-level class, one fused launch when the snapshot is small, else
-// tally -> feas -> assign.
+// tally -> feas -> assign. `signal`: the single-launch shapes write host
+// completion words (e->h_done) tagged e->epoch; *n_signals says how many.
 int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
-               int32_t* d_assign, hipStream_t s) {
+               int32_t* d_assign, hipStream_t s, bool signal = false, uint32_t* n_signals = nullptr,
+               bool want_tally = false) {
+    e->epoch = e->epoch % 0x3FFFFFFFu + 1u;
+    if (n_signals) *n_signals = 0;
     if (compact_ok(e)) {
         e->last_shape = 2;
-        jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
+        // the compaction keeps its sums in LDS; they go out only when asked for
+        jsp::TallyArgs a = want_tally ? tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total)
+                                      : tally_args(e, nullptr, nullptr, e->L_total);
         jsp::CompactArgs f{};
         f.ticket = e->ticket.as<unsigned long long>();
+        f.tile_base = e->tile_draws;
         f.granules = e->granules.as<unsigned long long>();
         f.pods = e->cls_h[0].pods;
         f.n_runs = n_runs;
         f.J = J;
         f.assign = d_assign;
         f.stats = stats_ptr(e);
-        e->epoch = e->epoch % 0x3FFFFFFFu + 1u;
         f.epoch = e->epoch;
-        f.coresident = e->n_blocks <= kCoresidentBlocks ? 1u : 0u;
+        f.err = e->h_err.as<uint32_t>();
+        f.spin_limit = e->spin_limit;
+        f.done = signal ? e->h_done.as<uint32_t>() : nullptr;
+        if (n_signals && signal) *n_signals = e->n_blocks;
         EvPair* p = ev_begin(e, 3, s);
         HIP_TRY(jsp::launch_compact(a, f, s));
         ev_end(p, s);
+        e->tile_draws += e->n_blocks + jsp::kSpareBlocks;
         return JSP_OK;
     }
     e->last_shape = fused_ok(e) ? 1 : 0;
@@ -327,6 +398,8 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
     jsp::FusedArgs f{};
     f.ticket = e->ticket.as<unsigned long long>();
+    f.tile_base = e->tile_draws;
+    f.done_base = e->done_draws;
     f.C = e->C;
     f.topo = e->topo;
     f.t_off = e->t_off.as<uint32_t>();
@@ -344,9 +417,14 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
     f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
                                        f.topo_in_lds ? topo_words : 0u);
+    f.done = signal ? e->h_done.as<uint32_t>() : nullptr;
+    f.epoch = e->epoch;
+    if (n_signals && signal) *n_signals = 1;
     EvPair* p = ev_begin(e, 3, s);
     HIP_TRY(jsp::launch_fused(a, f, s));
     ev_end(p, s);
+    e->tile_draws += e->n_blocks + jsp::kSpareBlocks;
+    e->done_draws += e->n_blocks;
     return JSP_OK;
 }
 
@@ -437,6 +515,11 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         delete e;
         return set_err(JSP_ENOMEM, "stats buffer");
     }
+    if (e->h_err.reserve(64) != hipSuccess) {
+        delete e;
+        return set_err(JSP_ENOMEM, "error word");
+    }
+    std::memset(e->h_err.p, 0, 64);
     *out = e;
     return JSP_OK;
 }
@@ -455,6 +538,8 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     if (!t) return set_err(JSP_EINVAL, "topology is NULL");
+    // a failed upload leaves the engine without topology (buffers may be gone)
+    e->have_topo = e->have_snap = e->have_cls = false;
     const uint32_t K = t->n_levels;
     if (K < 1 || K > JSP_MAX_LEVELS) return set_err(JSP_EINVAL, "n_levels %u out of range [1,%d]", K, JSP_MAX_LEVELS);
     const uint32_t L = t->n_domains[K - 1];
@@ -487,6 +572,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
         return set_err(JSP_ERANGE, "topology has %u bitmap words over all levels; engine limit is %u (%u domains)",
                        off, jsp::kMaxTakenWords, jsp::kMaxTakenWords * 64);
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     jsp::TopoDev td{};
     td.K = K;
     for (uint32_t k = 0; k < K; ++k) {
@@ -525,6 +611,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     std::lock_guard<std::mutex> g(e->mu);
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (!nd || !nd->leaf_start) return set_err(JSP_EINVAL, "nodes / leaf_start is NULL");
+    e->have_snap = false;  // until every column is resident again
     const uint32_t N = nd->n_nodes, W = nd->n_label_words, R = nd->n_res, NL = nd->n_leaves;
     if (W < 1 || W > JSP_MAX_LABEL_WORDS) return set_err(JSP_EINVAL, "n_label_words %u out of range", W);
     if (R < 1 || R > JSP_MAX_RES) return set_err(JSP_EINVAL, "n_res %u out of range", R);
@@ -563,6 +650,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     }
     const uint32_t npad = ((N + 63) / 64) * 64 + 64;
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(e->labels.reserve((size_t)W * npad * 8));
     HIP_TRY(e->taints.reserve((size_t)npad * 4));
     HIP_TRY(e->freer.reserve((size_t)R * npad * 4));
@@ -586,10 +674,12 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     for (size_t b = 0; b + 1 < blk.size(); ++b) bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
     HIP_TRY(upload(e->blk, bt.data(), std::max<size_t>(bt.size(), 1), s));
     HIP_TRY(e->ticket.reserve(16));
-    HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch ticket: grows by n_blocks per launch
+    HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch tickets (tile draws, finished tiles)
     HIP_TRY(e->granules.reserve(8 * blk.size()));
     HIP_TRY(hipMemsetAsync(e->granules.p, 0, 8 * blk.size(), s));  // look-back granules (epoch 0 never matches)
+    HIP_TRY(e->h_done.reserve(4 * blk.size()));
     HIP_TRY(hipStreamSynchronize(s));
+    std::memset(e->h_done.p, 0, 4 * blk.size());  // completion words (epoch 0 never matches)
     e->N = N;
     e->npad = npad;
     e->W = W;
@@ -603,6 +693,9 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
         for (size_t b = 0; b + 1 < blk.size(); ++b) most = std::max(most, blk[b + 1] - blk[b]);
         e->blk_leaves = (most + 3) & ~3u;
     }
+    e->tile_draws = e->done_draws = 0;
+    e->spin_limit = 1u << 22;
+    if (const char* v = std::getenv("JSP_LOOKBACK_SPINS")) e->spin_limit = (uint32_t)std::strtoul(v, nullptr, 10);
     e->have_snap = true;
     if (e->have_cls) {
         for (auto& c : e->cls_h)
@@ -624,6 +717,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(upload(e->tmp_a, rows, n, s));
     if (labels) HIP_TRY(upload(e->tmp_b, labels, (size_t)e->W * n, s));
     if (taints) HIP_TRY(upload(e->tmp_c, taints, n, s));
@@ -644,6 +738,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (C > (uint32_t)jsp::kMaxClasses) return set_err(JSP_ERANGE, "%u classes exceed the limit of %d", C, jsp::kMaxClasses);
     if (C > 0 && !classes) return set_err(JSP_EINVAL, "classes is NULL");
+    e->have_cls = false;  // until the new classes are resident
     std::vector<jsp::DevClass> h(std::max<uint32_t>(C, 1));
     std::vector<uint32_t> woff(C + 1, 0);
     for (uint32_t c = 0; c < C; ++c) {
@@ -669,6 +764,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
         woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
     }
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(upload(e->cls, h.data(), h.size(), s));
     HIP_TRY(upload(e->word_off, woff.data(), woff.size(), s));
     HIP_TRY(e->feas.reserve((size_t)std::max<uint32_t>(woff[C], 1) * 8));
@@ -688,6 +784,8 @@ int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t l
     if (int rc = ready(e, true)) return rc;
     if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
     if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, pick(e, stream))) return rc;
     return tally_impl(e, d_cap, d_occ, ld, pick(e, stream));
 }
 
@@ -701,6 +799,8 @@ int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_oc
     if (!d_cap || !d_occ) return set_err(JSP_EINVAL, "tally buffers are NULL");
     if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
     if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, pick(e, stream))) return rc;
     return assign_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
 }
 
@@ -713,6 +813,8 @@ int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t*
         return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
     if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
     if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, pick(e, stream))) return rc;
     return place_impl(e, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
 }
 
@@ -730,8 +832,12 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     hipStream_t s = e->stream;
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, s)) return rc;
     // runs in, assign[] and stats out through pinned mapped host memory: one
-    // launch sequence and one synchronize, no DMA round trips
+    // launch sequence, no DMA round trips. The single-launch shapes signal
+    // completion through host words (wait_done); the others, and calls that
+    // copy the tallies out, synchronise the stream.
     HIP_TRY(e->h_runs.reserve((size_t)std::max<uint32_t>(n_runs, 1) * 8));
     HIP_TRY(e->h_assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
     HIP_TRY(e->h_stats.reserve(16));
@@ -741,19 +847,30 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         std::memcpy(h_rc, run_class, (size_t)n_runs * 4);
         std::memcpy(h_rl, run_len, (size_t)n_runs * 4);
     }
+    const bool want_tally = (tally_out && e->C > 0) || occ_out;
     e->stats_override = e->h_stats.as<uint32_t>();
-    const int prc = place_impl(e, h_rc, h_rl, n_runs, J, e->h_assign.as<int32_t>(), s);
+    uint32_t n_sig = 0;
+    const auto t1 = std::chrono::steady_clock::now();
+    const int prc = place_impl(e, h_rc, h_rl, n_runs, J, e->h_assign.as<int32_t>(), s, !want_tally, &n_sig,
+                               want_tally);
     e->stats_override = nullptr;
     if (prc) return prc;
-    if (tally_out && e->C > 0)
-        HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
-    if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipStreamSynchronize(s));
+    const auto t2 = std::chrono::steady_clock::now();
+    if (want_tally) {
+        if (tally_out && e->C > 0)
+            HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
+        if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
+    }
+    if (n_sig > 0) {
+        if (int rc = wait_done(e, s, n_sig, e->epoch)) return rc;
+    } else {
+        HIP_TRY(hipStreamSynchronize(s));
+    }
+    const auto t3 = std::chrono::steady_clock::now();
     if (J > 0) std::memcpy(assign_out, e->h_assign.p, (size_t)J * 4);
-    uint32_t st[3];
+    if (int rc = check_launch_error(e)) return rc;
+    uint32_t st[2];
     std::memcpy(st, e->h_stats.p, sizeof st);
-    if (e->last_shape == 2 && st[2] != 0)
-        return set_err(JSP_EHIP, "compaction look-back timed out (a workgroup never published its count)");
     if (stats) {
         stats->jobs = J;
         stats->runs = n_runs > 0 ? st[0] : 0;
@@ -761,6 +878,13 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         stats->fused = e->last_shape;
         stats->wall_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     }
+    const auto t4 = std::chrono::steady_clock::now();
+    using us = std::chrono::duration<double, std::micro>;
+    e->acc.host_calls += 1;
+    e->acc.host_prep_us += us(t1 - t0).count();
+    e->acc.host_launch_us += us(t2 - t1).count();
+    e->acc.host_wait_us += us(t3 - t2).count();
+    e->acc.host_post_us += us(t4 - t3).count();
     return JSP_OK;
 }
 
@@ -786,6 +910,7 @@ int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const 
     if (n == 0) return JSP_OK;
     if (!leader_rows || !levels || !domain_out) return set_err(JSP_EINVAL, "NULL buffer");
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(upload(e->tmp_a, leader_rows, n, s));
     HIP_TRY(upload(e->tmp_b, levels, n, s));
     HIP_TRY(e->tmp_c.reserve((size_t)n * 4));
@@ -810,6 +935,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
         if (follower_off[i] > follower_off[i + 1]) return set_err(JSP_EINVAL, "follower_off not monotone at %u", i);
     if (M > 0 && !follower_domains) return set_err(JSP_EINVAL, "follower_domains is NULL");
     hipStream_t s = e->stream;
+    if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s));
     HIP_TRY(upload(e->tmp_b, levels, n_jobs, s));
     HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s));
@@ -852,8 +978,17 @@ void* jsp_engine_stream(jsp_engine* e) { return e ? static_cast<void*>(e->stream
 
 int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
     HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->have_last && e->last_stream != e->stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
     return JSP_OK;
+}
+
+int jsp_engine_check(jsp_engine* e) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (e->have_last) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    return check_launch_error(e);
 }
 
 }  // extern "C"

@@ -72,9 +72,18 @@ struct TallyArgs {
     int W, R;
 };
 
+// Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks
+// workgroups): each workgroup draws a tile from a ticket and workgroups that
+// draw past the last tile exit at once. On an idle GPU the XCDs start a
+// launch's workgroups up to ~4 us apart, so the tiles go to the
+// workgroups that started first instead of waiting for the last XCD.
+constexpr uint32_t kSpareBlocks = 64;
+
 // Tail of place_fused_kernel (the last tally workgroup runs the assignment).
 struct FusedArgs {
-    unsigned long long* ticket;  // zeroed at snapshot upload, grows by n_blocks per launch
+    unsigned long long* ticket;  // [0] tile ticket, [1] finished-tile count; zeroed at snapshot upload
+    unsigned long long tile_base;  // ticket[0] before this launch (the host counts every draw)
+    unsigned long long done_base;  // ticket[1] before this launch
     uint32_t C;
     TopoDev topo;
     const uint32_t* t_off;
@@ -90,19 +99,24 @@ struct FusedArgs {
     size_t lds_bytes;
     uint32_t topo_in_lds;        // hierarchy tables staged in LDS for the tail
     uint32_t topo_lds_words;     // their size (0 when not staged)
+    uint32_t* done;              // host-mapped completion word (host path) or null
+    uint32_t epoch;              // value written to *done when the tail has finished
 };
 
 // Single-class leaf-level placement as one compaction pass (decoupled look-back).
 struct CompactArgs {
-    unsigned long long* ticket;    // shared with FusedArgs::ticket
+    unsigned long long* ticket;    // shared with FusedArgs::ticket ([0] only)
+    unsigned long long tile_base;  // ticket[0] before this launch
     unsigned long long* granules;  // [n_blocks] {epoch|status, value}, zeroed at snapshot upload
     uint32_t pods;
     uint32_t n_runs;
     uint32_t J;
     int32_t* assign;
-    uint32_t* stats;               // [0] runs [1] placed [2] look-back timeout flag
+    uint32_t* stats;               // [0] runs [1] placed
     uint32_t epoch;                // per-launch tag (host counter), 30-bit, never 0
-    uint32_t coresident;           // 1: every workgroup is resident at once, tile = blockIdx.x
+    uint32_t* err;                 // host-mapped error word: a tile whose look-back timed out writes epoch
+    uint32_t* done;                // host-mapped [n_blocks] completion words (host path) or null
+    uint32_t spin_limit;           // look-back polls before a tile gives up (JSP_LOOKBACK_SPINS in tests)
 };
 
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt; }

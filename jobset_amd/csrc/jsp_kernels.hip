@@ -63,6 +63,32 @@ __device__ __forceinline__ uint32_t div_invariant(uint32_t n, uint32_t magic, ui
     return shift == kDivIdentity ? n : t;
 }
 
+// Completion word of the host placement path: every wave's stores of this
+// workgroup (assign[] and stats, in pinned host memory) are drained, then one
+// lane publishes `value` (vector store, system scope). The host spins on the
+// word instead of waiting for the kernel-end signal, which saves the ~5 us of
+// the end-of-kernel completion path. `fence`: a system-scope
+// release first -- needed when the workgroup's output went out as plain
+// stores; output written with system-scope stores (store_sys) is already at
+// the host once its wave's vmcnt has drained.
+__device__ __forceinline__ void signal_host(uint32_t* word, uint32_t value, bool fence) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (fence) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// An output word: to pinned host memory as a system-scope (write-through)
+// store when `sys`, else a plain store.
+template <class T>
+__device__ __forceinline__ void store_out(T* p, T v, bool sys) {
+    if (sys) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
+
 // last leaf index l in [0, n) with ls[l] <= row (ls ascending, n+1 entries)
 __device__ __forceinline__ uint32_t leaf_search(const uint32_t* ls, uint32_t n, uint32_t row) {
     uint32_t lo = 0, hi = n;  // invariant: ls[lo] <= row, answer < hi
@@ -306,6 +332,7 @@ __device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
     }
     __syncthreads();
     JSP_STAMP(blk, 7);
+    if (a.cap_out == nullptr) return;  // the caller keeps the sums in LDS (compaction without tally output)
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
         const uint32_t leaf = a.leaf_base + l0 + li;
         for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * la + li];
@@ -1151,23 +1178,31 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
 // ticket add). The workgroup that draws the last ticket of this launch
 // acquires (agent fence + drain + barrier), builds every class's feasibility
 // bitmap in LDS and runs the assignment (cdna_hip_programming.md §6 G16).
-// The 64-bit ticket is zeroed at snapshot upload and only ever grows by
-// n_blocks per launch, so "last" = (old + 1) % n_blocks == 0.
+// Tiles come from ticket[0] (oversubscribed grid, kSpareBlocks); ticket[1]
+// counts finished tiles. Both 64-bit counters are zeroed at snapshot upload
+// and the host adds every launch's draws to its bases, so "my tile" =
+// old - tile_base and "last" = old + 1 - done_base == n_blocks.
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a, FusedArgs f) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    tally_block<W, R>(a, blockIdx.x, lds);
+    uint32_t* s_flag = lds + tally_lds_words(a);
+    if (threadIdx.x == 0)
+        *s_flag = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                             f.tile_base);
+    __syncthreads();
+    const uint32_t tile = *s_flag;
+    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
+    tally_block<W, R>(a, tile, lds);
 
     // publish
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    uint32_t* s_flag = lds + tally_lds_words(a);
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long old =
-            __hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = ((old + 1) % a.n_blocks) == 0 ? 1u : 0u;
+            __hip_atomic_fetch_add(f.ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (old + 1 - f.done_base) == a.n_blocks ? 1u : 0u;
     }
     __syncthreads();
     if (*s_flag == 0) return;
@@ -1233,6 +1268,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     else
         assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
                                            f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
+    if (f.done) signal_host(f.done, f.epoch, true);
 }
 
 // ----------------------------------------------------------------- single-class compaction
@@ -1256,14 +1292,14 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     uint32_t* s_x = lds + tally_lds_words(a);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
     const int tid = threadIdx.x, lane = tid & 63;
     const uint32_t epoch = f.epoch;  // host launch counter, 30-bit, never 0
-    uint32_t tile = blockIdx.x;
-    if (!f.coresident) {  // more tiles than resident slots: take tiles in start order
-        if (tid == 0)
-            s_x[0] = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) %
-                                a.n_blocks);
-        __syncthreads();
-        tile = s_x[0];
-    }
+    // tiles in start order (oversubscribed grid): a tile only ever waits on
+    // tiles that workgroups already hold, and the first-started take them all
+    if (tid == 0)
+        s_x[0] = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                            f.tile_base);
+    __syncthreads();
+    const uint32_t tile = s_x[0];
+    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
     JSP_STAMP(tile, 0);
     tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     JSP_STAMP(tile, 2);
@@ -1291,7 +1327,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
                     v = (uint32_t)x;
                 }
                 if (__all(idx < 0 || st != 0)) break;
-                if (++spins > (1u << 22)) { timeout = true; break; }
+                if (++spins > f.spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
             const unsigned long long pm = __ballot(idx >= 0 && st == kPrefix);
@@ -1302,7 +1338,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
             if (pm || timeout) break;
         }
         if (lane == 0) {
-            if (tile != 0) put_granule(g + tile, epoch, kPrefix, prefix + total);
+            // A tile that timed out knows no prefix: it publishes none (its
+            // aggregate stays visible, so later tiles still sum correctly past
+            // it), scatters nothing and reports the launch as failed.
+            if (tile != 0 && !timeout) put_granule(g + tile, epoch, kPrefix, prefix + total);
             s_x[2] = prefix;
             s_x[3] = timeout ? 1u : 0u;
         }
@@ -1310,16 +1349,22 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     __syncthreads();
     JSP_STAMP(tile, 4);
     const uint32_t prefix = s_x[2];
-    if (ok && prefix + rank < f.J) f.assign[prefix + rank] = (int32_t)(a.leaf_base + l0 + tid);
-    if (tile + 1 == a.n_blocks) {
-        const uint32_t placed = prefix + total < f.J ? prefix + total : f.J;
-        for (uint32_t j = placed + tid; j < f.J; j += kTallyThreads) f.assign[j] = -1;
-        if (tid == 0 && f.stats) {
-            f.stats[0] = f.n_runs;
-            f.stats[1] = placed;
-            f.stats[2] = s_x[3];
+    const bool failed = s_x[3] != 0;
+    const bool sys = f.done != nullptr;  // host path: assign[] and stats are in pinned host memory
+    if (!failed) {
+        if (ok && prefix + rank < f.J) store_out(f.assign + prefix + rank, (int32_t)(a.leaf_base + l0 + tid), sys);
+        if (tile + 1 == a.n_blocks) {
+            const uint32_t placed = prefix + total < f.J ? prefix + total : f.J;
+            for (uint32_t j = placed + tid; j < f.J; j += kTallyThreads) store_out(f.assign + j, -1, sys);
+            if (tid == 0 && f.stats) {
+                store_out(f.stats, f.n_runs, sys);
+                store_out(f.stats + 1, placed, sys);
+            }
         }
+    } else if (tid == 0) {
+        __hip_atomic_store(f.err, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    if (sys) signal_host(f.done + tile, epoch, false);
     JSP_STAMP(tile, 5);
 }
 
@@ -1398,18 +1443,19 @@ static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
 
 template <int W, int R>
 static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads), f.lds_bytes, s, a, f);
+    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
+                       s, a, f);
     return hipGetLastError();
 }
 
 template <int W, int R>
 static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL((place_compact_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
+    hipLaunchKernelGGL((place_compact_kernel<W, R>), dim3(a.n_blocks + kSpareBlocks), dim3(kTallyThreads),
                        compact_lds_bytes(a.la), s, a, f);
     return hipGetLastError();
 }
 
-#define JSP_DISPATCH_WR(FN, ...)              \
+#define JSP_DISPATCH_WR_OR(DEF, FN, ...)     \
     switch (a.W * 8 + a.R) {                  \
         case 9: return FN<1, 1>(__VA_ARGS__); \
         case 10: return FN<1, 2>(__VA_ARGS__); \
@@ -1427,8 +1473,9 @@ static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hi
         case 34: return FN<4, 2>(__VA_ARGS__); \
         case 35: return FN<4, 3>(__VA_ARGS__); \
         case 36: return FN<4, 4>(__VA_ARGS__); \
-        default: return hipErrorInvalidValue; \
+        default: return DEF;                  \
     }
+#define JSP_DISPATCH_WR(FN, ...) JSP_DISPATCH_WR_OR(hipErrorInvalidValue, FN, __VA_ARGS__)
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s) { JSP_DISPATCH_WR(launch_tally_wr, a, s) }
 
@@ -1441,6 +1488,7 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 }
 
 size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }
+
 
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
                        uint32_t topo_words) {

@@ -163,6 +163,34 @@ class Engine:
                            occ=None if occ is None else occ[:L], placed=st.placed, runs=st.runs,
                            wall_us=st.wall_us, fused=int(st.fused))
 
+    def host_placer(self, run_class: np.ndarray, run_len: np.ndarray):
+        """A pre-bound jsp_place call for one run list (host buffers allocated
+        once): what a caller that places the same JobSet repeatedly -- the
+        recovery path, the benchmark -- binds. Returns a callable; its
+        `.assign` array and `.stats` struct hold the last call's results."""
+        rc = np.ascontiguousarray(run_class, dtype=np.uint32)
+        rl = np.ascontiguousarray(run_len, dtype=np.uint32)
+        J = int(rl.astype(np.int64).sum())
+        assign = np.empty(max(J, 1), dtype=np.int32)
+        st = JspStats()
+        fn = self._lib.jsp_place
+        args = (self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data, None, None,
+                ctypes.byref(st))
+
+        def call() -> JspStats:
+            r = fn(*args)
+            if r:
+                check(r)
+            return st
+        call.assign = assign[:J]
+        call.stats = st
+        call.keep = (rc, rl, assign)
+        return call
+
+    def check(self) -> None:
+        """jsp_engine_check: wait for the engine's launches, raise if one failed."""
+        check(self._lib.jsp_engine_check(self._h))
+
     def place_device(self, d_run_class: int, d_run_len: int, n_runs: int, n_jobs: int, d_assign: int,
                      stream: Optional[int] = None) -> None:
         check(self._lib.jsp_place_device(self._h, d_run_class, d_run_len, n_runs, n_jobs, d_assign, stream))

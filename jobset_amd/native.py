@@ -44,7 +44,10 @@ class JspStats(ctypes.Structure):
 
 class JspTiming(ctypes.Structure):
     _fields_ = [("calls", ctypes.c_uint64), ("tally_ms", ctypes.c_double), ("feas_ms", ctypes.c_double),
-                ("assign_ms", ctypes.c_double), ("fused_ms", ctypes.c_double), ("fused_calls", ctypes.c_uint64)]
+                ("assign_ms", ctypes.c_double), ("fused_ms", ctypes.c_double), ("fused_calls", ctypes.c_uint64),
+                ("host_calls", ctypes.c_uint64), ("host_prep_us", ctypes.c_double),
+                ("host_launch_us", ctypes.c_double), ("host_wait_us", ctypes.c_double),
+                ("host_post_us", ctypes.c_double)]
 
 
 JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
@@ -73,6 +76,7 @@ SIGNATURES = [
     ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
     ("jsp_engine_stream", vp, [vp]),
     ("jsp_engine_sync", ctypes.c_int, [vp]),
+    ("jsp_engine_check", ctypes.c_int, [vp]),
 ]
 
 _lib = None

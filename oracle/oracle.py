@@ -176,6 +176,73 @@ def assign_from_tallies(p: Problem, cap: np.ndarray, occ: np.ndarray) -> np.ndar
     return assign[:pk.J]
 
 
+# ------------------------------------------------------------------ optimized threaded CPU evaluator
+_FAST_PATH = os.path.join(_HERE, "libjsp_cpufast.so")
+_fast = None
+
+
+def fast_lib():
+    """oracle/libjsp_cpufast.so (cpu_fast.c): the CPU baseline bench.py times;
+    bit-exact with place_c (tests/test_oracle.py)."""
+    global _fast
+    if _fast is None:
+        if not os.path.exists(_FAST_PATH) or os.path.getmtime(_FAST_PATH) < os.path.getmtime(
+                os.path.join(_HERE, "cpu_fast.c")):
+            build()
+        f = ctypes.CDLL(_FAST_PATH)
+        f.jspf_create.restype = ctypes.c_void_p
+        f.jspf_create.argtypes = [ctypes.c_int]
+        f.jspf_destroy.restype = None
+        f.jspf_destroy.argtypes = [ctypes.c_void_p]
+        f.jspf_threads.restype = ctypes.c_int
+        f.jspf_threads.argtypes = [ctypes.c_void_p]
+        f.jspf_prepare.restype = ctypes.c_int
+        f.jspf_prepare.argtypes = [ctypes.c_void_p, ctypes.POINTER(_Problem)]
+        f.jspf_run.restype = ctypes.c_int
+        f.jspf_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        _fast = f
+    return _fast
+
+
+class FastCPU:
+    """The optimized evaluator on `threads` host threads (a persistent pool).
+    prepare() is the untimed upload; run() one timed placement."""
+
+    def __init__(self, threads: int = 1):
+        self.lib = fast_lib()
+        self.h = self.lib.jspf_create(int(threads))
+        if not self.h:
+            raise MemoryError("jspf_create failed")
+        self.threads = self.lib.jspf_threads(self.h)
+        self.pk: Optional[PackedProblem] = None
+
+    def prepare(self, p: Problem) -> None:
+        self.pk = PackedProblem(p)
+        if self.lib.jspf_prepare(self.h, ctypes.byref(self.pk.st)) != 0:
+            raise MemoryError("jspf_prepare failed")
+        self.assign = np.empty(max(self.pk.J, 1), dtype=np.int32)
+
+    def run(self, want_tally: bool = False):
+        pk = self.pk
+        cap = np.empty((pk.C, max(pk.L, 1)), dtype=np.uint32) if want_tally else None
+        occ = np.empty(max(pk.L, 1), dtype=np.uint32) if want_tally else None
+        placed = self.lib.jspf_run(self.h, _ptr(self.assign), None if cap is None else _ptr(cap),
+                                   None if occ is None else _ptr(occ))
+        return (self.assign[:pk.J], None if cap is None else cap[:, :pk.L], None if occ is None else occ[:pk.L],
+                placed)
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.jspf_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 # ------------------------------------------------------------------ pure Python
 def place_py(p: Problem) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
     """Literal restatement for small cases: per-node loops and an O(J*D) greedy

@@ -424,3 +424,121 @@ def test_webhook_consults_engine_identically(engine):
     assert len({tuple(m.items()) for m in muts}) > 1
     sb, sp = bound.stats(), plain.stats()
     assert sb["nodeGets"] == 0 and sb["engineCalls"] > 0 and sp["nodeGets"] > 0
+
+
+def test_host_placer_equals_place(engine):
+    """The pre-bound host-API call the bench times returns the oracle's
+    assignment, repeatedly (completion words are tagged per launch)."""
+    from jobset_amd.snapshot import job_runs
+    for cfg in (1, 2, 3, 5):
+        p = synth.CONFIGS[cfg]()
+        engine.load(p)
+        call = engine.host_placer(*job_runs(p.job_class))
+        a = O.place_c(p)[0]
+        for _ in range(30):
+            st = call()
+            np.testing.assert_array_equal(call.assign, a)
+            assert st.placed == int((a >= 0).sum())
+
+
+def test_lookback_timeout_is_reported(engine, monkeypatch):
+    """A compaction launch whose look-back gives up must not return a silently
+    wrong assign[]: jsp_place raises, and on the device path jsp_engine_check
+    (or the next call) does. JSP_LOOKBACK_SPINS=0 makes every wait a timeout."""
+    import torch
+    from jobset_amd.native import JSP_EHIP
+    from jobset_amd.snapshot import job_runs
+    p = synth.config4()
+    p.classes = [p.classes[0]]
+    p.job_class = np.zeros(30_000, dtype=np.uint32)
+    monkeypatch.setenv("JSP_LOOKBACK_SPINS", "0")  # read at snapshot upload
+    engine.load(p)
+    with pytest.raises(JspError) as ei:
+        for _ in range(5):  # ~1000 tiles: some tile always finds a predecessor unpublished
+            engine.place(p.job_class)
+    assert ei.value.code == JSP_EHIP and "look-back" in str(ei.value)
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(JspError) as ei:
+        for _ in range(5):
+            engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
+            engine.check()
+    assert ei.value.code == JSP_EHIP
+    monkeypatch.delenv("JSP_LOOKBACK_SPINS")
+    engine.check()  # nothing new since the last report
+    engine.load(p)
+    got = engine.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    assert_same(got, a, cap, occ)
+
+
+@pytest.mark.parametrize("jobs", [0, 1, 39_000])
+def test_compaction_ticket_interleaved_with_fused(engine, jobs):
+    """Both single-launch kernels draw tiles from one ticket (oversubscribed
+    grids, spare workgroups exit) and the fused one counts finished tiles on a
+    second: their bases must stay right across interleaved launches of both
+    shapes and snapshot re-uploads."""
+    p = synth.config4()
+    p.classes = [p.classes[0]]
+    p.job_class = np.zeros(jobs, dtype=np.uint32)
+    q = synth.config5()
+    a, cap, occ = O.place_c(p)
+    aq = O.place_c(q)[0]
+    engine.load(p)
+    for _ in range(3):
+        got = engine.place(p.job_class, want_tally=True)
+        assert got.fused == 2
+        assert_same(got, a, cap, occ)
+    engine.load(q)
+    for _ in range(3):
+        np.testing.assert_array_equal(engine.place(q.job_class).assign, aq)
+    engine.load(p)
+    for _ in range(2):
+        np.testing.assert_array_equal(engine.place(p.job_class).assign, a)
+
+
+def test_patch_after_device_place_is_ordered(engine):
+    """jsp_snapshot_patch (engine stream) right after jsp_place_device on the
+    caller's stream must not overwrite rows the placement is still reading: the
+    engine orders the streams. Then the device placement on the caller's
+    stream sees the patch."""
+    import torch
+    from jobset_amd.snapshot import job_runs
+    p = synth.config2()
+    engine.load(p)
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    side = torch.cuda.Stream()
+    outs = [torch.empty(p.n_jobs, dtype=torch.int32, device="cuda") for _ in range(2)]
+    a0 = O.place_c(p)[0]
+    rows = np.arange(0, 15 * 40, 15, dtype=np.uint32)  # first node of racks 0..39
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, outs[0].data_ptr(), side.cuda_stream)
+    engine.patch_rows(rows, taints=np.ones(rows.shape[0], dtype=np.uint32))
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, outs[1].data_ptr(), side.cuda_stream)
+    engine.check()
+    np.testing.assert_array_equal(outs[0].cpu().numpy(), a0)
+    p.nodes.taints[rows] = 1
+    np.testing.assert_array_equal(outs[1].cpu().numpy(), O.place_c(p)[0])
+
+
+def test_tally_width_bound_is_erange(engine):
+    """Per-leaf capacities are u32 sums of min(pods, fit) over the leaf's rows:
+    classes whose pods x rows-per-leaf could reach 2^32 are refused."""
+    from jobset_amd.native import JSP_ERANGE
+    topo = Topology(level_keys=["k"], n_domains=[1], first_leaf=[np.arange(2, dtype=np.uint32)])
+    N = 2048
+    nodes = Nodes(leaf_start=np.array([0, N], dtype=np.uint32), labels=np.zeros((1, N), dtype=np.uint64),
+                  taints=np.zeros(N, dtype=np.uint32), free=np.full((1, N), 1 << 31, dtype=np.uint32),
+                  excl=np.full(N, -1, dtype=np.int32))
+    engine.upload_topology(topo)
+    engine.upload_snapshot(nodes)
+    with pytest.raises(JspError) as ei:
+        engine.upload_classes([JobClass(pods=1 << 21)])  # 2^21 x 2048 rows = 2^32
+    assert ei.value.code == JSP_ERANGE
+    engine.upload_classes([JobClass(pods=(1 << 21) - 1)])
+    got = engine.place(np.zeros(1, dtype=np.uint32), want_tally=True)
+    assert got.cap[0, 0] == ((1 << 21) - 1) * N and got.assign.tolist() == [0]

@@ -98,3 +98,27 @@ def test_invariant_checker_catches_violations():
     bad[-1] = -1
     with pytest.raises(AssertionError):
         O.check_invariants(p, bad, cap, occ)
+
+
+@pytest.mark.parametrize("threads", [1, 2, 3])
+def test_fast_cpu_evaluator_bit_exact(threads):
+    """oracle/cpu_fast.c (the bench's CPU baseline) equals cpu_ref.c on ragged
+    random snapshots (1-4 levels, empty leaves, W/R 1..4) and configs 1, 2, 3, 5,
+    at any thread count."""
+    fc = O.FastCPU(threads)
+    try:
+        problems = [synth.random_problem(s, max_nodes=3000) for s in range(25)]
+        problems += [synth.random_problem(5000 + s, max_nodes=20_000, max_levels=4, max_leaves=1500, max_jobs=1200)
+                     for s in range(3)]
+        problems += [synth.CONFIGS[c]() for c in (1, 2, 3, 5)]
+        for p in problems:
+            fc.prepare(p)
+            for _ in range(2):  # the pool and buffers are reused across runs
+                a, cap, occ, placed = fc.run(want_tally=True)
+                a2, cap2, occ2 = O.place_c(p)
+                np.testing.assert_array_equal(cap, cap2)
+                np.testing.assert_array_equal(occ, occ2)
+                np.testing.assert_array_equal(a, a2)
+                assert placed == int((a2 >= 0).sum())
+    finally:
+        fc.close()
