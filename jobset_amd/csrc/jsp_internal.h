@@ -119,7 +119,7 @@ struct CompactArgs {
     uint32_t spin_limit;           // look-back polls before a tile gives up (JSP_LOOKBACK_SPINS in tests)
 };
 
-constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt; }
+constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }
 constexpr uint32_t kFusedMaxWords = 6144;  // taken + feasibility words the fused tail keeps in LDS (48 KiB)
 constexpr uint32_t kFusedStage = 2048;     // ranks the fused tail stages per long-run step (8 KiB)
 constexpr uint32_t kMinStage = 4096;       // assign_kernel stages the bitmaps in LDS only if this much stage remains

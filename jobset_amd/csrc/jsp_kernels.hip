@@ -35,7 +35,15 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
     do {                                                                                  \
         if (threadIdx.x == 0 && (blk) < 4096) jsp_dbg[(blk) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+// shader-clock stamp (s_memtime) beside a real-time one: the effective clock of a phase
+#define JSP_CLK(blk, i)                                                                   \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && (blk) < 4096) jsp_dbg[(blk) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
+#define JSP_CLK(blk, i) \
+    do {                \
+    } while (0)
 #define JSP_STAMP(blk, i) \
     do {                  \
     } while (0)
@@ -53,6 +61,53 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int /*lane*/) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return x;
+}
+
+// Wave64 OR / unsigned-min of a value, uniform result (DPP row steps within
+// each 16-lane row, row_bcast15/31 across rows; lane 63 holds the total).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_or(uint32_t x) {
+    return x | (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = dpp_or<0x111, 0xf>(lo); hi = dpp_or<0x111, 0xf>(hi);  // row_shr:1
+    lo = dpp_or<0x112, 0xf>(lo); hi = dpp_or<0x112, 0xf>(hi);  // row_shr:2
+    lo = dpp_or<0x114, 0xf>(lo); hi = dpp_or<0x114, 0xf>(hi);  // row_shr:4
+    lo = dpp_or<0x118, 0xf>(lo); hi = dpp_or<0x118, 0xf>(hi);  // row_shr:8
+    lo = dpp_or<0x142, 0xa>(lo); hi = dpp_or<0x142, 0xa>(hi);  // row_bcast:15
+    lo = dpp_or<0x143, 0xc>(lo); hi = dpp_or<0x143, 0xc>(hi);  // row_bcast:31
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+}
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_and(uint32_t x) {
+    return x & (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFF, (int)x, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint64_t wave_and64(uint64_t v) {
+    uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+    lo = dpp_and<0x111, 0xf>(lo); hi = dpp_and<0x111, 0xf>(hi);
+    lo = dpp_and<0x112, 0xf>(lo); hi = dpp_and<0x112, 0xf>(hi);
+    lo = dpp_and<0x114, 0xf>(lo); hi = dpp_and<0x114, 0xf>(hi);
+    lo = dpp_and<0x118, 0xf>(lo); hi = dpp_and<0x118, 0xf>(hi);
+    lo = dpp_and<0x142, 0xa>(lo); hi = dpp_and<0x142, 0xa>(hi);
+    lo = dpp_and<0x143, 0xc>(lo); hi = dpp_and<0x143, 0xc>(hi);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)lo, 63);
+}
+// number of set bits of a uniform 64-bit mask below this lane
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+    // bound_ctrl off: lanes without a source keep their own value (old = x)
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x111, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x112, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xf, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xa, 0xf, false));
+    x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xc, 0xf, false));
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
 }
 
 // floor(n / d) for a divisor known per class, exact for every uint32 n
@@ -527,6 +582,7 @@ struct AssignMeta {
     uint32_t* s_rc;      // NT run classes (tile)
     uint32_t* s_ro;      // NT run job offsets (tile)
     uint32_t* s_long;    // NT indices of the tile's long runs
+    uint32_t* s_bcls;    // 64: class of each run start of a wave-0 batch (job offset -> class)
 };
 
 template <int NT>
@@ -546,6 +602,7 @@ __device__ __forceinline__ AssignMeta carve_meta(uint32_t* s_small) {
     m.s_rc = m.s_coff + 8;
     m.s_ro = m.s_rc + NT;
     m.s_long = m.s_ro + NT;
+    m.s_bcls = m.s_long + NT;
     return m;
 }
 
@@ -802,19 +859,6 @@ __device__ __forceinline__ uint32_t topo_par(const TopoDev& topo, const uint32_t
     else return (uint32_t)topo.par[k][i];
 }
 
-__device__ __forceinline__ uint64_t reg_load_f(const uint64_t* __restrict__ feas, uint32_t rc_l, uint32_t q, uint32_t C,
-                                               uint32_t g_toff, uint32_t g_woff, uint32_t g_nw, int lane) {
-    // g_*: run q's class fields, gathered per lane (lane = run), so every readlane
-    // here is indexed by q alone and none waits on another
-    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
-    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)g_toff, (int)q);
-    const uint32_t nw = (uint32_t)__builtin_amdgcn_readlane((int)g_nw, (int)q);
-    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)g_woff, (int)q);
-    if (c >= C) return 0ull;
-    const uint32_t wi = (uint32_t)lane - t0;  // wraps for lanes below the level
-    return wi < nw ? feas[wo + wi] : 0ull;
-}
-
 // Mark the descendants of every taken bit of `took` (level lvl, its words at
 // lanes [t0, ...)) at all finer levels: contiguous taken bits of one word are
 // one domain range, whose descendants are one range per level.
@@ -914,8 +958,6 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
     RegState rs;
     rs.T = rs.P = 0;  // s_taken starts zeroed
     rs.pend = -1;
-    uint32_t my_nw = 0;  // wave 0, lane c: bitmap words of class c's level
-    if (wid == 0 && (uint32_t)lane < C) my_nw = (my_D + 63) >> 6;
     for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
         // ---- a tile of runs: job offsets (block scan of run lengths) and the long-run list
         const uint32_t ri = r0 + tid;
@@ -931,97 +973,164 @@ __device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, cons
         __syncthreads();
         const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
         if (wid == 0 && regmode) {
-            for (uint32_t t0 = 0; t0 < nr; t0 += 64) {
-                const uint32_t tl = t0 + (uint32_t)lane;
-                const uint32_t rc_l = tl < nr ? m.s_rc[tl] : 0u;
-                const uint32_t ro_l = tl < nr ? m.s_ro[tl] : 0u;
-                const uint32_t rn_l = tl + 1 < nr ? m.s_ro[tl + 1] : tile_total;
-                const uint32_t nb = (nr - t0) < 64u ? (nr - t0) : 64u;
-                // feasibility word of run q's class for this lane (0 outside its level),
-                // loaded one run ahead so it is in flight while the previous run is placed
-                JSP_STAMP(4010u + t0 / 64, 0);
-                // class fields of each lane's run (lane = run t0 + lane), one gather per 64 runs
-                const int cc = (int)(rc_l < C ? rc_l : 0u);
-                const uint32_t g_toff = (uint32_t)__shfl((int)my_toff, cc);
-                const uint32_t g_woff = (uint32_t)__shfl((int)my_woff, cc);
-                const uint32_t g_nw = (uint32_t)__shfl((int)my_nw, cc);
-                const uint32_t g_lvl = (uint32_t)__shfl((int)my_lvl, cc);
-                uint64_t f_next = reg_load_f(feas, rc_l, 0, C, g_toff, g_woff, g_nw, lane);
-                for (uint32_t q = 0; q < nb; ++q) {
-                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 0);
-                    const uint64_t f = f_next;
-                    if (q + 1 < nb) f_next = reg_load_f(feas, rc_l, q + 1, C, g_toff, g_woff, g_nw, lane);
-                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 1);
-                    const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)rc_l, (int)q);
-                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readlane((int)ro_l, (int)q);
-                    const uint32_t o1 = (uint32_t)__builtin_amdgcn_readlane((int)rn_l, (int)q);
-                    const uint32_t j0 = jbase + o0;
-                    const uint32_t jend = jbase + o1 < J ? jbase + o1 : J;
-                    if (j0 >= jend) continue;
-                    if (c >= C) {  // malformed run: its jobs are unplaceable
-                        for (uint32_t j = j0 + lane; j < jend; j += 64) assign[j] = -1;
-                        continue;
-                    }
-                    const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)g_lvl, (int)q);
-                    const uint32_t t0l = (uint32_t)__builtin_amdgcn_readlane((int)g_toff, (int)q);
-                    if (o1 - o0 > kWaveRunMax) {
-                        // long run: fold pending ancestors, publish the bitmaps, join the
-                        // workgroup (cursor 0: the whole level is one window), reload
-                        if (rs.pend >= 1) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
-                        if ((uint32_t)lane < t_words) s_taken[lane] = rs.T;
-                        if (lane == 0) m.s_cursor[c] = 0;
-                        long_run<NT, TOPO_LDS>(c, j0, jend, feas, topo, assign, s_taken, m, s_topo, s_win, s_stage,
-                                               stage_cap, recs, placed);
-                        if ((uint32_t)lane < t_words) rs.T = s_taken[lane];
-                        continue;
-                    }
-                    if (rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
-                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 2);
-                    const uint64_t avail = f & ~rs.T;
-                    const uint32_t n = jend - j0;
-                    uint64_t took = 0;
-                    if (n == 1) {
-                        const uint64_t nz = __ballot(avail != 0);
-                        if (nz == 0) {
-                            if (lane == 0) assign[j0] = -1;
-                        } else {
-                            const int k = __builtin_ctzll(nz);
-                            const uint64_t word =
-                                ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(avail >> 32), k) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)avail, k);
-                            const uint32_t b = (uint32_t)__builtin_ctzll(word);
-                            if (lane == 0) assign[j0] = (int32_t)(((uint32_t)k - t0l) * 64 + b);
-                            took = lane == k ? (1ull << b) : 0ull;
-                            placed += 1;
-                        }
-                    } else {
-                        const uint32_t cnt = (uint32_t)__popcll(avail);
-                        const uint32_t incl = wave_incl_scan(cnt, lane);
-                        const uint32_t pre = incl - cnt;
-                        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                        const uint32_t used = total < n ? total : n;
-                        if (cnt != 0 && pre < used)
-                            took = pre + cnt <= used ? avail : avail & ((1ull << select_bit(avail, used - pre)) - 1ull);
-                        uint64_t x = took;
-                        uint32_t r = j0 + pre;
-                        while (x) {
-                            assign[r++] = (int32_t)(((uint32_t)lane - t0l) * 64 + (uint32_t)__builtin_ctzll(x));
-                            x &= x - 1;
-                        }
-                        for (uint32_t j = j0 + used + lane; j < jend; j += 64) assign[j] = -1;
-                        placed += used;
-                    }
-                    rs.T |= took;
-                    if (lvl >= 1) {
-                        rs.P |= took;
-                        rs.pend = rs.pend > (int)lvl ? rs.pend : (int)lvl;
-                    }
-                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 3);
-                    if (lvl + 1 < K) reg_mark_desc<TOPO_LDS>(rs, took, lvl, t0l, K, topo, s_topo, m, lane);
-                    if (t0 == 0 && q < 16) JSP_STAMP(4030u + q, 4);
-                    if (q == 15 || q == 31 || q == 47) JSP_STAMP(4010u + t0 / 64, 1 + q / 16);
+            // Short runs are taken in batches: up to 64 consecutive jobs (lane = job)
+            // of short runs at one level. Within a batch the lowest-index greedy
+            // ("each job in order takes its lowest free feasible domain") equals the
+            // domain-order greedy ("each domain in order goes to the earliest
+            // untaken job that finds it feasible": with one priority order per
+            // side, both are the same unique stable matching). So the batch scans
+            // the level's words from the lowest class cursor; per word each lane
+            // holds its job's free feasible bits and every candidate domain costs
+            // one ballot plus a few scalar ops -- no per-job chain of dependent
+            // vector work.
+            uint32_t q = 0, nbatch = 0;
+            while (q < nr) {
+                const uint32_t rk = q + (uint32_t)lane;
+                const bool in = rk < nr;
+                const uint32_t rc_v = in ? m.s_rc[rk] : 0xFFFFFFFFu;
+                const uint32_t ro_v = in ? m.s_ro[rk] : tile_total;
+                const uint32_t re_v = rk + 1 < nr ? m.s_ro[rk + 1] : tile_total;
+                const uint32_t c = (uint32_t)__builtin_amdgcn_readfirstlane((int)rc_v);
+                const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ro_v);
+                const uint32_t o1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)re_v);
+                const uint32_t j0 = jbase + o0;
+                const uint32_t jend = jbase + o1 < J ? jbase + o1 : J;
+                if (j0 >= jend) {
+                    ++q;
+                    continue;
                 }
-                JSP_STAMP(4010u + t0 / 64, 4);
+                if (c >= C) {  // malformed run: its jobs are unplaceable
+                    for (uint32_t j = j0 + lane; j < jend; j += 64) assign[j] = -1;
+                    ++q;
+                    continue;
+                }
+                if (o1 - o0 > kWaveRunMax) {
+                    // long run: fold pending ancestors, publish the bitmaps, join the
+                    // workgroup (cursor 0: the whole level is one window), reload
+                    if (rs.pend >= 1) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
+                    if ((uint32_t)lane < t_words) s_taken[lane] = rs.T;
+                    if (lane == 0) m.s_cursor[c] = 0;
+                    long_run<NT, TOPO_LDS>(c, j0, jend, feas, topo, assign, s_taken, m, s_topo, s_win, s_stage,
+                                           stage_cap, recs, placed);
+                    if ((uint32_t)lane < t_words) rs.T = s_taken[lane];
+                    ++q;
+                    continue;
+                }
+                const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
+                const uint32_t sb = 4010u + (nbatch < 39u ? nbatch : 39u);
+                (void)sb;
+                ++nbatch;
+                JSP_STAMP(sb, 0);
+                // ---- the batch: runs q .. q+nrb-1 (lane k = run q+k), all short, valid,
+                // at level lvl, ending within 64 jobs of o0
+                const uint32_t lvl_v = (uint32_t)__shfl((int)my_lvl, (int)(rc_v < C ? rc_v : 0u));
+                const bool ok_v = in && rc_v < C && lvl_v == lvl && re_v - ro_v <= kWaveRunMax && re_v - o0 <= 64u;
+                const uint64_t okm = __ballot(ok_v);
+                const uint32_t nrb = ~okm == 0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);  // >= 1: run q qualifies
+                uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)re_v, (int)nrb - 1) - o0;
+                if (j0 + nb > J) nb = J - j0;
+                // job offset -> class: each non-empty run writes its class at its first
+                // job; a job takes the class of the last run start at or below it
+                const bool starts = (uint32_t)lane < nrb && re_v > ro_v;
+                if (starts) m.s_bcls[ro_v - o0] = rc_v;
+                const uint64_t smask = wave_or64(starts ? 1ull << (ro_v - o0) : 0ull);
+                const uint64_t le = (uint32_t)lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                const bool job = (uint32_t)lane < nb;
+                const uint32_t my_start = job ? 63u - (uint32_t)__builtin_clzll(smask & le) : 0u;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t cls = job ? m.s_bcls[my_start] : 0u;
+                const uint32_t woff = (uint32_t)__shfl((int)my_woff, (int)cls);
+                q += nrb;
+                if (rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
+                // classes of the batch; the scan starts at their lowest cursor (every
+                // class's domains below its cursor are taken or infeasible)
+                const uint64_t cmask = wave_or64(job ? 1ull << cls : 0ull);
+                const uint32_t D = m.s_D[lvl];
+                const uint32_t curc = (uint32_t)lane < C && ((cmask >> lane) & 1ull) ? my_cur : D;
+                const uint32_t d0 = wave_min_u32(curc);
+                const uint32_t tl = m.s_toff[lvl], nwl = (D + 63) >> 6;
+                uint64_t unassigned = __ballot(job);
+                int32_t res = -1;
+                uint64_t tookv = 0;
+                JSP_STAMP(sb, 1);
+                for (uint32_t w = d0 >> 6; w < nwl && unassigned != 0; ++w) {
+                    const uint64_t tw =
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rs.T >> 32), (int)(tl + w)) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rs.T, (int)(tl + w));
+                    const bool mine = (unassigned >> lane) & 1ull;
+                    const uint64_t av = mine ? feas[woff + w] & ~tw : 0ull;
+                    const uint64_t any = wave_or64(av);
+                    if (any == 0ull) continue;
+                    // Per word: domains every unassigned job can take ("universal") go
+                    // to the unassigned jobs in job order; a domain only some can take
+                    // is settled on its own, in domain order: the universal domains
+                    // below it have gone to the first m jobs, so it goes to the first
+                    // job after those that can take it. Only these are sequential.
+                    const uint64_t univ = wave_and64(mine ? av : ~0ull);
+                    uint64_t nu = any & ~univ;
+                    uint64_t R = unassigned;  // not taken by a non-universal domain (yet)
+                    uint32_t rank = mbcnt64(R);
+                    uint64_t took = 0;
+                    while (nu != 0ull) {
+                        uint32_t vq[4], mq[4];
+                        uint64_t lq[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint64_t low = nu & (0ull - nu);
+                            nu ^= low;
+                            vq[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(low ? (uint32_t)__builtin_ctzll(low) : 0u));
+                            mq[u] = (uint32_t)__popcll(univ & (low - 1ull));
+                            lq[u] = low ? __ballot((av & low) != 0ull) : 0ull;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint64_t col = __ballot(rank >= mq[u]) & R & lq[u];
+                            const uint64_t win = col & (0ull - col);
+                            R ^= win;
+                            rank = mbcnt64(R);
+                            took |= win ? (1ull << vq[u]) : 0ull;
+                            if (((win >> lane) & 1ull) != 0ull) res = (int32_t)(w * 64 + vq[u]);
+                        }
+                    }
+                    // universal domains: the r-th job left in R takes the r-th of them
+                    const uint32_t nuniv = (uint32_t)__popcll(univ);
+                    const bool inr = (R >> lane) & 1ull;
+                    if (inr && rank < nuniv) res = (int32_t)(w * 64 + select_bit(univ, rank));
+                    const uint32_t nr_left = (uint32_t)__popcll(R);
+                    if (nr_left != 0u && univ != 0ull) {
+                        if (nr_left >= nuniv) {
+                            took |= univ;
+                        } else {  // the last job of R took the highest universal domain used
+                            const int32_t hi = __builtin_amdgcn_readlane(res, 63 - __builtin_clzll(R));
+                            const uint32_t pos = (uint32_t)hi & 63u;
+                            took |= univ & (pos == 63u ? ~0ull : ((2ull << pos) - 1ull));
+                        }
+                    }
+                    unassigned &= R & ~__ballot(inr && rank < nuniv);
+                    if ((uint32_t)lane == tl + w) tookv |= took;
+                }
+                JSP_STAMP(sb, 2);
+                if (job) assign[j0 + lane] = res;
+                placed += (uint32_t)__popcll(__ballot(job && res >= 0));
+                // cursors: a class's last job in the batch holds its largest domain
+                // (or -1: the class has nothing left at this level)
+                uint64_t cm = cmask;
+                while (cm != 0ull) {
+                    const uint32_t cc = (uint32_t)__builtin_ctzll(cm);
+                    cm &= cm - 1ull;
+                    const uint64_t lanes_c = __ballot(job && cls == cc);
+                    const int32_t last = __builtin_amdgcn_readlane(res, 63 - __builtin_clzll(lanes_c));
+                    if ((uint32_t)lane == cc) my_cur = last < 0 ? D : (uint32_t)last + 1u;
+                }
+                rs.T |= tookv;
+                if (lvl >= 1) {
+                    rs.P |= tookv;
+                    rs.pend = rs.pend > (int)lvl ? rs.pend : (int)lvl;
+                }
+                if (lvl + 1 < K) reg_mark_desc<TOPO_LDS>(rs, tookv, lvl, tl, K, topo, s_topo, m, lane);
+                JSP_STAMP(sb, 3);
             }
         } else if (wid == 0) {
             for (uint32_t t0 = 0; t0 < nr; t0 += 64) {
@@ -1206,6 +1315,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     }
     __syncthreads();
     if (*s_flag == 0) return;
+    JSP_STAMP(4000u, 1);
     // the tail: small tables first (independent of the other workgroups' sums)
     uint64_t* s_taken = reinterpret_cast<uint64_t*>(lds);
     uint64_t* s_win = s_taken + f.t_words;
@@ -1218,56 +1328,93 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     if (threadIdx.x == 0) m.s_misc[1] = 0;
     if (f.topo_in_lds) stage_topo<kTallyThreads>(s_topo, f.topo);
     for (uint32_t i = threadIdx.x; i < f.t_words; i += kTallyThreads) s_taken[i] = 0;
+    for (uint32_t i = threadIdx.x; i < f.feas_words; i += kTallyThreads) s_feas[i] = 0;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
+    JSP_STAMP(4000u, 3);
     // feasibility bitmaps of every class into LDS. The tallies were written by
-    // other workgroups (after the acquire every load misses to HBM/MALL), so a
-    // wave issues the loads of kTailBatch leaf-level words before it uses any.
+    // other workgroups (after the acquire every load misses to HBM/MALL), so
+    // loads are issued in bulk before they are used.
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    constexpr int kTailBatch = 8;
     const uint32_t Kt = f.topo.K;
-    for (uint32_t g0 = wid; g0 < f.feas_words; g0 += kTallyWaves * kTailBatch) {
-        uint32_t cv[kTailBatch], ov[kTailBatch], cc[kTailBatch];
+    // per-class fields in registers (lane c = class c)
+    const uint32_t c_beg = (uint32_t)lane < f.C ? m.s_woff[lane] : 0u;
+    const uint32_t c_end = (uint32_t)lane < f.C ? m.s_woff[lane + 1] : 0u;
+    const uint32_t c_lvl = (uint32_t)lane < f.C ? m.s_lvl[lane] : 0xFFFFu;
+    const uint32_t c_pods = (uint32_t)lane < f.C ? m.s_pods[lane] : 0u;
+    const uint64_t leaf_cls = __ballot((uint32_t)lane < f.C && c_lvl + 1 == Kt);
+    const uint64_t upper_cls = __ballot((uint32_t)lane < f.C && c_lvl + 1 < Kt);
+    // leaf-level classes: every thread takes 4-leaf chunks, loads occupancy once and
+    // every class's capacities (8 classes per pass, all loads first), then ORs each
+    // class's 4 feasibility bits into its LDS word
+    {
+        const uint32_t L = f.topo.D[Kt - 1];
+        const uint32_t nlc = (uint32_t)__popcll(leaf_cls);
+        for (uint32_t q = threadIdx.x; q * 4u < L; q += kTallyThreads) {
+            const uint32_t l0 = q * 4u;
+            uint32_t ov[4];
 #pragma unroll
-        for (int u = 0; u < kTailBatch; ++u) {
-            const uint32_t gw = g0 + (uint32_t)u * kTallyWaves;
-            cv[u] = 0;
-            ov[u] = 1;
-            cc[u] = 0;
-            if (gw < f.feas_words) {
-                uint32_t c = 0;
-                while (m.s_woff[c + 1] <= gw) ++c;
-                cc[u] = c;
-                const uint32_t lvl = m.s_lvl[c];
-                const uint32_t d = (gw - m.s_woff[c]) * 64 + (uint32_t)lane;
-                if (lvl + 1 == Kt && d < f.topo.D[lvl]) {
-                    cv[u] = a.cap_out[(size_t)c * a.ld + d];
-                    ov[u] = a.occ_out[d];
+            for (int i = 0; i < 4; ++i) ov[i] = l0 + i < L ? a.occ_out[l0 + i] : 1u;
+            for (uint32_t j0 = 0; j0 < nlc; j0 += 8) {
+                uint32_t cid[8], cv[8][4];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t j = j0 + (uint32_t)u;
+                    cid[u] = j < nlc ? select_bit(leaf_cls, j) : 0u;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        cv[u][i] = (j < nlc && l0 + i < L) ? a.cap_out[(size_t)cid[u] * a.ld + l0 + i] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    if (j0 + (uint32_t)u >= nlc) break;
+                    const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)c_pods, (int)cid[u]);
+                    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)c_beg, (int)cid[u]);
+                    uint64_t bits = 0;
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) bits |= (cv[u][i] >= pods && ov[i] == 0u) ? (1ull << i) : 0ull;
+                    if (bits) atomicOr(reinterpret_cast<unsigned long long*>(&s_feas[wo + (l0 >> 6)]),
+                                       (unsigned long long)(bits << (l0 & 63u)));
                 }
             }
         }
-#pragma unroll
-        for (int u = 0; u < kTailBatch; ++u) {
-            const uint32_t gw = g0 + (uint32_t)u * kTallyWaves;
-            if (gw >= f.feas_words) break;
-            const uint32_t c = cc[u], lvl = m.s_lvl[c];
-            const uint64_t word =
-                lvl + 1 == Kt ? __ballot(cv[u] >= m.s_pods[c] && ov[u] == 0)
-                              : feas_word_upper(a.cap_out, a.occ_out, a.ld, lvl, m.s_pods[c], c, gw - m.s_woff[c],
-                                                f.topo, lane);
-            if (lane == 0) s_feas[gw] = word;
+    }
+    // classes above the leaves: one wave per word (prefix sums over the word's
+    // leaf range, feas_word_upper), words dealt to the waves in turn
+    {
+        uint64_t uc = upper_cls;
+        uint32_t base = 0;
+        while (uc != 0ull) {
+            const uint32_t c = (uint32_t)__builtin_ctzll(uc);
+            uc &= uc - 1ull;
+            const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)c_beg, (int)c);
+            const uint32_t we = (uint32_t)__builtin_amdgcn_readlane((int)c_end, (int)c);
+            const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)c_lvl, (int)c);
+            const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)c_pods, (int)c);
+            for (uint32_t gw = wb; gw < we; ++gw) {
+                if ((base + gw - wb) % kTallyWaves == (uint32_t)wid) {
+                    const uint64_t word = feas_word_upper(a.cap_out, a.occ_out, a.ld, lvl, pods, c, gw - wb, f.topo, lane);
+                    if (lane == 0) s_feas[gw] = word;
+                }
+            }
+            base += we - wb;
         }
     }
     __syncthreads();
+    JSP_STAMP(4000u, 2);
+    JSP_CLK(4090u, 0);
+    JSP_STAMP(4090u, 1);
     if (f.topo_in_lds)
         assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
     else
         assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
                                            f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
+    JSP_CLK(4090u, 2);
+    JSP_STAMP(4090u, 3);
     if (f.done) signal_host(f.done, f.epoch, true);
 }
 

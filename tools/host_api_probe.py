@@ -18,9 +18,10 @@ def main():
     from jobset_amd.snapshot import job_runs
     torch.cuda.init()
     eng = Engine(0)
-    for cfg in (1, 2, 3, 5):
+    for cfg, fused in ((1, True), (2, True), (3, True), (5, True), (5, False), (3, False)):
         p = synth.CONFIGS[cfg]()
         eng.load(p)
+        eng.set_fused(fused)
         call = eng.host_placer(*job_runs(p.job_class))
         for _ in range(50):
             call()
@@ -46,7 +47,8 @@ def main():
             if i >= 20:
                 dev.append((time.perf_counter() - t0) * 1e6)
         dev.sort()
-        print(f"cfg{cfg}: host API p50 {wall[500]:.1f} us p99 {wall[990]:.1f} | lib phases (mean us): prep "
+        eng.set_fused(True)
+        print(f"cfg{cfg}{'' if fused else ' (three launches)'}: host API p50 {wall[500]:.1f} us p99 {wall[990]:.1f} | lib phases (mean us): prep "
               f"{t.host_prep_us / n:.2f} launch {t.host_launch_us / n:.2f} wait {t.host_wait_us / n:.2f} post "
               f"{t.host_post_us / n:.2f} | device path + stream sync p50 {dev[len(dev) // 2]:.1f} us",
               flush=True)

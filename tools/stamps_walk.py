@@ -34,7 +34,7 @@ def main():
     rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
     out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
     buf = np.zeros(4096 * 8, dtype=np.uint64)
-    rows = []
+    rows, clk = [], []
     for i in range(reps):
         lib.jsp_debug_clear()
         torch.cuda.synchronize()
@@ -46,8 +46,12 @@ def main():
         t0 = nz.min() if nz.size else 0
         sel = st[4000:4050]
         rows.append(np.where(sel != 0, (sel - t0) * 10, -1))
+        r = st[4090]
+        if r[0] and r[2]:
+            clk.append((r[2] - r[0]) / ((r[3] - r[1]) * 10.0))  # shader cycles per ns = GHz
     med = np.median(np.stack(rows[3:]), axis=0)
-    print(f"cfg{cfg} fused={fused} runs={rc.shape[0]}: ns from the launch's first stamp")
+    print(f"cfg{cfg} fused={fused} runs={rc.shape[0]}: ns from the launch's first stamp; "
+          f"effective shader clock over the walk {np.median(clk) if clk else float('nan'):.2f} GHz")
     for r in range(50):
         if (med[r] >= 0).any():
             print(f"  row {4000 + r}: " + "  ".join(f"{x:8.0f}" for x in med[r]))
