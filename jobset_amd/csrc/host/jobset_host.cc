@@ -25,6 +25,7 @@
 #include "../../../include/jsk_host.h"
 #include "../../../include/jsplace.h"
 #include "json.h"
+#include "placement.h"
 #include "sha1.h"
 
 namespace jsk {
@@ -357,6 +358,8 @@ struct Cache {
     std::vector<std::string> level_keys;
     std::vector<std::vector<std::string>> domain_values;
     std::vector<std::map<std::string, int32_t>> domain_ids;
+    // planner: the engine's snapshot built from this cache's objects (placement.h)
+    std::unique_ptr<Planner> planner;
     // call counters (tests check which path ran)
     int64_t node_gets = 0, pod_lists = 0, engine_calls = 0;
     std::vector<std::string> deleted, status_updates;
@@ -401,24 +404,43 @@ Err listPods(Cache& c, const std::string& ns, const std::string& field, const st
 
 // Topology value of the node a pod is bound to: pod_mutating_webhook.go:173-194
 // and pod_controller.go:242-263 (identical logic). With an engine bound, the
-// domain comes from the resident snapshot (jsp_resolve_leader_domains);
-// NotFound keeps the reference's "" + nil, a missing label its error.
+// domain of a node the snapshot holds, at one of its topology levels, comes
+// from the resident snapshot (jsp_resolve_leader_domains). Anything else -- a
+// key that is not an engine level, a node the snapshot does not hold (absent
+// from the cache, or lacking a level label) -- takes the reference's Node Get
+// path, so NotFound stays "" + nil and a missing label stays its error.
+bool engineTopology(Cache& c, const std::string& node, const std::string& key, int32_t* row, uint32_t* level) {
+    if (!c.eng) return false;
+    if (c.planner) {
+        const int lk = c.planner->level_of(key);
+        if (lk < 0 || !c.planner->synced() || !c.planner->row_of(node, row)) return false;
+        *level = (uint32_t)lk;
+        return true;
+    }
+    auto lk = std::find(c.level_keys.begin(), c.level_keys.end(), key);
+    auto it = c.node_rows.find(node);
+    if (lk == c.level_keys.end() || it == c.node_rows.end()) return false;
+    *row = it->second;
+    *level = (uint32_t)(lk - c.level_keys.begin());
+    return true;
+}
+
+const std::string& domainValue(Cache& c, uint32_t level, int32_t dom) {
+    static const std::string empty;
+    const std::vector<std::string>& v = c.planner ? c.planner->domain_values((int)level) : c.domain_values[level];
+    return dom >= 0 && (size_t)dom < v.size() ? v[dom] : empty;
+}
+
 Err topologyFromPod(Cache& c, const Json& pod, const std::string& key, std::string* out) {
     const std::string node = node_name(pod);
-    if (c.eng) {
-        auto lk = std::find(c.level_keys.begin(), c.level_keys.end(), key);
-        auto it = c.node_rows.find(node);
-        if (it == c.node_rows.end()) { *out = ""; return Err::none(); }  // NotFound
-        if (lk == c.level_keys.end()) return Err::e("node does not have topology label: " + key);
-        const int32_t row = it->second;
-        const uint32_t level = (uint32_t)(lk - c.level_keys.begin());
+    int32_t row = -1;
+    uint32_t level = 0;
+    if (engineTopology(c, node, key, &row, &level)) {
         int32_t dom = -1;
         ++c.engine_calls;
         if (jsp_resolve_leader_domains(c.eng, &row, &level, 1, &dom) != JSP_OK)
             return Err::e(std::string("placement engine: ") + jsp_last_error());
-        if (dom < 0 || (size_t)dom >= c.domain_values[level].size())
-            return Err::e("node does not have topology label: " + key);
-        *out = c.domain_values[level][dom];
+        *out = domainValue(c, level, dom);
         return Err::none();
     }
     Json n;
@@ -533,6 +555,82 @@ Err Default(Cache& c, Json& pod) {
     return setNodeSelector(c, pod);
 }
 
+// Default over a batch of pods -- every pod of a JobSet's (re)created Jobs as
+// the Job controller creates them: per pod exactly
+// Default's result and error, but the followers whose leader node the engine
+// holds at a level key are resolved by ONE jsp_resolve_leader_domains call.
+Json DefaultBatch(Cache& c, const Json& pods) {
+    struct Pending {
+        size_t i;
+        int32_t row;
+        uint32_t level;
+        std::string key;
+    };
+    std::vector<Pending> pend;
+    std::vector<Json> res;
+    std::vector<Err> errs;
+    for (size_t i = 0; i < pods.size(); ++i) {
+        Json pod = pods.at(i);
+        Err e = Err::none();
+        const Json& ann = annotations(pod);
+        if (has_key(ann, kExclusiveKey) && !has_key(ann, kNodeSelectorStrategyKey)) {
+            if (str_at(ann, kJobCompletionIndexAnnotation) == "0") {
+                setExclusiveAffinities(pod);
+            } else {
+                // setNodeSelector's order: leader lookup, leader bound, then the topology value
+                Json leader;
+                if (leaderPodForFollower(c, pod, &leader).ok && !node_name(leader).empty()) {
+                    const std::string key = str_at(ann, kExclusiveKey);
+                    int32_t row = -1;
+                    uint32_t level = 0;
+                    if (engineTopology(c, node_name(leader), key, &row, &level)) {
+                        pend.push_back({i, row, level, key});
+                    } else {
+                        std::string value;
+                        e = topologyFromPod(c, leader, key, &value);
+                        if (e.ok) {
+                            Json& ns = pod["spec"]["nodeSelector"];
+                            if (!ns.is_object()) ns = Json::object();
+                            ns[key] = value;
+                        }
+                    }
+                }
+            }
+        }
+        res.push_back(std::move(pod));
+        errs.push_back(e);
+    }
+    if (!pend.empty()) {
+        std::vector<int32_t> rows, doms(pend.size(), -1);
+        std::vector<uint32_t> levels;
+        for (const auto& p : pend) {
+            rows.push_back(p.row);
+            levels.push_back(p.level);
+        }
+        ++c.engine_calls;
+        const bool ok = jsp_resolve_leader_domains(c.eng, rows.data(), levels.data(), (uint32_t)rows.size(),
+                                                   doms.data()) == JSP_OK;
+        const std::string msg = ok ? "" : std::string("placement engine: ") + jsp_last_error();
+        for (size_t k = 0; k < pend.size(); ++k) {
+            if (!ok) {
+                errs[pend[k].i] = Err::e(msg);
+                continue;
+            }
+            Json& ns = res[pend[k].i]["spec"]["nodeSelector"];
+            if (!ns.is_object()) ns = Json::object();
+            ns[pend[k].key] = domainValue(c, pend[k].level, doms[k]);
+        }
+    }
+    Json out = Json::array();
+    for (size_t i = 0; i < res.size(); ++i) {
+        Json x = Json::object();
+        x["pod"] = res[i];
+        x["error"] = errs[i].ok ? Json() : Json(errs[i].msg);
+        out.push_back(x);
+    }
+    return out;
+}
+
 // leaderPodScheduled, pod_admission_webhook.go:78-89
 Err leaderPodScheduled(Cache& c, const Json& pod, bool* scheduled) {
     Json leader;
@@ -561,10 +659,51 @@ Err ValidateCreate(Cache& c, const Json& pod) {
 }
 
 // ============================================================ PodReconciler
-// validatePodPlacements, pod_controller.go:172-194 (A9)
+// validatePodPlacements, pod_controller.go:172-194 (A9). With an engine
+// holding the leader's node at the key's level, the whole job is checked by
+// one jsp_audit_placements call (followers' selector values as domain ids
+// against the leader's row); only when it reports a mismatch are the
+// followers walked on the host, to return the reference's first error.
 Err validatePodPlacements(Cache& c, const Json& leader, const Json& podList, bool* valid) {
     *valid = false;
     const std::string key = str_at(annotations(leader), kExclusiveKey);
+    int32_t row = -1;
+    uint32_t level = 0;
+    if (c.planner && engineTopology(c, node_name(leader), key, &row, &level)) {
+        std::vector<int32_t> fdom;
+        bool selector_error = false;
+        for (const auto& pod : podList.elems()) {
+            if (IsLeaderPod(pod)) continue;
+            std::string ft;
+            if (!followerPodTopology(pod, key, &ft).ok) {
+                selector_error = true;
+                break;
+            }
+            const int32_t d = c.planner->domain_id((int)level, ft);
+            fdom.push_back(d < 0 ? -2 : d);  // a value no domain has never matches
+        }
+        if (!selector_error) {
+            const uint32_t off[2] = {0, (uint32_t)fdom.size()};
+            uint32_t bad = 0;
+            ++c.engine_calls;
+            if (jsp_audit_placements(c.eng, &row, &level, off, fdom.empty() ? nullptr : fdom.data(), 1, &bad) != JSP_OK)
+                return Err::e(std::string("placement engine: ") + jsp_last_error());
+            if (bad == 0) {
+                *valid = true;
+                return Err::none();
+            }
+        }
+        // the reference's walk, for its first error (leader value from the snapshot)
+        const std::string lt = domainValue(c, level, c.planner->row_domain((uint32_t)row, (int)level));
+        for (const auto& pod : podList.elems()) {
+            if (IsLeaderPod(pod)) continue;
+            std::string ft;
+            if (Err e = followerPodTopology(pod, key, &ft); !e.ok) return e;
+            if (ft != lt) return Err::e("follower topology " + go_quote(ft) + " != leader topology " + go_quote(lt));
+        }
+        *valid = true;
+        return Err::none();
+    }
     std::string lt;
     if (Err e = topologyFromPod(c, leader, key, &lt); !e.ok) return e;
     for (const auto& pod : podList.elems()) {
@@ -623,6 +762,144 @@ Err Reconcile(Cache& c, const std::string& ns, const std::string& name, const st
     return Err::none();
 }
 
+// ============================================================ engine placement (A10, §8f rows 1 and 4)
+// Plan child Jobs through the engine: one requirement class per
+// (replicatedJob, exclusive-topology key), runs in the jobs' order (the order
+// constructJobsFromTemplate produces them: globalJobIndex), the snapshot
+// re-synced from this cache's Node / Pod objects first. Jobs without the
+// exclusive annotation, or with the node-selector strategy, are not placed by
+// the engine (the reference's webhooks skip them too, pod_mutating_webhook.go:72-76).
+Json classesJson(const Planner& pl, const std::vector<ClassSpec>& classes) {
+    std::vector<jsp_job_class> jc;
+    pl.encode(classes, &jc);
+    Json out = Json::array();
+    for (size_t i = 0; i < classes.size(); ++i) {
+        const jsp_job_class& x = jc[i];
+        Json o = Json::object(), req = Json::array(), fb = Json::array(), res = Json::array();
+        for (int w = 0; w < JSP_MAX_LABEL_WORDS; ++w) {
+            char a[24], b[24];
+            std::snprintf(a, sizeof a, "%016llx", (unsigned long long)x.req_labels[w]);
+            std::snprintf(b, sizeof b, "%016llx", (unsigned long long)x.forbid_labels[w]);
+            req.push_back(std::string(a));
+            fb.push_back(std::string(b));
+        }
+        for (int r = 0; r < JSP_MAX_RES; ++r) res.push_back((int64_t)x.req_res[r]);
+        o["reqLabels"] = req;
+        o["forbidLabels"] = fb;
+        o["toleratedTaints"] = (int64_t)x.tolerated_taints;
+        o["level"] = (int64_t)x.level;
+        o["pods"] = (int64_t)x.pods;
+        o["reqRes"] = res;
+        out.push_back(o);
+    }
+    return out;
+}
+
+// The requirement classes of `jobs` and each placed job's class index.
+Err jobClasses(Planner& pl, const Json& jobs, std::vector<ClassSpec>* classes, std::vector<uint32_t>* job_class,
+               std::vector<std::string>* names, std::vector<std::string>* keys) {
+    std::map<std::string, uint32_t> class_of_rj;
+    for (const auto& job : jobs.elems()) {
+        const Json& ann = annotations(job);
+        if (!has_key(ann, kExclusiveKey) || has_key(ann, kNodeSelectorStrategyKey)) continue;
+        const std::string key = str_at(ann, kExclusiveKey);
+        const std::string ck = str_at(labels(job), kReplicatedJobNameKey) + "\n" + key;
+        auto it = class_of_rj.find(ck);
+        uint32_t ci = 0;
+        if (it == class_of_rj.end()) {
+            ClassSpec cs;
+            const Json& js = job.get("spec");
+            const int64_t par = js.has("parallelism") ? js.get("parallelism").as_int() : 1;
+            if (Err2 e = pl.class_of(js.get("template"), par, key, &cs); !e.ok()) return Err::e(e.msg);
+            ci = (uint32_t)classes->size();
+            classes->push_back(std::move(cs));
+            class_of_rj[ck] = ci;
+        } else {
+            ci = it->second;
+        }
+        job_class->push_back(ci);
+        names->push_back(name_of(job));
+        keys->push_back(key);
+    }
+    if (classes->size() > JSP_MAX_CLASSES) return Err::e("placement planner: more than 64 requirement classes");
+    return Err::none();
+}
+
+Err planJobs(Cache& c, const Json& jobs, Json* out) {
+    if (!c.planner) return Err::e("no placement planner bound to this cache");
+    Planner& pl = *c.planner;
+    std::vector<ClassSpec> classes;
+    std::vector<uint32_t> job_class;
+    std::vector<std::string> names, keys;
+    if (Err e = jobClasses(pl, jobs, &classes, &job_class, &names, &keys); !e.ok) return e;
+    Json stats;
+    if (Err2 e = pl.sync(c.nodes, c.pods, &stats); !e.ok()) return Err::e(e.msg);
+    std::vector<uint32_t> rc, rl;
+    for (uint32_t ci : job_class) {
+        if (rc.empty() || rc.back() != ci) {
+            rc.push_back(ci);
+            rl.push_back(0);
+        }
+        ++rl.back();
+    }
+    std::vector<int32_t> assign;
+    jsp_stats st{};
+    ++c.engine_calls;
+    if (Err2 e = pl.place(classes, rc, rl, &assign, &st); !e.ok()) return Err::e(e.msg);
+    Json r = Json::object(), js = Json::array(), un = Json::array();
+    for (size_t j = 0; j < names.size(); ++j) {
+        Json x = Json::object();
+        x["name"] = names[j];
+        x["topologyKey"] = keys[j];
+        x["domainId"] = (int64_t)assign[j];
+        if (assign[j] >= 0) {
+            x["domain"] = pl.domain_values(pl.level_of(keys[j]))[assign[j]];
+        } else {
+            x["domain"] = Json();
+            un.push_back(names[j]);
+        }
+        js.push_back(x);
+    }
+    r["jobs"] = js;
+    r["unplaceable"] = un;
+    r["placed"] = (int64_t)st.placed;
+    r["snapshot"] = stats;
+    r["classes"] = classesJson(pl, classes);
+    Json jcj = Json::array();
+    for (uint32_t ci : job_class) jcj.push_back((int64_t)ci);
+    r["jobClass"] = jcj;
+    *out = r;
+    return Err::none();
+}
+
+// The recreate path consulting the engine (A10): the reconcile step after
+// failurePolicyRecreateAll bumped status.restarts (failure_policy.go:155-175).
+// getChildJobs buckets the old attempt into `delete` (jobset_controller.go:
+// 281-290); while any is listed nothing is created (shouldCreateJob, :698-709,
+// and the Foreground deletion, :553-576). Once they are gone, every
+// replicatedJob's Jobs are constructed (constructJobsFromTemplate, :638-649,
+// unchanged) and placed by the engine on the post-delete snapshot. The plan is
+// reported beside the Jobs; the Jobs and the pods' mutations are not changed.
+Err reconcileRecreate(Cache& c, const Json& js, const Json& jobs, Json* out) {
+    Json owned;
+    if (Err e = getChildJobs(js, jobs, &owned); !e.ok) return e;
+    Json r = Json::object(), del = Json::array(), create = Json::array();
+    for (const auto& j : owned.get("delete").elems()) del.push_back(name_of(j));
+    if (owned.get("delete").size() == 0)
+        for (const auto& rj : js.get("spec").get("replicatedJobs").elems())
+            for (const auto& j : constructJobsFromTemplate(js, rj, owned).elems()) create.push_back(j);
+    r["delete"] = del;
+    r["create"] = create;
+    r["plan"] = Json();
+    if (create.size() > 0 && c.planner) {
+        Json plan;
+        if (Err e = planJobs(c, create, &plan); !e.ok) r["planError"] = e.msg;
+        else r["plan"] = plan;
+    }
+    *out = r;
+    return Err::none();
+}
+
 // ============================================================ node-selector strategy
 // generate_namespaced_jobs, hack/label_nodes/label_nodes.py:99-112
 Json generateNamespacedJobs(const Json& js) {
@@ -634,6 +911,56 @@ Json generateNamespacedJobs(const Json& js) {
             out.push_back(ns + "_" + name_of(js) + "-" + rj.get("name").as_string() + "-" + std::to_string(i));
     }
     return out;
+}
+
+// Deterministic replacement for label_nodes.py (hack/label_nodes/
+// label_nodes.py:36-120; its job -> node-pool map iterates a Python set,
+// :115-120): the JobSet's jobs (generate_namespaced_jobs order) are placed on
+// the exclusive-topology key's domains by the engine's lowest-index rule, and
+// every node of a job's domain gets the script's patch body (:65-80).
+Err labelNodes(Cache& c, const Json& js, Json* out) {
+    if (!c.planner) return Err::e("no placement planner bound to this cache");
+    Planner& pl = *c.planner;
+    const Json ns_jobs = generateNamespacedJobs(js);
+    std::vector<ClassSpec> classes;
+    std::vector<uint32_t> rc, rl;
+    std::string key;
+    for (const auto& rj : js.get("spec").get("replicatedJobs").elems()) {
+        std::string k = "cloud.google.com/gke-nodepool";  // label_nodes.py:33 NODE_POOL_KEY
+        if (has_key(annotations(js), kExclusiveKey)) k = str_at(annotations(js), kExclusiveKey);
+        const Json& rja = rj.get("template").get("metadata").get("annotations");
+        if (has_key(rja, kExclusiveKey)) k = str_at(rja, kExclusiveKey);
+        if (!key.empty() && k != key) return Err::e("label nodes: replicated jobs use different topology keys");
+        key = k;
+        const Json& jspec = rj.get("template").get("spec");
+        ClassSpec cs;
+        const int64_t par = jspec.has("parallelism") ? jspec.get("parallelism").as_int() : 1;
+        if (Err2 e = pl.class_of(jspec.get("template"), par, key, &cs); !e.ok()) return Err::e(e.msg);
+        rc.push_back((uint32_t)classes.size());
+        rl.push_back((uint32_t)(rj.has("replicas") ? rj.get("replicas").as_int() : 1));
+        classes.push_back(std::move(cs));
+    }
+    if (classes.size() > JSP_MAX_CLASSES) return Err::e("label nodes: more than 64 replicated jobs");
+    Json stats;
+    if (Err2 e = pl.sync(c.nodes, c.pods, &stats); !e.ok()) return Err::e(e.msg);
+    std::vector<int32_t> assign;
+    jsp_stats st{};
+    ++c.engine_calls;
+    if (Err2 e = pl.place(classes, rc, rl, &assign, &st); !e.ok()) return Err::e(e.msg);
+    std::vector<std::string> names;
+    for (const auto& n : ns_jobs.elems()) names.push_back(n.as_string());
+    const int level = pl.level_of(key);
+    Json mapping = Json::object(), un = Json::array();
+    for (size_t j = 0; j < names.size() && j < assign.size(); ++j) {
+        if (assign[j] >= 0) mapping[names[j]] = pl.domain_values(level)[assign[j]];
+        else un.push_back(names[j]);
+    }
+    Json r = Json::object();
+    r["mapping"] = mapping;
+    r["unplaceable"] = un;
+    r["patches"] = label_nodes(pl, level, names, assign);
+    *out = r;
+    return Err::none();
 }
 
 // ============================================================ registry of caches
@@ -749,12 +1076,62 @@ Json dispatch(const std::string& m, const Json& q) {
     }
     Cache& c = *cache_of(q);
     std::lock_guard<std::mutex> g(c.mu);
-    if (m == "cache.add") {
+    if (m == "cache.add") {  // watch Added / Modified
         const Json& o = q.get("object");
         if (q.get("kind").as_string() == "Node") c.nodes[name_of(o)] = o;
         else c.pods[ns_of(o) + "/" + name_of(o)] = o;
         return ok(true);
     }
+    if (m == "cache.remove") {  // watch Deleted
+        if (q.get("kind").as_string() == "Node") c.nodes.erase(q.get("name").as_string());
+        else c.pods.erase(q.get("namespace").as_string() + "/" + q.get("name").as_string());
+        return ok(true);
+    }
+    if (m == "planner.new") {
+        std::vector<std::string> lk, res;
+        for (const auto& k : q.get("levelKeys").elems()) lk.push_back(k.as_string());
+        for (const auto& r : q.get("resources").elems()) res.push_back(r.as_string());
+        c.eng = reinterpret_cast<jsp_engine*>((uintptr_t)q.get("engine").as_int());
+        c.planner = std::make_unique<Planner>(c.eng, lk, res);
+        return ok(true);
+    }
+    if (m == "planner.sync" || m == "planner.columns") {
+        if (!c.planner) return err_json(Err::e("no placement planner bound to this cache"));
+        Json stats;
+        if (Err2 e = c.planner->sync(c.nodes, c.pods, &stats); !e.ok()) return err_json(Err::e(e.msg));
+        return ok(m == "planner.sync" ? stats : c.planner->columns());
+    }
+    if (m == "planner.encode") {  // classes of `jobs` without placing (tests, oracle inputs)
+        if (!c.planner) return err_json(Err::e("no placement planner bound to this cache"));
+        std::vector<ClassSpec> classes;
+        std::vector<uint32_t> job_class;
+        std::vector<std::string> names, keys;
+        if (Err e = jobClasses(*c.planner, q.get("jobs"), &classes, &job_class, &names, &keys); !e.ok) return err_json(e);
+        Json stats;
+        if (Err2 e = c.planner->sync(c.nodes, c.pods, &stats); !e.ok()) return err_json(Err::e(e.msg));
+        Json r = Json::object();
+        r["classes"] = classesJson(*c.planner, classes);
+        Json jcj = Json::array();
+        for (uint32_t ci : job_class) jcj.push_back((int64_t)ci);
+        r["jobClass"] = jcj;
+        return ok(r);
+    }
+    if (m == "planner.plan") {
+        Json out;
+        Err e = planJobs(c, q.get("jobs"), &out);
+        return err_json(e, out);
+    }
+    if (m == "controllers.reconcileRecreate") {
+        Json out;
+        Err e = reconcileRecreate(c, q.get("jobSet"), q.get("jobs"), &out);
+        return err_json(e, out);
+    }
+    if (m == "hack.labelNodes") {
+        Json out;
+        Err e = labelNodes(c, q.get("jobSet"), &out);
+        return err_json(e, out);
+    }
+    if (m == "webhooks.DefaultBatch") return ok(DefaultBatch(c, q.get("pods")));
     if (m == "cache.inject") {
         if (q.get("error").is_null()) c.inject.erase(q.get("what").as_string());
         else c.inject[q.get("what").as_string()] = q.get("error").as_string();

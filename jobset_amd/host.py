@@ -189,3 +189,44 @@ class Cache:
 
     def Reconcile(self, ns: str, name: str, now: str = "2024-10-08T00:00:00Z") -> Optional[str]:
         return call("controllers.Reconcile", cache=self.id, namespace=ns, name=name, now=now)[1]
+
+    def remove_pod(self, ns: str, name: str):
+        call("cache.remove", cache=self.id, kind="Pod", namespace=ns, name=name)
+
+    def remove_node(self, name: str):
+        call("cache.remove", cache=self.id, kind="Node", name=name)
+
+    # placement planner (jobset_amd/csrc/host/placement.h): the engine's snapshot
+    # built from this cache's Node / Pod objects
+    def planner_new(self, engine, level_keys: List[str], resources: List[str]):
+        """engine=None: a host-only planner (ingestion without uploads)."""
+        call("planner.new", cache=self.id, engine=engine._h.value if engine is not None else 0,
+             levelKeys=level_keys, resources=resources)
+
+    def _ok(self, method: str, **req):
+        r, e = call(method, cache=self.id, **req)
+        if e is not None:
+            raise HostCallError(e)
+        return r
+
+    def planner_sync(self) -> dict:
+        return self._ok("planner.sync")
+
+    def planner_columns(self) -> dict:
+        return self._ok("planner.columns")
+
+    def planner_encode(self, jobs: List[dict]) -> dict:
+        return self._ok("planner.encode", jobs=jobs)
+
+    def plan(self, jobs: List[dict]):
+        return call("planner.plan", cache=self.id, jobs=jobs)
+
+    def reconcileRecreate(self, js: dict, jobs: List[dict]):
+        return call("controllers.reconcileRecreate", cache=self.id, jobSet=js, jobs=jobs)
+
+    def labelNodes(self, js: dict):
+        return call("hack.labelNodes", cache=self.id, jobSet=js)
+
+    def DefaultBatch(self, pods: List[dict]) -> List[Tuple[dict, Optional[str]]]:
+        r = call("webhooks.DefaultBatch", cache=self.id, pods=pods)[0]
+        return [(x["pod"], x["error"]) for x in r]
