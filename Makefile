@@ -42,8 +42,23 @@ tools/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip jobset_amd/csrc/jsp_en
 	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -x hip -c -o build/diag/e.o jobset_amd/csrc/jsp_engine.cc
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag/k.o build/diag/e.o $(HOST_OBJ)
 
+# ASan + UBSan build of the host mirror (webhook / reconciler / planner / JSON)
+# linked with the product engine objects, and of the C oracles; tests/
+# test_sanitizers.py runs the host and oracle suites against them under a
+# preloaded libasan. Host code only: GPU sanitizers are not used.
+SANFLAGS = -O1 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -fsanitize=address,undefined \
+	-fno-omit-frame-pointer -fno-sanitize-recover=undefined
+ASAN_OBJ = $(patsubst jobset_amd/csrc/host/%.cc,build/asan/host_%.o,$(HOST_SRC))
+sanitize: build/asan/libjsplace.so
+	$(MAKE) -s -C oracle sanitize
+build/asan/host_%.o: jobset_amd/csrc/host/%.cc $(HOST_HDR) $(HDR)
+	@mkdir -p build/asan
+	$(CXX) $(SANFLAGS) -c -o $@ $<
+build/asan/libjsplace.so: build/jsp_kernels.o build/jsp_engine.o $(ASAN_OBJ)
+	$(CXX) -shared -fsanitize=address,undefined -o $@ $^ -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean diag
+.PHONY: all oracle clean diag sanitize

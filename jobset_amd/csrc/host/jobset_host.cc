@@ -886,8 +886,10 @@ Err reconcileRecreate(Cache& c, const Json& js, const Json& jobs, Json* out) {
     Json r = Json::object(), del = Json::array(), create = Json::array();
     for (const auto& j : owned.get("delete").elems()) del.push_back(name_of(j));
     if (owned.get("delete").size() == 0)
-        for (const auto& rj : js.get("spec").get("replicatedJobs").elems())
-            for (const auto& j : constructJobsFromTemplate(js, rj, owned).elems()) create.push_back(j);
+        for (const auto& rj : js.get("spec").get("replicatedJobs").elems()) {
+            const Json made = constructJobsFromTemplate(js, rj, owned);  // outlives the loop below
+            for (const auto& j : made.elems()) create.push_back(j);
+        }
     r["delete"] = del;
     r["create"] = create;
     r["plan"] = Json();

@@ -26,7 +26,7 @@ from typing import Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libjsp_oracle.so")
+_LIB_PATH = os.environ.get("JSPO_LIB_PATH") or os.path.join(_HERE, "libjsp_oracle.so")
 _lib = None
 
 sys.path.insert(0, os.path.dirname(_HERE))
@@ -177,7 +177,7 @@ def assign_from_tallies(p: Problem, cap: np.ndarray, occ: np.ndarray) -> np.ndar
 
 
 # ------------------------------------------------------------------ optimized threaded CPU evaluator
-_FAST_PATH = os.path.join(_HERE, "libjsp_cpufast.so")
+_FAST_PATH = os.environ.get("JSPF_LIB_PATH") or os.path.join(_HERE, "libjsp_cpufast.so")
 _fast = None
 
 

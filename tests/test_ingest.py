@@ -171,3 +171,23 @@ def test_unsupported_selectors_are_errors():
         c.planner_encode([job("j", "rack", {"affinity": two_terms})])
     with pytest.raises(host.HostCallError, match="not one of the engine's topology keys"):
         c.planner_encode([job("j", "zone", {})])
+
+
+def test_reconcile_recreate_without_engine():
+    """controllers.reconcileRecreate's Job side (no planner bound): old attempt
+    listed -> delete only; gone -> the new attempt's Jobs, unchanged."""
+    js = {"metadata": {"name": "train", "namespace": "default", "annotations": {
+        "alpha.jobset.sigs.k8s.io/exclusive-topology": "rack"}},
+        "spec": {"network": {}, "replicatedJobs": [
+            {"name": "a", "replicas": 2, "template": {"spec": {"parallelism": 2, "template": {"spec": {}}}}},
+            {"name": "b", "replicas": 1, "template": {"spec": {"parallelism": 1, "template": {"spec": {}}}}}]},
+        "status": {"restarts": 0}}
+    c = host.Cache()
+    jobs = sum((host.constructJobsFromTemplate(js, rj, {}) for rj in js["spec"]["replicatedJobs"]), [])
+    js1 = host.failurePolicyRecreateAll(js, True)
+    out, err = c.reconcileRecreate(js1, jobs)
+    assert err is None and out["delete"] == ["train-a-0", "train-a-1", "train-b-0"] and out["create"] == []
+    out, err = c.reconcileRecreate(js1, [])
+    want = sum((host.constructJobsFromTemplate(js1, rj, {}) for rj in js1["spec"]["replicatedJobs"]), [])
+    assert err is None and out["delete"] == [] and out["create"] == want and out["plan"] is None
+    assert [j["metadata"]["labels"]["jobset.sigs.k8s.io/restart-attempt"] for j in want] == ["1", "1", "1"]
