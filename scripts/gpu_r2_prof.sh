@@ -1,0 +1,15 @@
+# Round-2 profile set: rocprofv3 kernel trace of the bench command, then one
+# PMC pass per counter group (FETCH_SIZE, WRITE_SIZE, SQ) on configs 2, 4, 5.
+# Every GPU step is time-limited; the script stops at the first failure.
+set -u
+cd "$GRAFT_REPO_ROOT"; R="$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+OUT="$R/gpurun_out/${PROF_TAG:-r02}"; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/bench_trace" -o run --output-format csv -- python3 "$R/bench.py" --trials 100 --cpu-seconds 0 > "$OUT/bench_trace.log" 2>&1 || exit $?
+for cfg in 2 4 5; do
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20 > "$OUT/pmc_fetch$cfg.log" 2>&1 || exit $?
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20 > "$OUT/pmc_write$cfg.log" 2>&1 || exit $?
+timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/pmc_sq$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20 > "$OUT/pmc_sq$cfg.log" 2>&1 || exit $?
+done
+python3 "$R/tools/summarize_prof.py" "$OUT" > "$OUT/summary.txt" 2>&1
+echo prof-done
