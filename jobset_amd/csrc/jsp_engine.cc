@@ -415,8 +415,13 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
     f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
     f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
+    {
+        uint32_t lv[jsp::kMaxClasses];
+        for (uint32_t c = 0; c < e->C; ++c) lv[c] = e->cls_h[c].level;
+        f.fscr_words = jsp::fused_scratch_words(e->K, e->topo.D, lv, e->C);
+    }
     f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
-                                       f.topo_in_lds ? topo_words : 0u);
+                                       f.topo_in_lds ? topo_words : 0u, f.fscr_words);
     f.done = signal ? e->h_done.as<uint32_t>() : nullptr;
     f.epoch = e->epoch;
     if (n_signals && signal) *n_signals = 1;

@@ -99,6 +99,7 @@ struct FusedArgs {
     size_t lds_bytes;
     uint32_t topo_in_lds;        // hierarchy tables staged in LDS for the tail
     uint32_t topo_lds_words;     // their size (0 when not staged)
+    uint32_t fscr_words;         // LDS scratch (u64) for upper-level domain sums + occupancy bits, 0 = none
     uint32_t* done;              // host-mapped completion word (host path) or null
     uint32_t epoch;              // value written to *done when the tail has finished
 };
@@ -125,6 +126,7 @@ constexpr uint32_t kFusedStage = 2048;     // ranks the fused tail stages per lo
 constexpr uint32_t kMinStage = 4096;       // assign_kernel stages the bitmaps in LDS only if this much stage remains
 constexpr uint32_t kMaxStage = 32768;
 constexpr uint32_t kFusedTopoMax = 8192;   // hierarchy-table words the fused tail stages in LDS (32 KiB)
+constexpr uint32_t kFusedScrMax = 4096;    // upper-level feasibility scratch of the fused tail (u64 words, 32 KiB)
 constexpr size_t kLdsBytes = 160 * 1024;   // gfx950 LDS per workgroup
 // window of a long-run step: NT u64 words + NT u32 ranks, in u64 units
 constexpr uint32_t kAssignWinWords64 = kAssignThreads + kAssignThreads / 2;
@@ -156,7 +158,12 @@ hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
-                       uint32_t topo_words);
+                       uint32_t topo_words, uint32_t fscr_words);
+// u64 words of the fused tail's upper-level feasibility scratch: one sum per
+// domain of every class above the leaves, one occupancy bit per domain of
+// every level above the leaves; 0 when there is no such class or it exceeds
+// kFusedScrMax (the tail then builds those words one wave per word).
+uint32_t fused_scratch_words(uint32_t K, const uint32_t* D, const uint32_t* class_level, uint32_t C);
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s);

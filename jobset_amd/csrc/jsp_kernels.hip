@@ -258,7 +258,7 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 }
 
 template <int W, int R>
-__device__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
+__device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
     DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
@@ -453,7 +453,7 @@ __device__ __forceinline__ uint64_t wave_incl_scan64(uint64_t x) {
 // previous lane's P(hi). One pass, no per-domain serial loops, so a zone of
 // thousands of racks costs ~(leaves / 512) memory round trips, not one per leaf.
 constexpr int kUpperBatch = 8;
-__device__ uint64_t feas_word_upper(const uint32_t* __restrict__ cap, const uint32_t* __restrict__ occ, uint32_t ld,
+__device__ __forceinline__ uint64_t feas_word_upper(const uint32_t* __restrict__ cap, const uint32_t* __restrict__ occ, uint32_t ld,
                                     uint32_t lvl, uint32_t pods, uint32_t c, uint32_t w, const TopoDev& topo,
                                     int lane) {
     const uint32_t D = topo.D[lvl];
@@ -934,7 +934,7 @@ __device__ void reg_flush(RegState& s, uint32_t K, const TopoDev& topo, uint64_t
 // (domains below the cursor are taken or infeasible: the cursor only grows).
 // Wave 0 walks every run; the other waves only join the long ones.
 template <int NT, bool TOPO_LDS>
-__device__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, const TopoDev& topo,
+__device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, uint32_t C, const TopoDev& topo,
                              const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
                              uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
@@ -1281,6 +1281,133 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
     }
 }
 
+// ---- fused tail: leaf pass of the feasibility build (see place_fused_kernel)
+struct TailFeasArgs {
+    const uint32_t* cap;
+    const uint32_t* occ;
+    uint32_t ld, L;
+    uint64_t pass_cls, leaf_cls;
+    uint32_t npc;
+    bool scr;
+    uint32_t K;
+    uint32_t ooff0, ooff1, ooff2;  // occupancy-bit word offset of upper levels 0..2 (no arrays: they
+                                   // would be indexed at run time and live in scratch)
+    uint64_t* s_uocc;
+    uint64_t* s_usum;
+    uint64_t* s_feas;
+    uint32_t c_pods, c_beg, c_lvl, c_uoff;  // lane c: class c's fields
+    const uint32_t* s_topo;  // hierarchy tables in LDS, or null
+    const uint32_t* s_poff;  // parent-table offsets in s_topo per level
+    const int32_t *par1, *par2, *par3;  // the same tables in global memory (levels 1..3)
+};
+static_assert(kMaxLevels == 4, "TailFeasArgs spells out the levels");
+
+__device__ __forceinline__ uint32_t tail_ooff(const TailFeasArgs& t, uint32_t k) {
+    const uint32_t o0 = t.ooff0, o1 = t.ooff1, o2 = t.ooff2;  // values: a conditional of lvalues would select
+    return k == 0 ? o0 : k == 1 ? o1 : o2;                    // field addresses and keep t in scratch
+}
+
+// ancestor at level lvl of leaf l (hierarchy tables from LDS when staged)
+__device__ __forceinline__ uint32_t tail_up_dom(const TailFeasArgs& t, uint32_t l, uint32_t lvl) {
+    const int32_t *p1 = t.par1, *p2 = t.par2, *p3 = t.par3;  // values, as in tail_ooff
+    for (uint32_t k = t.K - 1; k > lvl; --k)
+        l = t.s_topo ? t.s_topo[t.s_poff[k] + l] : (uint32_t)(k == 1 ? p1 : k == 2 ? p2 : p3)[l];
+    return l;
+}
+
+// Every thread takes 4-leaf chunks, loads occupancy once and the capacities of
+// the NG classes of the pass, then ORs each leaf-level class's 4 feasibility
+// bits into its LDS word and adds each upper class's clamped capacities into
+// its domain sums (and flags occupied leaves' domains).
+template <int NG>
+__device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
+    const uint32_t L = t.L, npc = t.npc;
+    // the pass's classes and their capacity rows, wave-uniform (SGPRs): each
+    // load below is one instruction on a scalar base and a shared lane offset
+    uint32_t cid[NG];
+    const uint32_t* crow[NG];
+    {
+        uint64_t m = t.pass_cls;
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+            const uint32_t c = (uint32_t)__builtin_ctzll(m);  // past npc: the last class again
+            if ((uint32_t)u + 1 < npc) m &= m - 1ull;
+            cid[u] = to_sgpr(c);
+            crow[u] = t.cap + (size_t)cid[u] * t.ld;
+        }
+    }
+    JSP_STAMP(4008u, 3);
+    for (uint32_t q = threadIdx.x; q * 4u < L; q += kTallyThreads) {
+        const uint32_t l0 = q * 4u;
+        // every load at a clamped index (classes past npc repeat the last one,
+        // leaves past L the last leaf) and masked afterwards: straight-line
+        // code, so all of them are in flight before the first wait
+        uint32_t ix[4], ov[4], cv[NG][4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ix[i] = l0 + i < L ? l0 + i : L - 1;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ov[i] = t.occ[ix[i]];
+#pragma unroll
+        for (int u = 0; u < NG; ++u)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) cv[u][i] = crow[u][ix[i]];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = l0 + i < L;
+            ov[i] = in ? ov[i] : 1u;
+#pragma unroll
+            for (int u = 0; u < NG; ++u) cv[u][i] = in ? cv[u][i] : 0u;
+        }
+#ifdef JSP_STAMPS
+        JSP_STAMP(4008u, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        JSP_STAMP(4008u, 1);
+#endif
+        if (t.scr) {  // occupied leaves flag their domain at every level above the leaves
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                if (l0 + i >= L || ov[i] == 0u) continue;
+                for (uint32_t k = 0; k + 1 < t.K; ++k) {
+                    const uint32_t d = tail_up_dom(t, l0 + i, k);
+                    atomicOr(reinterpret_cast<unsigned long long*>(&t.s_uocc[tail_ooff(t, k) + (d >> 6)]),
+                             (unsigned long long)(1ull << (d & 63u)));
+                }
+            }
+        }
+        JSP_STAMP(4008u, 2);
+#pragma unroll
+        for (int u = 0; u < NG; ++u) {
+            if ((uint32_t)u >= npc) continue;
+            const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)t.c_pods, (int)cid[u]);
+            if ((t.leaf_cls >> cid[u]) & 1ull) {
+                const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)t.c_beg, (int)cid[u]);
+                uint64_t bits = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) bits |= (cv[u][i] >= pods && ov[i] == 0u) ? (1ull << i) : 0ull;
+                if (bits) atomicOr(reinterpret_cast<unsigned long long*>(&t.s_feas[wo + (l0 >> 6)]),
+                                   (unsigned long long)(bits << (l0 & 63u)));
+            } else {
+                const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)t.c_lvl, (int)cid[u]);
+                uint64_t* sum = t.s_usum + (uint32_t)__builtin_amdgcn_readlane((int)t.c_uoff, (int)cid[u]);
+                uint32_t dcur = tail_up_dom(t, l0, lvl);
+                uint64_t acc = 0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if (l0 + i >= L) break;
+                    const uint32_t d = i == 0 ? dcur : tail_up_dom(t, l0 + i, lvl);
+                    if (d != dcur) {
+                        if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(&sum[dcur]), (unsigned long long)acc);
+                        acc = 0;
+                        dcur = d;
+                    }
+                    acc += cv[u][i] < pods ? cv[u][i] : pods;
+                }
+                if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(&sum[dcur]), (unsigned long long)acc);
+            }
+        }
+    }
+}
+
 // ----------------------------------------------------------------- fused small-snapshot placement
 // Tally workgroups publish their leaf sums (plain stores, every wave drains
 // vmcnt, workgroup barrier, one lane: agent release fence, drain, relaxed agent
@@ -1301,6 +1428,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     __syncthreads();
     const uint32_t tile = *s_flag;
     if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
+    JSP_STAMP(tile, 0);
     tally_block<W, R>(a, tile, lds);
 
     // publish
@@ -1314,6 +1442,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
         *s_flag = (old + 1 - f.done_base) == a.n_blocks ? 1u : 0u;
     }
     __syncthreads();
+    JSP_STAMP(tile, 5);
     if (*s_flag == 0) return;
     JSP_STAMP(4000u, 1);
     // the tail: small tables first (independent of the other workgroups' sums)
@@ -1341,50 +1470,72 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint32_t Kt = f.topo.K;
     // per-class fields in registers (lane c = class c)
-    const uint32_t c_beg = (uint32_t)lane < f.C ? m.s_woff[lane] : 0u;
-    const uint32_t c_end = (uint32_t)lane < f.C ? m.s_woff[lane + 1] : 0u;
-    const uint32_t c_lvl = (uint32_t)lane < f.C ? m.s_lvl[lane] : 0xFFFFu;
-    const uint32_t c_pods = (uint32_t)lane < f.C ? m.s_pods[lane] : 0u;
-    const uint64_t leaf_cls = __ballot((uint32_t)lane < f.C && c_lvl + 1 == Kt);
-    const uint64_t upper_cls = __ballot((uint32_t)lane < f.C && c_lvl + 1 < Kt);
-    // leaf-level classes: every thread takes 4-leaf chunks, loads occupancy once and
-    // every class's capacities (8 classes per pass, all loads first), then ORs each
-    // class's 4 feasibility bits into its LDS word
+    const bool c_in = (uint32_t)lane < f.C;
+    const uint32_t c_beg = c_in ? m.s_woff[lane] : 0u;
+    const uint32_t c_end = c_in ? m.s_woff[lane + 1] : 0u;
+    const uint32_t c_lvl = c_in ? m.s_lvl[lane] : 0u;
+    const uint32_t c_pods = c_in ? m.s_pods[lane] : 0u;
+    const uint64_t leaf_cls = __ballot(c_in && c_lvl + 1 == Kt);
+    const uint64_t upper_cls = __ballot(c_in && c_lvl + 1 < Kt);
+    // Upper-level classes with the scratch: every leaf's capacity (clamped to
+    // pods, which keeps capsum >= pods exact) is added into its domain's 64-bit
+    // LDS sum and its occupancy into the domain's bit, in the same pass over
+    // the leaves as the leaf-level classes; the words follow from the sums.
+    // Scratch: [sums of each upper class's domains][occupancy bits per upper level].
+    const bool scr = f.fscr_words != 0 && upper_cls != 0ull;
+    uint64_t* s_usum = reinterpret_cast<uint64_t*>(
+        (reinterpret_cast<uintptr_t>(s_stage + kFusedStage) + 7) & ~static_cast<uintptr_t>(7));
+    const uint32_t usz = scr && ((upper_cls >> lane) & 1ull) ? f.topo.D[c_lvl] : 0u;
+    const uint32_t uincl = wave_incl_scan(usz, lane);
+    const uint32_t c_uoff = uincl - usz;  // lane c: first sum of class c
+    uint64_t* s_uocc = s_usum + (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
+    const uint32_t ooff0 = 0, ooff1 = (f.topo.D[0] + 63) >> 6, ooff2 = ooff1 + ((f.topo.D[1] + 63) >> 6);
+    if (scr) {
+        for (uint32_t i = threadIdx.x; i < f.fscr_words; i += kTallyThreads) s_usum[i] = 0;
+        __syncthreads();
+    }
+    // every thread takes 4-leaf chunks, loads occupancy once and the capacities
+    // of every class in the pass (8 classes per group, all loads first), then
+    // ORs each leaf-level class's 4 feasibility bits into its LDS word and adds
+    // each upper class's clamped capacities into its domain sums
     {
         const uint32_t L = f.topo.D[Kt - 1];
-        const uint32_t nlc = (uint32_t)__popcll(leaf_cls);
-        for (uint32_t q = threadIdx.x; q * 4u < L; q += kTallyThreads) {
-            const uint32_t l0 = q * 4u;
-            uint32_t ov[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) ov[i] = l0 + i < L ? a.occ_out[l0 + i] : 1u;
-            for (uint32_t j0 = 0; j0 < nlc; j0 += 8) {
-                uint32_t cid[8], cv[8][4];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t j = j0 + (uint32_t)u;
-                    cid[u] = j < nlc ? select_bit(leaf_cls, j) : 0u;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i)
-                        cv[u][i] = (j < nlc && l0 + i < L) ? a.cap_out[(size_t)cid[u] * a.ld + l0 + i] : 0u;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    if (j0 + (uint32_t)u >= nlc) break;
-                    const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)c_pods, (int)cid[u]);
-                    const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)c_beg, (int)cid[u]);
-                    uint64_t bits = 0;
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) bits |= (cv[u][i] >= pods && ov[i] == 0u) ? (1ull << i) : 0ull;
-                    if (bits) atomicOr(reinterpret_cast<unsigned long long*>(&s_feas[wo + (l0 >> 6)]),
-                                       (unsigned long long)(bits << (l0 & 63u)));
-                }
-            }
-        }
+        const uint64_t pass_cls = leaf_cls | (scr ? upper_cls : 0ull);
+        const uint32_t npc = (uint32_t)__popcll(pass_cls);
+        static_assert(kTallyClasses <= 16, "the fused tail's leaf pass takes at most 16 classes");
+        const TailFeasArgs t{a.cap_out, a.occ_out, a.ld, L, pass_cls, leaf_cls, npc, scr, Kt, ooff0, ooff1, ooff2,
+                             s_uocc, s_usum, s_feas, c_pods, c_beg, c_lvl, c_uoff,
+                             f.topo_in_lds ? s_topo : nullptr, m.s_poff, f.topo.par[1], f.topo.par[2], f.topo.par[3]};
+        if (npc > 8) tail_leaf_pass<16>(t);
+        else if (npc > 0) tail_leaf_pass<8>(t);
     }
-    // classes above the leaves: one wave per word (prefix sums over the word's
-    // leaf range, feas_word_upper), words dealt to the waves in turn
-    {
+    JSP_STAMP(4000u, 4);
+    if (scr) {
+        __syncthreads();
+        // upper classes' words from the sums: one wave per word, words dealt to the waves in turn
+        uint64_t uc = upper_cls;
+        uint32_t base = 0;
+        while (uc != 0ull) {
+            const uint32_t c = (uint32_t)__builtin_ctzll(uc);
+            uc &= uc - 1ull;
+            const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)c_beg, (int)c);
+            const uint32_t we = (uint32_t)__builtin_amdgcn_readlane((int)c_end, (int)c);
+            const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)c_lvl, (int)c);
+            const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)c_pods, (int)c);
+            const uint64_t* sum = s_usum + (uint32_t)__builtin_amdgcn_readlane((int)c_uoff, (int)c);
+            const uint32_t D = f.topo.D[lvl];
+            for (uint32_t gw = wb + (wid + kTallyWaves - base % kTallyWaves) % kTallyWaves; gw < we;
+                 gw += kTallyWaves) {
+                const uint32_t d = (gw - wb) * 64u + (uint32_t)lane;
+                const bool ok = d < D && sum[d] >= pods && ((s_uocc[(lvl == 0 ? ooff0 : lvl == 1 ? ooff1 : ooff2) + (d >> 6)] >> (d & 63u)) & 1ull) == 0ull;
+                const uint64_t word = __ballot(ok);
+                if (lane == 0) s_feas[gw] = word;
+            }
+            base += we - wb;
+        }
+    } else {
+        // classes above the leaves: one wave per word (prefix sums over the word's
+        // leaf range, feas_word_upper), words dealt to the waves in turn
         uint64_t uc = upper_cls;
         uint32_t base = 0;
         while (uc != 0ull) {
@@ -1638,11 +1789,22 @@ size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_wor
 
 
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
-                       uint32_t topo_words) {
+                       uint32_t topo_words, uint32_t fscr_words) {
     const size_t tail = (size_t)(t_words + kFusedWinWords64 + feas_words) * 8 +
-                        sizeof(uint32_t) * (assign_small_words(kTallyThreads) + topo_words + kFusedStage);
+                        sizeof(uint32_t) * (assign_small_words(kTallyThreads) + topo_words + kFusedStage) +
+                        (fscr_words ? (size_t)fscr_words * 8 + 8 : 0);
     const size_t head = sizeof(uint32_t) * (tally_lds_words((int)nc, (int)nv, (int)la) + 4);
     return ((tail > head ? tail : head) + 15) & ~size_t(15);
+}
+
+uint32_t fused_scratch_words(uint32_t K, const uint32_t* D, const uint32_t* class_level, uint32_t C) {
+    if (K < 2) return 0;
+    uint64_t w = 0;
+    for (uint32_t c = 0; c < C; ++c)
+        if (class_level[c] + 1 < K) w += D[class_level[c]];
+    if (w == 0) return 0;
+    for (uint32_t k = 0; k + 1 < K; ++k) w += (D[k] + 63) / 64;
+    return w <= kFusedScrMax ? (uint32_t)w : 0u;
 }
 
 AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_words) {

@@ -42,9 +42,10 @@ def main():
         torch.cuda.synchronize()
         lib.jsp_debug_stamps(buf.ctypes.data, buf.shape[0])
         st = buf.reshape(4096, 8).astype(np.int64)
-        nz = st[st != 0]
+        rt = st[:4090]  # real-time stamps (row 4090 mixes in shader-clock values)
+        nz = rt[rt != 0]
         t0 = nz.min() if nz.size else 0
-        sel = st[4000:4050]
+        sel = np.concatenate([st[4000:4050], st[0:64]])  # walk rows, then tally tiles 0..63
         rows.append(np.where(sel != 0, (sel - t0) * 10, -1))
         r = st[4090]
         if r[0] and r[2]:
@@ -55,6 +56,10 @@ def main():
     for r in range(50):
         if (med[r] >= 0).any():
             print(f"  row {4000 + r}: " + "  ".join(f"{x:8.0f}" for x in med[r]))
+    print("  tally tiles (0 entry, 1 staged, 6 row pass, 7 leaf pass, 5 published):")
+    for r in range(50, 114):
+        if (med[r] >= 0).any():
+            print(f"  tile {r - 50:4d}: " + "  ".join(f"{med[r][i]:8.0f}" for i in (0, 1, 6, 7, 5)))
 
 
 if __name__ == "__main__":
