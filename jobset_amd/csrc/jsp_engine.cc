@@ -419,6 +419,12 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
         uint32_t lv[jsp::kMaxClasses];
         for (uint32_t c = 0; c < e->C; ++c) lv[c] = e->cls_h[c].level;
         f.fscr_words = jsp::fused_scratch_words(e->K, e->topo.D, lv, e->C);
+        bool upper = false;
+        for (uint32_t c = 0; c < e->C; ++c) upper |= lv[c] + 1 < e->K;
+        // write-through hand-off of the tallies to the tail (no release/acquire
+        // fences) unless the tail's per-wave upper-class path, which reads them
+        // with plain loads, will run
+        a.sc1_out = (!upper || f.fscr_words != 0) && !std::getenv("JSP_FENCED_HANDOFF") ? 1 : 0;
     }
     f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
                                        f.topo_in_lds ? topo_words : 0u, f.fscr_words);

@@ -70,6 +70,7 @@ struct TallyArgs {
     uint32_t* occ_out;
     uint32_t ld, leaf_base;
     int W, R;
+    int sc1_out;                // write cap/occ write-through (sc1): the fused kernel's hand-off to its tail
 };
 
 // Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks

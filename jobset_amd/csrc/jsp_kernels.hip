@@ -144,6 +144,17 @@ __device__ __forceinline__ void store_out(T* p, T v, bool sys) {
     else *p = v;
 }
 
+// Store of bytes another workgroup of the same launch reads: write-through
+// (agent-scope relaxed = `sc1`) when `sc1`, so the writer needs no release fence
+// and a reader using `sc1` loads no acquire (cdna_hip_programming.md G16).
+__device__ __forceinline__ void store_handoff(uint32_t* p, uint32_t v, int sc1) {
+    if (sc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+__device__ __forceinline__ uint32_t load_handoff(const uint32_t* p) {
+    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // last leaf index l in [0, n) with ls[l] <= row (ls ascending, n+1 entries)
 __device__ __forceinline__ uint32_t leaf_search(const uint32_t* ls, uint32_t n, uint32_t row) {
     uint32_t lo = 0, hi = n;  // invariant: ls[lo] <= row, answer < hi
@@ -390,8 +401,8 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     if (a.cap_out == nullptr) return;  // the caller keeps the sums in LDS (compaction without tally output)
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
         const uint32_t leaf = a.leaf_base + l0 + li;
-        for (int c = 0; c < nc; ++c) a.cap_out[(size_t)(a.c0 + c) * a.ld + leaf] = s_acc[c * la + li];
-        if (a.do_occ) a.occ_out[leaf] = s_acc[nc * la + li];
+        for (int c = 0; c < nc; ++c) store_handoff(a.cap_out + (size_t)(a.c0 + c) * a.ld + leaf, s_acc[c * la + li], a.sc1_out);
+        if (a.do_occ) store_handoff(a.occ_out + leaf, s_acc[nc * la + li], a.sc1_out);
     }
 }
 
@@ -1051,65 +1062,67 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 const uint32_t curc = (uint32_t)lane < C && ((cmask >> lane) & 1ull) ? my_cur : D;
                 const uint32_t d0 = wave_min_u32(curc);
                 const uint32_t tl = m.s_toff[lvl], nwl = (D + 63) >> 6;
-                uint64_t unassigned = __ballot(job);
+                uint64_t R = __ballot(job);  // jobs of the batch without a domain yet
                 int32_t res = -1;
                 uint64_t tookv = 0;
+                const bool cl = (uint32_t)lane < C && ((cmask >> lane) & 1ull);
                 JSP_STAMP(sb, 1);
-                for (uint32_t w = d0 >> 6; w < nwl && unassigned != 0; ++w) {
+                // Domain words in order; in each, the jobs still without a domain take,
+                // in job order, the lowest free bit of their class's word (job order
+                // and domain order give the same matching inside one word, see above).
+                // The per-job step is a scalar chain -- two readlanes of the job's
+                // class word, and-not / lowest-bit / or on the word's taken mask, one
+                // select into the job's lane -- so its cost is a dozen instructions of one
+                // wave, whatever the classes' feasibility patterns.
+                for (uint32_t w = d0 >> 6; w < nwl && R != 0ull; ++w) {
                     const uint64_t tw =
                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rs.T >> 32), (int)(tl + w)) << 32) |
                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rs.T, (int)(tl + w));
-                    const bool mine = (unassigned >> lane) & 1ull;
-                    const uint64_t av = mine ? feas[woff + w] & ~tw : 0ull;
-                    const uint64_t any = wave_or64(av);
-                    if (any == 0ull) continue;
-                    // Per word: domains every unassigned job can take ("universal") go
-                    // to the unassigned jobs in job order; a domain only some can take
-                    // is settled on its own, in domain order: the universal domains
-                    // below it have gone to the first m jobs, so it goes to the first
-                    // job after those that can take it. Only these are sequential.
-                    const uint64_t univ = wave_and64(mine ? av : ~0ull);
-                    uint64_t nu = any & ~univ;
-                    uint64_t R = unassigned;  // not taken by a non-universal domain (yet)
-                    uint32_t rank = mbcnt64(R);
-                    uint64_t took = 0;
-                    while (nu != 0ull) {
-                        uint32_t vq[4], mq[4];
-                        uint64_t lq[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const uint64_t low = nu & (0ull - nu);
-                            nu ^= low;
-                            vq[u] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(low ? (uint32_t)__builtin_ctzll(low) : 0u));
-                            mq[u] = (uint32_t)__popcll(univ & (low - 1ull));
-                            lq[u] = low ? __ballot((av & low) != 0ull) : 0ull;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const uint64_t col = __ballot(rank >= mq[u]) & R & lq[u];
-                            const uint64_t win = col & (0ull - col);
-                            R ^= win;
-                            rank = mbcnt64(R);
-                            took |= win ? (1ull << vq[u]) : 0ull;
-                            if (((win >> lane) & 1ull) != 0ull) res = (int32_t)(w * 64 + vq[u]);
-                        }
+                    const uint64_t g = cl ? feas[my_woff + w] & ~tw : 0ull;  // lane c: class c's free feasible bits
+                    // job lane j: its class's word
+                    const uint32_t gl = (uint32_t)__shfl((int)(uint32_t)g, (int)cls);
+                    const uint32_t gh = (uint32_t)__shfl((int)(uint32_t)(g >> 32), (int)cls);
+                    const uint64_t gj = ((uint64_t)gh << 32) | gl;
+                    const uint64_t V0 = R & __ballot(job && gj != 0ull);  // jobs that can take something here
+                    if (V0 == 0ull) continue;
+                    // The chain runs on bits 0..62: s_ff1 of an empty word is -1, and the
+                    // s_bitset1 that follows then sets bit 63, which the chain never reads.
+                    // Bit 63 goes afterwards to the first visited job left without a domain
+                    // whose class has it (job order inside the word: it is the word's last
+                    // domain, so only jobs that found nothing below it can want it).
+                    const uint32_t gh62 = gh & 0x7FFFFFFFu;
+                    uint64_t V = V0, taken = 0;
+                    int32_t wres = -1;
+                    do {
+                        uint32_t j;  // next job: lowest bit of V, cleared
+                        asm("s_ff1_i32_b64 %[j], %[V]\n\t"
+                            "s_bitset0_b64 %[V], %[j]"
+                            : [V] "+s"(V), [j] "=&s"(j));
+                        const uint64_t gc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)j) << 32) |
+                                            (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)j);
+                        uint64_t t;
+                        int32_t bpos;
+                        // taken |= lowest bit of (gc & ~taken); the job's lane gets its
+                        // position (-1: none). SALU only, plus one writelane whose lane
+                        // select (m0) a SALU move wrote three instructions earlier.
+                        asm("s_mov_b32 m0, %[j]\n\t"
+                            "s_andn2_b64 %[t], %[g], %[tk]\n\t"
+                            "s_ff1_i32_b64 %[b], %[t]\n\t"
+                            "s_bitset1_b64 %[tk], %[b]\n\t"
+                            "v_writelane_b32 %[w], %[b], m0"
+                            : [tk] "+s"(taken), [w] "+v"(wres), [t] "=&s"(t), [b] "=&s"(bpos)
+                            : [g] "s"(gc), [j] "s"(j)
+                            : "m0", "scc");  // s_andn2 sets SCC
+                    } while (V != 0ull);
+                    taken &= ~(1ull << 63);
+                    const uint64_t m63 = __ballot(((V0 >> lane) & 1ull) && wres < 0 && (gh >> 31) != 0u);
+                    if (m63 != 0ull) {
+                        if ((uint32_t)lane == (uint32_t)__builtin_ctzll(m63)) wres = 63;
+                        taken |= 1ull << 63;
                     }
-                    // universal domains: the r-th job left in R takes the r-th of them
-                    const uint32_t nuniv = (uint32_t)__popcll(univ);
-                    const bool inr = (R >> lane) & 1ull;
-                    if (inr && rank < nuniv) res = (int32_t)(w * 64 + select_bit(univ, rank));
-                    const uint32_t nr_left = (uint32_t)__popcll(R);
-                    if (nr_left != 0u && univ != 0ull) {
-                        if (nr_left >= nuniv) {
-                            took |= univ;
-                        } else {  // the last job of R took the highest universal domain used
-                            const int32_t hi = __builtin_amdgcn_readlane(res, 63 - __builtin_clzll(R));
-                            const uint32_t pos = (uint32_t)hi & 63u;
-                            took |= univ & (pos == 63u ? ~0ull : ((2ull << pos) - 1ull));
-                        }
-                    }
-                    unassigned &= R & ~__ballot(inr && rank < nuniv);
-                    if ((uint32_t)lane == tl + w) tookv |= took;
+                    if (wres >= 0) res = (int32_t)(w * 64u + (uint32_t)wres);
+                    R &= ~__ballot(wres >= 0);
+                    if ((uint32_t)lane == tl + w) tookv |= taken;
                 }
                 JSP_STAMP(sb, 2);
                 if (job) assign[j0 + lane] = res;
@@ -1346,11 +1359,11 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) ix[i] = l0 + i < L ? l0 + i : L - 1;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = t.occ[ix[i]];
+        for (int i = 0; i < 4; ++i) ov[i] = load_handoff(t.occ + ix[i]);
 #pragma unroll
         for (int u = 0; u < NG; ++u)
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cv[u][i] = crow[u][ix[i]];
+            for (int i = 0; i < 4; ++i) cv[u][i] = load_handoff(crow[u] + ix[i]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const bool in = l0 + i < L;
@@ -1431,11 +1444,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     JSP_STAMP(tile, 0);
     tally_block<W, R>(a, tile, lds);
 
-    // publish
+    // publish. With sc1_out the sums went out write-through, so every storing
+    // wave's wait and the barrier order them before the ticket add (G16 R1: no
+    // release fence); otherwise the agent release writes this XCD's L2 back.
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        if (!a.sc1_out) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long old =
             __hip_atomic_fetch_add(f.ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1458,7 +1473,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     if (f.topo_in_lds) stage_topo<kTallyThreads>(s_topo, f.topo);
     for (uint32_t i = threadIdx.x; i < f.t_words; i += kTallyThreads) s_taken[i] = 0;
     for (uint32_t i = threadIdx.x; i < f.feas_words; i += kTallyThreads) s_feas[i] = 0;
-    if (threadIdx.x == 0) {
+    // With sc1_out every load of the other tiles' sums below is an sc1 load
+    // (load_handoff) issued after the ticket add returned and this barrier, so
+    // no acquire is needed; the per-wave upper-class path reads them with plain
+    // loads and keeps it (the host sets sc1_out only when that path cannot run).
+    if (threadIdx.x == 0 && !a.sc1_out) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
