@@ -32,7 +32,7 @@ oracle:
 	$(MAKE) -s -C oracle
 
 # diagnostic build with in-kernel phase stamps (tools/stamps.py); never the product library
-diag: tools/diag/libjsplace.so tools/diag/dispatch_probe
+diag: tools/diag/libjsplace.so tools/diag/dispatch_probe tools/diag/stream_ceiling
 tools/diag/dispatch_probe: tools/dispatch_probe.hip
 	@mkdir -p tools/diag
 	$(HIPCC) --offload-arch=gfx950 -O3 -o $@ $<
@@ -62,3 +62,8 @@ clean:
 	$(MAKE) -s -C oracle clean
 
 .PHONY: all oracle clean diag sanitize
+
+# achievable streaming ceiling (read-only and copy, cold and warm) at the placement kernels' byte counts
+tools/diag/stream_ceiling: tools/stream_ceiling.hip
+	@mkdir -p tools/diag
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<

@@ -40,7 +40,14 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
     do {                                                                                  \
         if (threadIdx.x == 0 && (blk) < 4096) jsp_dbg[(blk) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
     } while (0)
+#define JSP_DBGV(row, i, v)                                                               \
+    do {                                                                                  \
+        if (threadIdx.x == 0 && (row) < 4096) jsp_dbg[(row) * 8 + (i)] = (unsigned long long)(v); \
+    } while (0)
 #else
+#define JSP_DBGV(row, i, v) \
+    do {                    \
+    } while (0)
 #define JSP_CLK(blk, i) \
     do {                \
     } while (0)
@@ -969,6 +976,24 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
     RegState rs;
     rs.T = rs.P = 0;  // s_taken starts zeroed
     rs.pend = -1;
+    // Register mode: classes with no feasible domain at all ("dead") take
+    // nothing and block nothing, so their jobs (-1) join a batch of any level
+    // instead of cutting the level's job sequence into separate batches.
+    uint64_t dead = 0;
+    if (regmode) {
+        uint64_t* s_alive = reinterpret_cast<uint64_t*>(m.s_misc + 2);
+        if (tid == 0) *s_alive = 0;
+        __syncthreads();
+        const uint32_t nfw = m.s_woff[C];
+        for (uint32_t wi = tid; wi < nfw; wi += NT) {
+            if (feas[wi] == 0ull) continue;
+            uint32_t c = 0;
+            while (m.s_woff[c + 1] <= wi) ++c;  // C <= kMaxClasses
+            atomicOr(reinterpret_cast<unsigned long long*>(s_alive), (unsigned long long)(1ull << c));
+        }
+        __syncthreads();
+        dead = ~*s_alive & (C >= 64 ? ~0ull : ((1ull << C) - 1ull));
+    }
     for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
         // ---- a tile of runs: job offsets (block scan of run lengths) and the long-run list
         const uint32_t ri = r0 + tid;
@@ -1027,15 +1052,21 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     ++q;
                     continue;
                 }
-                const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
                 const uint32_t sb = 4010u + (nbatch < 39u ? nbatch : 39u);
                 (void)sb;
                 ++nbatch;
                 JSP_STAMP(sb, 0);
                 // ---- the batch: runs q .. q+nrb-1 (lane k = run q+k), all short, valid,
-                // at level lvl, ending within 64 jobs of o0
+                // at level lvl (the level of its first live run; dead runs fit any
+                // level), ending within 64 jobs of o0
                 const uint32_t lvl_v = (uint32_t)__shfl((int)my_lvl, (int)(rc_v < C ? rc_v : 0u));
-                const bool ok_v = in && rc_v < C && lvl_v == lvl && re_v - ro_v <= kWaveRunMax && re_v - o0 <= 64u;
+                const bool dead_v = rc_v < C && ((dead >> rc_v) & 1ull);
+                const uint64_t live_runs = __ballot(in && rc_v < C && !dead_v);
+                const uint32_t lvl = live_runs != 0ull
+                                         ? (uint32_t)__builtin_amdgcn_readlane((int)lvl_v, __builtin_ctzll(live_runs))
+                                         : (uint32_t)__builtin_amdgcn_readlane((int)my_lvl, (int)c);
+                const bool ok_v = in && rc_v < C && (lvl_v == lvl || dead_v) && re_v - ro_v <= kWaveRunMax &&
+                                  re_v - o0 <= 64u;
                 const uint64_t okm = __ballot(ok_v);
                 const uint32_t nrb = ~okm == 0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);  // >= 1: run q qualifies
                 uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)re_v, (int)nrb - 1) - o0;
@@ -1054,10 +1085,10 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 const uint32_t cls = job ? m.s_bcls[my_start] : 0u;
                 const uint32_t woff = (uint32_t)__shfl((int)my_woff, (int)cls);
                 q += nrb;
-                if (rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
-                // classes of the batch; the scan starts at their lowest cursor (every
-                // class's domains below its cursor are taken or infeasible)
-                const uint64_t cmask = wave_or64(job ? 1ull << cls : 0ull);
+                // live classes of the batch; the scan starts at their lowest cursor
+                // (every class's domains below its cursor are taken or infeasible)
+                const uint64_t cmask = wave_or64(job ? 1ull << cls : 0ull) & ~dead;
+                if (cmask != 0ull && rs.pend > (int)lvl) reg_flush<TOPO_LDS>(rs, K, topo, s_taken, t_words, s_topo, m, lane);
                 const uint32_t D = m.s_D[lvl];
                 const uint32_t curc = (uint32_t)lane < C && ((cmask >> lane) & 1ull) ? my_cur : D;
                 const uint32_t d0 = wave_min_u32(curc);
@@ -1091,18 +1122,33 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     // whose class has it (job order inside the word: it is the word's last
                     // domain, so only jobs that found nothing below it can want it).
                     const uint32_t gh62 = gh & 0x7FFFFFFFu;
+                    const uint32_t dbg_row = 4020u + (nbatch - 1u) * 4u + (w - (d0 >> 6));  // diag build only
+                    (void)dbg_row;
+                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) JSP_CLK(dbg_row, 0);
                     uint64_t V = V0, taken = 0;
                     int32_t wres = -1;
-                    do {
-                        uint32_t j;  // next job: lowest bit of V, cleared
+                    // software-pipelined: the next job's class word is read (two
+                    // readlanes) before the current job's scalar chain runs. Measured
+                    // ~100 shader cycles per job visit (tools/stamps_words.py): about
+                    // 7 per instruction of the 14-instruction loop on one wave; a
+                    // two-job unroll compiled to the same count per job.
+                    uint32_t j;  // current job: lowest bit of V, cleared
+                    asm("s_ff1_i32_b64 %[j], %[V]\n\t"
+                        "s_bitset0_b64 %[V], %[j]"
+                        : [V] "+s"(V), [j] "=&s"(j));
+                    uint64_t gc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)j) << 32) |
+                                  (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)j);
+                    while (true) {
+                        uint32_t jn;  // next job (-1: none; V stays 0)
                         asm("s_ff1_i32_b64 %[j], %[V]\n\t"
                             "s_bitset0_b64 %[V], %[j]"
-                            : [V] "+s"(V), [j] "=&s"(j));
-                        const uint64_t gc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)j) << 32) |
-                                            (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)j);
+                            : [V] "+s"(V), [j] "=&s"(jn));
+                        const uint64_t gn =
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)(jn & 63u)) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)(jn & 63u));
                         uint64_t t;
                         int32_t bpos;
-                        // taken |= lowest bit of (gc & ~taken); the job's lane gets its
+                        // taken |= lowest bit of (gc & ~taken); job j's lane gets its
                         // position (-1: none). SALU only, plus one writelane whose lane
                         // select (m0) a SALU move wrote three instructions earlier.
                         asm("s_mov_b32 m0, %[j]\n\t"
@@ -1113,7 +1159,14 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                             : [tk] "+s"(taken), [w] "+v"(wres), [t] "=&s"(t), [b] "=&s"(bpos)
                             : [g] "s"(gc), [j] "s"(j)
                             : "m0", "scc");  // s_andn2 sets SCC
-                    } while (V != 0ull);
+                        if ((int32_t)jn < 0) break;
+                        j = jn;
+                        gc = gn;
+                    }
+                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) {
+                        JSP_CLK(dbg_row, 1);
+                        JSP_DBGV(dbg_row, 3, __popcll(V0));
+                    }
                     taken &= ~(1ull << 63);
                     const uint64_t m63 = __ballot(((V0 >> lane) & 1ull) && wres < 0 && (gh >> 31) != 0u);
                     if (m63 != 0ull) {
@@ -1123,6 +1176,10 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     if (wres >= 0) res = (int32_t)(w * 64u + (uint32_t)wres);
                     R &= ~__ballot(wres >= 0);
                     if ((uint32_t)lane == tl + w) tookv |= taken;
+                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) {
+                        JSP_CLK(dbg_row, 2);
+                        JSP_DBGV(dbg_row, 4, __popcll(taken));
+                    }
                 }
                 JSP_STAMP(sb, 2);
                 if (job) assign[j0 + lane] = res;
