@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 2
+#define JSP_ABI_VERSION 3
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -120,7 +120,8 @@ typedef struct jsp_stats {
     uint32_t jobs;             /* J */
     uint32_t placed;           /* assign[j] != -1 */
     uint32_t runs;             /* replicated-job runs the assignment walked */
-    uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction */
+    uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction,
+                                  3 one-class compaction answered by the resident service */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
@@ -137,12 +138,31 @@ typedef struct jsp_timing {
     double host_launch_us;     /* the kernel launch call(s) */
     double host_wait_us;       /* launch return to completion seen (completion words or stream sync) */
     double host_post_us;       /* assign[] (and tallies) out, stats */
+    /* resident service (jsp_engine_set_service) */
+    uint64_t svc_calls;        /* jsp_place calls it answered */
+    uint64_t svc_starts;       /* service launches (first use, after uploads, idle exits, restarts) */
+    double svc_us;             /* summed in-kernel request time (first tile saw the request -> last tile
+                                  done, 100 MHz device clock); accumulated while timing is on */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */
 #define JSP_FUSED_OFF 0       /* always tally -> feas -> assign (three launches) */
 #define JSP_FUSED_AUTO 1      /* one launch when possible (default): the single-class compaction
                                  for one leaf-level class, the fused tail for small snapshots */
+
+/* jsp_engine_set_service modes. With AUTO, a host-API jsp_place of the
+ * one-class compaction shape (no tallies requested) is answered by a
+ * resident service kernel: one workgroup per tile stays on the GPU, polls a
+ * request word in pinned host memory, and writes assign[] back into pinned
+ * memory -- no launch per placement. It is started by the first such
+ * jsp_place, stopped by every upload, jsp_engine_set_service/set_fused and
+ * jsp_engine_destroy, and leaves by itself after JSP_SERVICE_IDLE_MS
+ * (default 50 ms) without a request; jsp_place restarts it when needed.
+ * While it runs, a device-wide synchronize (hipDeviceSynchronize,
+ * torch.cuda.synchronize) waits for it to leave: call
+ * jsp_engine_service_stop first. */
+#define JSP_SERVICE_OFF 0
+#define JSP_SERVICE_AUTO 1     /* default */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);
@@ -208,6 +228,9 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
 
 /* ---- instrumentation / tuning ---- */
 int jsp_engine_set_fused(jsp_engine* e, int mode);
+int jsp_engine_set_service(jsp_engine* e, int mode);
+/* Stops the resident service (if running) and waits for its workgroups to leave. */
+int jsp_engine_service_stop(jsp_engine* e);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

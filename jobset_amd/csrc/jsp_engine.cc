@@ -141,6 +141,22 @@ struct jsp_engine {
     bool have_last = false;
     hipEvent_t ev_switch = nullptr;
 
+    // resident placement service: the compaction shape kept on the GPU
+    // between host-API placements (place_service_kernel), fed by a host-mapped
+    // request word instead of a launch
+    struct Service {
+        bool running = false;
+        hipStream_t stream = nullptr;
+        HostBuf box;     // [0] request word: (J << 32) | seq
+        HostBuf words;   // done[nb] | stats[2] | err[1] | clk[2 nb]
+        HostBuf assign;  // [cap]
+        DevBuf granules;
+        uint32_t cap = 0, nb = 0, seq = 0, err_ack = 0;
+        bool clk = false;
+        std::chrono::steady_clock::time_point last{};
+    } svc;
+    int svc_mode = JSP_SERVICE_AUTO;
+
     // timing
     bool timing = false;
     std::vector<EvPair> ev;
@@ -155,6 +171,7 @@ struct jsp_engine {
         }
         if (ev_switch) (void)hipEventDestroy(ev_switch);
         if (stream) (void)hipStreamDestroy(stream);
+        if (svc.stream) (void)hipStreamDestroy(svc.stream);
     }
 };
 
@@ -439,6 +456,156 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     return JSP_OK;
 }
 
+// ---- resident placement service ----
+// Host side of place_service_kernel. The request word is written last with one
+// 64-bit store (x86 keeps store order; the kernel reads it with system-scope
+// vector loads). The host answers from the done words, as for a launch.
+// Idle exit: a workgroup leaves after JSP_SERVICE_IDLE_MS without a request;
+// the host restarts the service when its own last request is older than half
+// of that, so it never posts into an exit (and if it ever did, the dead
+// service is seen by a stream query and the request re-posted once).
+constexpr uint32_t kSvcMaxBlocks = 256;  // one tile per workgroup, all co-resident (<= one per CU)
+constexpr int kSvcGone = 1;
+
+double svc_idle_ms() {
+    static const double ms = [] {
+        const char* v = std::getenv("JSP_SERVICE_IDLE_MS");
+        const double x = v ? std::strtod(v, nullptr) : 50.0;
+        return x >= 1.0 && x <= 5000.0 ? x : 50.0;
+    }();
+    return ms;
+}
+
+bool svc_ok(jsp_engine* e) {
+    return e->svc_mode == JSP_SERVICE_AUTO && compact_ok(e) && e->n_blocks <= kSvcMaxBlocks;
+}
+
+int svc_stop(jsp_engine* e) {
+    auto& v = e->svc;
+    if (!v.running) return JSP_OK;
+    v.running = false;
+    __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
+    HIP_TRY(hipStreamSynchronize(v.stream));
+    return JSP_OK;
+}
+
+int svc_start(jsp_engine* e, uint32_t J) {
+    auto& v = e->svc;
+    if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+    const uint32_t nb = e->n_blocks;
+    if (J > v.cap || !v.assign.p) {
+        const uint32_t cap = std::max<uint32_t>(4096, J + J / 2);
+        HIP_TRY(v.assign.reserve((size_t)cap * 4));
+        v.cap = cap;
+    }
+    HIP_TRY(v.words.reserve((size_t)(3 * nb + 3) * 4));
+    std::memset(v.words.p, 0, (size_t)(3 * nb + 3) * 4);  // done words: seq 0 is never posted
+    HIP_TRY(v.box.reserve(64));
+    HIP_TRY(v.granules.reserve((size_t)8 * std::max<uint32_t>(nb, 1)));
+    // after everything the engine enqueued on any stream (the last stream's
+    // event), without making later calls wait for the service
+    if (e->have_last) {
+        if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
+        HIP_TRY(hipStreamWaitEvent(v.stream, e->ev_switch, 0));
+    }
+    HIP_TRY(hipMemsetAsync(v.granules.p, 0, (size_t)8 * std::max<uint32_t>(nb, 1), v.stream));
+    __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
+    uint32_t* w = v.words.as<uint32_t>();
+    jsp::ServiceArgs a{};
+    a.mailbox = v.box.as<unsigned long long>();
+    a.granules = v.granules.as<unsigned long long>();
+    a.pods = e->cls_h[0].pods;
+    a.seq0 = v.seq;
+    a.assign = v.assign.as<int32_t>();
+    a.done = w;
+    a.stats = w + nb;
+    a.err = w + nb + 2;
+    a.clk = e->timing ? w + nb + 3 : nullptr;
+    a.spin_limit = e->spin_limit;
+    a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
+    v.err_ack = 0;
+    v.nb = nb;
+    v.clk = e->timing;
+    HIP_TRY(jsp::launch_service(tally_args(e, nullptr, nullptr, e->L_total), a, v.stream));
+    v.running = true;
+    v.last = std::chrono::steady_clock::now();
+    e->acc.svc_starts += 1;
+    return JSP_OK;
+}
+
+// Waits for every tile's done word == seq. kSvcGone: the service left before
+// answering (its stream finished).
+int svc_wait(jsp_engine* e, uint32_t seq) {
+    auto& v = e->svc;
+    const uint32_t* words = v.words.as<uint32_t>();
+    uint32_t i = 0;
+    for (uint64_t spins = 1;; ++spins) {
+        while (i < v.nb && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) ++i;
+        if (i == v.nb) return JSP_OK;
+        if ((spins & 255) == 0) {
+            const hipError_t q = hipStreamQuery(v.stream);
+            if (q == hipSuccess) {
+                for (; i < v.nb; ++i)
+                    if (__atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq) return kSvcGone;
+                return JSP_OK;
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
+        }
+    }
+}
+
+// One placement through the service: J jobs of the engine's one class.
+int svc_place(jsp_engine* e, uint32_t J, int32_t* assign_out, uint32_t* placed) {
+    auto& v = e->svc;
+    const auto now = std::chrono::steady_clock::now();
+    bool restart = !v.running || J > v.cap || v.clk != e->timing || v.nb != e->n_blocks ||
+                   std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
+    uint32_t seq = 0;
+    for (int attempt = 0;; ++attempt) {
+        if (restart) {
+            if (int rc = svc_stop(e)) return rc;
+            if (int rc = svc_start(e, J)) return rc;
+        }
+        seq = v.seq + 1;
+        if (seq == 0 || seq == jsp::kSvcStop) seq = 1;
+        v.seq = seq;
+        v.last = std::chrono::steady_clock::now();
+        __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)J << 32) | seq, __ATOMIC_RELEASE);
+        const int rc = svc_wait(e, seq);
+        if (rc == kSvcGone && attempt == 0) {
+            v.running = false;
+            restart = true;
+            continue;
+        }
+        if (rc == kSvcGone) return set_err(JSP_EHIP, "placement service left before answering request %u", seq);
+        if (rc) return rc;
+        break;
+    }
+    const uint32_t* w = v.words.as<uint32_t>();
+    const uint32_t ew = __atomic_load_n(w + v.nb + 2, __ATOMIC_ACQUIRE);
+    if (ew != v.err_ack) {
+        v.err_ack = ew;
+        (void)svc_stop(e);
+        return set_err(JSP_EHIP, "placement service request %u failed: the compaction look-back timed out; "
+                                 "its assign[] is invalid", seq);
+    }
+    if (J > 0) std::memcpy(assign_out, v.assign.p, (size_t)J * 4);
+    *placed = __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
+    e->acc.svc_calls += 1;
+    if (v.clk && v.nb > 0) {
+        const uint32_t* clk = w + v.nb + 3;
+        const uint32_t ref = clk[0];
+        int32_t lo = 0, hi = 0;
+        for (uint32_t t = 0; t < v.nb; ++t) {
+            lo = std::min(lo, (int32_t)(clk[2 * t] - ref));
+            hi = std::max(hi, (int32_t)(clk[2 * t + 1] - ref));
+        }
+        e->acc.svc_us += (double)(hi - lo) / 100.0;
+    }
+    return JSP_OK;
+}
+
 // Host-side validation of a run list; returns the job count through *J.
 int check_runs(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint64_t* J) {
     uint64_t n = 0;
@@ -531,6 +698,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         return set_err(JSP_ENOMEM, "error word");
     }
     std::memset(e->h_err.p, 0, 64);
+    if (const char* v = std::getenv("JSP_SERVICE")) e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : JSP_SERVICE_AUTO;
     *out = e;
     return JSP_OK;
 }
@@ -540,6 +708,7 @@ void jsp_engine_destroy(jsp_engine* e) {
     {
         std::lock_guard<std::mutex> g(e->mu);
         (void)hipSetDevice(e->device);
+        (void)svc_stop(e);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
     }
     delete e;
@@ -548,6 +717,7 @@ void jsp_engine_destroy(jsp_engine* e) {
 int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
     if (!t) return set_err(JSP_EINVAL, "topology is NULL");
     // a failed upload leaves the engine without topology (buffers may be gone)
     e->have_topo = e->have_snap = e->have_cls = false;
@@ -620,6 +790,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
 int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (!nd || !nd->leaf_start) return set_err(JSP_EINVAL, "nodes / leaf_start is NULL");
     e->have_snap = false;  // until every column is resident again
@@ -746,6 +917,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
 int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (C > (uint32_t)jsp::kMaxClasses) return set_err(JSP_ERANGE, "%u classes exceed the limit of %d", C, jsp::kMaxClasses);
     if (C > 0 && !classes) return set_err(JSP_EINVAL, "classes is NULL");
@@ -842,6 +1014,26 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (int rc = check_runs(e, run_class, run_len, n_runs, &J64)) return rc;
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
+    const bool want_tally = (tally_out && e->C > 0) || occ_out;
+    if (!want_tally && svc_ok(e)) {
+        const auto t1 = std::chrono::steady_clock::now();
+        uint32_t placed = 0;
+        if (int rc = svc_place(e, J, assign_out, &placed)) return rc;
+        const auto t2 = std::chrono::steady_clock::now();
+        e->last_shape = 3;
+        if (stats) {
+            stats->jobs = J;
+            stats->runs = n_runs;
+            stats->placed = n_runs > 0 ? placed : 0;
+            stats->fused = 3;
+            stats->wall_us = std::chrono::duration<double, std::micro>(t2 - t0).count();
+        }
+        using us = std::chrono::duration<double, std::micro>;
+        e->acc.host_calls += 1;
+        e->acc.host_prep_us += us(t1 - t0).count();
+        e->acc.host_wait_us += us(t2 - t1).count();
+        return JSP_OK;
+    }
     hipStream_t s = e->stream;
     if (int rc = check_launch_error(e)) return rc;
     if (int rc = enter_stream(e, s)) return rc;
@@ -858,7 +1050,6 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         std::memcpy(h_rc, run_class, (size_t)n_runs * 4);
         std::memcpy(h_rl, run_len, (size_t)n_runs * 4);
     }
-    const bool want_tally = (tally_out && e->C > 0) || occ_out;
     e->stats_override = e->h_stats.as<uint32_t>();
     uint32_t n_sig = 0;
     const auto t1 = std::chrono::steady_clock::now();
@@ -965,8 +1156,28 @@ int jsp_engine_set_fused(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_FUSED_OFF && mode != JSP_FUSED_AUTO) return set_err(JSP_EINVAL, "fused mode %d", mode);
+    if (mode != e->fused_mode) {
+        if (int rc = svc_stop(e)) return rc;
+    }
     e->fused_mode = mode;
     return JSP_OK;
+}
+
+int jsp_engine_set_service(jsp_engine* e, int mode) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO) return set_err(JSP_EINVAL, "service mode %d", mode);
+    if (mode == JSP_SERVICE_OFF) {
+        if (int rc = svc_stop(e)) return rc;
+    }
+    e->svc_mode = mode;
+    return JSP_OK;
+}
+
+int jsp_engine_service_stop(jsp_engine* e) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    return svc_stop(e);
 }
 
 int jsp_engine_set_timing(jsp_engine* e, int enable) {

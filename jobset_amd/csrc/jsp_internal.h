@@ -121,6 +121,24 @@ struct CompactArgs {
     uint32_t spin_limit;           // look-back polls before a tile gives up (JSP_LOOKBACK_SPINS in tests)
 };
 
+// Resident placement service (place_service_kernel): the compaction shape kept
+// on the GPU between host-API placements, fed through a host-mapped request
+// word instead of a launch.
+constexpr uint32_t kSvcStop = 0xFFFFFFFFu;  // request word's low half: every workgroup leaves
+struct ServiceArgs {
+    const unsigned long long* mailbox;  // host-mapped: (J << 32) | seq, seq != 0; written last by the host
+    unsigned long long* granules;       // [n_blocks] the service's own look-back granules (tag = seq)
+    uint32_t pods;
+    uint32_t seq0;                      // the request word's seq at launch (already answered)
+    int32_t* assign;                    // host-mapped [capacity >= J of every request]
+    uint32_t* stats;                    // host-mapped [2]: runs (1), placed
+    uint32_t* done;                     // host-mapped [n_blocks]: seq of the last answered request
+    uint32_t* err;                      // host-mapped: a tile whose look-back timed out writes its epoch
+    uint32_t* clk;                      // host-mapped [2 n_blocks] {seen, done} 100 MHz stamps, or null
+    uint32_t spin_limit;
+    unsigned long long idle_ticks;      // 100 MHz ticks without a request before a workgroup leaves
+};
+
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }
 constexpr uint32_t kFusedMaxWords = 6144;  // taken + feasibility words the fused tail keeps in LDS (48 KiB)
 constexpr uint32_t kFusedStage = 2048;     // ranks the fused tail stages per long-run step (8 KiB)
@@ -157,6 +175,7 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
+hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
                        uint32_t topo_words, uint32_t fscr_words);

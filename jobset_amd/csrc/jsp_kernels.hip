@@ -1660,32 +1660,26 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoc
     __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// One compaction tile: tally its leaves, count the feasible ones, look back
+// for the feasible leaves before it, scatter its jobs' domains. `sys`: assign[]
+// and stats are in pinned host memory (system-scope stores). s_x: the small
+// LDS words after the tally carve ([2] prefix [3] timeout [4..16] scan).
 template <int W, int R>
-__global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs a, CompactArgs f) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* s_x = lds + tally_lds_words(a);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
+__device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint32_t epoch, uint32_t pods,
+                                             uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
+                                             int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
+                                             uint32_t* s_x) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const uint32_t epoch = f.epoch;  // host launch counter, 30-bit, never 0
-    // tiles in start order (oversubscribed grid): a tile only ever waits on
-    // tiles that workgroups already hold, and the first-started take them all
-    if (tid == 0)
-        s_x[0] = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                            f.tile_base);
-    __syncthreads();
-    const uint32_t tile = s_x[0];
-    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
-    JSP_STAMP(tile, 0);
     tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     JSP_STAMP(tile, 2);
 
     const uint32_t* s_acc = lds + tally_acc_off(1);
     const uint4 bt = a.blk[tile];
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
-    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= f.pods && s_acc[a.la + tid] == 0;
+    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
     uint32_t total;
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
     JSP_STAMP(tile, 3);
-    unsigned long long* g = f.granules;
     if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total);
     if (tid < 64) {  // wave 0: look back
         uint32_t prefix = 0, spins = 0;
@@ -1701,7 +1695,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
                     v = (uint32_t)x;
                 }
                 if (__all(idx < 0 || st != 0)) break;
-                if (++spins > f.spin_limit) { timeout = true; break; }
+                if (++spins > spin_limit) { timeout = true; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
             const unsigned long long pm = __ballot(idx >= 0 && st == kPrefix);
@@ -1724,22 +1718,105 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     JSP_STAMP(tile, 4);
     const uint32_t prefix = s_x[2];
     const bool failed = s_x[3] != 0;
-    const bool sys = f.done != nullptr;  // host path: assign[] and stats are in pinned host memory
     if (!failed) {
-        if (ok && prefix + rank < f.J) store_out(f.assign + prefix + rank, (int32_t)(a.leaf_base + l0 + tid), sys);
+        if (ok && prefix + rank < J) store_out(assign + prefix + rank, (int32_t)(a.leaf_base + l0 + tid), sys);
         if (tile + 1 == a.n_blocks) {
-            const uint32_t placed = prefix + total < f.J ? prefix + total : f.J;
-            for (uint32_t j = placed + tid; j < f.J; j += kTallyThreads) store_out(f.assign + j, -1, sys);
-            if (tid == 0 && f.stats) {
-                store_out(f.stats, f.n_runs, sys);
-                store_out(f.stats + 1, placed, sys);
+            const uint32_t placed = prefix + total < J ? prefix + total : J;
+            for (uint32_t j = placed + tid; j < J; j += kTallyThreads) store_out(assign + j, -1, sys);
+            if (tid == 0 && stats) {
+                store_out(stats, n_runs, sys);
+                store_out(stats + 1, placed, sys);
             }
         }
     } else if (tid == 0) {
-        __hip_atomic_store(f.err, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(err, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-    if (sys) signal_host(f.done + tile, epoch, false);
+}
+
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs a, CompactArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* s_x = lds + tally_lds_words(a);  // [0] tile [2] prefix [3] timeout [4..] scan scratch
+    // tiles in start order (oversubscribed grid): a tile only ever waits on
+    // tiles that workgroups already hold, and the first-started take them all
+    if (threadIdx.x == 0)
+        s_x[0] = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                            f.tile_base);
+    __syncthreads();
+    const uint32_t tile = s_x[0];
+    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
+    JSP_STAMP(tile, 0);
+    const bool sys = f.done != nullptr;  // host path: assign[] and stats are in pinned host memory
+    compact_tile<W, R>(a, tile, f.epoch, f.pods, f.J, f.n_runs, f.granules, f.spin_limit, f.assign, f.stats, f.err,
+                       sys, lds, s_x);
+    if (sys) signal_host(f.done + tile, f.epoch, false);
     JSP_STAMP(tile, 5);
+}
+
+// ----------------------------------------------------------------- resident placement service
+// The compaction kept resident between placements: one
+// workgroup per tile, each polling the host-mapped request word (vector
+// system-scope loads; the host writes it with one 64-bit store). A request is
+// (J << 32) | seq; the tile runs compact_tile with granules tagged by seq,
+// writes assign[] / stats into pinned host memory and publishes done[tile] =
+// seq. Every workgroup leaves on kSvcStop or after idle_ticks of the 100 MHz
+// clock without a request, so the grid always drains; a tile whose look-back
+// partner left (the host posted into an exit) times out and reports it.
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs a, ServiceArgs v) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* s_x = lds + tally_lds_words(a);  // compact_tile's words, then [16] request seq [17] J
+    const uint32_t tile = blockIdx.x;
+    uint32_t seq = v.seq0;
+    while (true) {
+        if (threadIdx.x == 0) {
+            uint32_t next = 0, J = 0;  // next == 0: leave
+            uint64_t t0 = wall_clock64();
+            while (true) {
+                const unsigned long long m =
+                    __hip_atomic_load(const_cast<unsigned long long*>(v.mailbox), __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint32_t q = (uint32_t)m;
+                if (q == kSvcStop) break;
+                if (q != seq && q != 0) {
+                    next = q;
+                    J = (uint32_t)(m >> 32);
+                    break;
+                }
+                const uint64_t t = wall_clock64();
+                if (t - t0 > v.idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            // the snapshot may have been patched since this workgroup's last
+            // request (another launch, other XCDs): drop this CU's stale lines
+            // before any of this request's loads (one lane; the barrier below
+            // holds the other waves until the invalidate has completed)
+            if (next != 0) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            s_x[16] = next;
+            s_x[17] = J;
+            if (next != 0 && v.clk) __hip_atomic_store(v.clk + 2 * tile, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        __syncthreads();
+        const uint32_t next = s_x[16], J = s_x[17];
+        if (next == 0) return;
+        const uint32_t epoch = next & 0x3FFFFFFFu;
+        compact_tile<W, R>(a, tile, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit, v.assign,
+                           v.stats, v.err, true, lds, s_x);
+        if (v.clk) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            if (threadIdx.x == 0)
+                __hip_atomic_store(v.clk + 2 * tile + 1, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        signal_host(v.done + tile, next, false);
+        seq = next;
+        __syncthreads();  // s_x[16..17] and the tally carve are rewritten by the next request
+    }
 }
 
 // ----------------------------------------------------------------- A5 / A9 batch kernels
@@ -1859,6 +1936,17 @@ hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
 
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
     JSP_DISPATCH_WR(launch_compact_wr, a, f, s)
+}
+
+template <int W, int R>
+static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
+    hipLaunchKernelGGL((place_service_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads), compact_lds_bytes(a.la),
+                       s, a, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_service_wr, a, v, s)
 }
 
 size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }

@@ -206,6 +206,15 @@ class Engine:
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
+    def set_service(self, enable: bool) -> None:
+        """Resident placement service for host-API compaction placements
+        (jsp_engine_set_service; on by default)."""
+        check(self._lib.jsp_engine_set_service(self._h, native.JSP_SERVICE_AUTO if enable else native.JSP_SERVICE_OFF))
+
+    def service_stop(self) -> None:
+        """Stop the resident service now (before a device-wide synchronize)."""
+        check(self._lib.jsp_engine_service_stop(self._h))
+
     # ---------------------------------------------------------------- webhook / reconciler batches
     def resolve_leader_domains(self, leader_rows: np.ndarray, levels: np.ndarray) -> np.ndarray:
         rows = np.ascontiguousarray(leader_rows, dtype=np.int32)

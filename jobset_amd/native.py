@@ -47,10 +47,12 @@ class JspTiming(ctypes.Structure):
                 ("assign_ms", ctypes.c_double), ("fused_ms", ctypes.c_double), ("fused_calls", ctypes.c_uint64),
                 ("host_calls", ctypes.c_uint64), ("host_prep_us", ctypes.c_double),
                 ("host_launch_us", ctypes.c_double), ("host_wait_us", ctypes.c_double),
-                ("host_post_us", ctypes.c_double)]
+                ("host_post_us", ctypes.c_double), ("svc_calls", ctypes.c_uint64), ("svc_starts", ctypes.c_uint64),
+                ("svc_us", ctypes.c_double)]
 
 
 JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
+JSP_SERVICE_OFF, JSP_SERVICE_AUTO = 0, 1
 
 
 # (name, restype, argtypes) — every entry point declared in include/jsplace.h
@@ -72,6 +74,8 @@ SIGNATURES = [
     ("jsp_resolve_leader_domains", ctypes.c_int, [vp, vp, vp, u32, vp]),
     ("jsp_audit_placements", ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp]),
     ("jsp_engine_set_fused", ctypes.c_int, [vp, ctypes.c_int]),
+    ("jsp_engine_set_service", ctypes.c_int, [vp, ctypes.c_int]),
+    ("jsp_engine_service_stop", ctypes.c_int, [vp]),
     ("jsp_engine_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
     ("jsp_engine_stream", vp, [vp]),

@@ -490,7 +490,7 @@ def test_compaction_ticket_interleaved_with_fused(engine, jobs):
     engine.load(p)
     for _ in range(3):
         got = engine.place(p.job_class, want_tally=True)
-        assert got.fused == 2
+        assert got.fused == 2  # tallies requested: the launch path
         assert_same(got, a, cap, occ)
     engine.load(q)
     for _ in range(3):

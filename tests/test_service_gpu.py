@@ -1,0 +1,165 @@
+"""Resident placement service (jsp_engine_set_service): host-API
+placements of the one-class compaction shape answered by the persistent
+kernel through the pinned request word. Bit-exact against the oracle and the
+launch path, across repeated requests, job counts that outgrow the output
+buffer, snapshot re-uploads and patches, idle exits and explicit stops."""
+import dataclasses
+import time
+
+import numpy as np
+import pytest
+
+from jobset_amd import synth
+from jobset_amd.snapshot import job_runs
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture
+def svc_engine(engine):
+    engine.set_service(True)
+    engine.set_fused(True)
+    yield engine
+    engine.service_stop()
+
+
+def one_leaf_class(p):
+    """The problem reduced to its first class moved to the leaf level (the
+    compaction shape the service answers)."""
+    K = p.topology.n_levels
+    p.classes = [dataclasses.replace(p.classes[0], level=K - 1)]
+    p.job_class = np.zeros(p.n_jobs, dtype=np.uint32)
+    return p
+
+
+def test_service_configs_repeated(svc_engine):
+    """cfg1 and cfg2 (the headline), 200 requests each on one service."""
+    svc_engine.timing(reset=True)
+    for cfg in (1, 2):
+        p = synth.CONFIGS[cfg]()
+        svc_engine.load(p)
+        a = O.place_c(p)[0]
+        call = svc_engine.host_placer(*job_runs(p.job_class))
+        for _ in range(200):
+            st = call()
+            assert st.fused == 3
+            np.testing.assert_array_equal(call.assign, a)
+            assert st.placed == int((a >= 0).sum())
+    t = svc_engine.timing(reset=True)
+    assert t.svc_calls == 400
+    assert 2 <= t.svc_starts <= 4  # one per upload (+ a rare idle restart)
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_service_random_parity(svc_engine, seed):
+    """Ragged random snapshots (empty and 1-node leaves, 1-3 levels, W/R 1..4,
+    occupancy) with one leaf-level class: service == oracle == launch path."""
+    p = one_leaf_class(synth.random_problem(seed))
+    svc_engine.load(p)
+    a, cap, occ = O.place_c(p)
+    for _ in range(3):
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, a)
+        assert got.placed == int((a >= 0).sum())
+    ref = svc_engine.place(p.job_class, want_tally=True)  # launch path (tallies requested)
+    assert ref.fused == 2
+    np.testing.assert_array_equal(ref.assign, a)
+    np.testing.assert_array_equal(ref.cap, cap)
+
+
+def test_service_job_counts_and_growth(svc_engine):
+    """J = 0, 1, more jobs than feasible racks, and a J beyond the service's
+    output capacity (restart with a larger pinned buffer)."""
+    p = synth.config2()
+    svc_engine.load(p)
+    for J in (0, 1, 990, 1500, 5000, 7000, 3, 0):
+        p.job_class = np.zeros(J, dtype=np.uint32)
+        a = O.place_c(p)[0]
+        got = svc_engine.place(p.job_class)
+        assert got.assign.shape == (J,)
+        np.testing.assert_array_equal(got.assign, a)
+        assert got.fused == 3
+
+
+def test_service_patch_and_reupload(svc_engine):
+    """Patches (no restart: the service is idle between requests and the patch
+    is synchronous) and re-uploads (restart on new buffers) are both seen."""
+    p = synth.config2()
+    svc_engine.load(p)
+    np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, O.place_c(p)[0])
+    svc_engine.timing(reset=True)
+    rng = np.random.default_rng(7)
+    for step in range(10):
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=50, replace=False)).astype(np.uint32)
+        taints = rng.integers(0, 2, size=50).astype(np.uint32)
+        svc_engine.patch_rows(rows, taints=taints)
+        p.nodes.taints[rows] = taints
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    assert svc_engine.timing(reset=True).svc_starts <= 1  # patches do not restart it (an idle gap might)
+    for t in range(5):  # recovery trials: a new post-delete snapshot each
+        q = synth.config2(trial=t)
+        svc_engine.load(q)
+        got = svc_engine.place(q.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
+    assert svc_engine.timing(reset=True).svc_starts == 5
+
+
+def test_service_idle_exit_and_stop(svc_engine):
+    """After an idle gap the service has left (or is about to): the host
+    restarts it and the answer is unchanged. An explicit stop, a device-wide
+    synchronize, and the launch path in between all keep working."""
+    import torch
+    p = synth.config2()
+    svc_engine.load(p)
+    a = O.place_c(p)[0]
+    svc_engine.timing(reset=True)
+    for gap in (0.0, 0.03, 0.2, 0.0):
+        time.sleep(gap)
+        np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, a)
+    assert svc_engine.timing(reset=True).svc_starts >= 2
+    svc_engine.service_stop()
+    torch.cuda.synchronize()  # nothing resident: returns at once
+    np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, a)
+    t0 = time.perf_counter()
+    torch.cuda.synchronize()  # waits for the service's idle exit (JSP_SERVICE_IDLE_MS, 50 ms)
+    assert time.perf_counter() - t0 < 5.0
+    np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, a)
+
+
+def test_service_off_equals_on(svc_engine):
+    p = synth.config2(trial=3)
+    svc_engine.load(p)
+    on = svc_engine.place(p.job_class)
+    svc_engine.set_service(False)
+    off = svc_engine.place(p.job_class)
+    svc_engine.set_service(True)
+    assert on.fused == 3 and off.fused == 2
+    np.testing.assert_array_equal(on.assign, off.assign)
+
+
+def test_service_timing_stamps(svc_engine):
+    """With timing on, every request's in-kernel time (first tile saw it ->
+    last tile done, 100 MHz device clock) is accumulated and is below the
+    host wall time of the call."""
+    p = synth.config2()
+    svc_engine.load(p)
+    svc_engine.set_timing(True)
+    try:
+        call = svc_engine.host_placer(*job_runs(p.job_class))
+        svc_engine.timing(reset=True)
+        walls = []
+        for _ in range(100):
+            t0 = time.perf_counter()
+            call()
+            walls.append((time.perf_counter() - t0) * 1e6)
+        t = svc_engine.timing(reset=True)
+    finally:
+        svc_engine.set_timing(False)
+    assert t.svc_calls == 100
+    per = t.svc_us / t.svc_calls
+    assert 0.0 < per < float(np.median(walls))
