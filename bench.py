@@ -50,8 +50,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 SHAPES = {0: "three launches (tally -> feas -> assign + expand)", 1: "fused single launch",
-          2: "single-class compaction, one launch"}
-KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel"}
+          2: "single-class compaction, one launch",
+          3: "single-class compaction answered by the resident service (no launch per placement)"}
+KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel"}
 
 
 def tally_bytes(p) -> int:
@@ -194,8 +195,8 @@ def host_api_latency(eng, p, trials: int, trial_fn=None):
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=200)
-    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=2000)
+    ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99) on config 2")
     ap.add_argument("--cpu-seconds", type=float, default=9.0, help="bounded CPU-baseline sample (all legs)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the 1M-node sharded leg")
@@ -239,18 +240,44 @@ def main() -> None:
     call = eng.host_placer(*job_runs(p.job_class))
     for _ in range(args.warmup):
         call()
+    # The resident service (shape 3) stays on the GPU between calls, and a
+    # device-wide synchronize waits for it to leave: it is stopped right
+    # before each synchronize, and its restart by the first timed call and
+    # its stop after the last are inside the timed region.
+    eng.service_stop()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         call()
+    eng.service_stop()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
     placed = int((call.assign >= 0).sum())
     value = placed * args.steps * world / elapsed
+
+    # the service's own clock: per request, first tile saw it -> last tile's
+    # assign[] drained (100 MHz device stamps, timing on; not the timed loop)
+    svc = None
+    if shape == 3:
+        eng.set_timing(True)
+        for _ in range(args.warmup):
+            call()
+        eng.timing(reset=True)
+        for _ in range(args.steps):
+            call()
+        ts = eng.timing(reset=True)
+        eng.set_timing(False)
+        eng.service_stop()
+        req_us = ts.svc_us / max(ts.svc_calls, 1)
+        svc = {"request_us_device": round(req_us, 3),
+               "achieved_gbs": round(compact_bytes(p) / (req_us * 1e-6) / 1e9, 2),
+               "calls": int(ts.svc_calls),
+               "note": "device time of one request inside the resident kernel (stamps on, which add "
+                       "~0.5-1 us); the host-API wall adds the host-link hand-offs"}
 
     # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
     step, out = device_step(p)
@@ -266,10 +293,14 @@ def main() -> None:
     el_dev = max_over_ranks(time.perf_counter() - t0, world)
     assert int((out[:J].cpu().numpy() >= 0).sum()) == placed
 
-    # dominant kernel: the step's single launch (compaction / fused), else the tally
-    if shape in (1, 2):
+    # dominant kernel: the step's single launch (compaction / fused), else the
+    # tally. With the resident service (shape 3) the same tile code runs inside
+    # the persistent kernel, which HIP events cannot bracket per request: the
+    # roofline is the launch-path compaction kernel's, the service's own
+    # per-request device time is under "service".
+    if shape in (1, 2, 3):
         dom_us = event_loop_us(step, args.steps, stream)
-        tb = compact_bytes(p) if shape == 2 else tally_bytes(p) + placement_tail_bytes(p)
+        tb = compact_bytes(p) if shape in (2, 3) else tally_bytes(p) + placement_tail_bytes(p)
     else:
         cap = torch.empty((len(p.classes) + 1, p.topology.n_leaves), dtype=torch.int32, device="cuda")
         dom_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
@@ -281,6 +312,7 @@ def main() -> None:
 
     # ------------------------------------------------ p50/p99 recovery latency (host API, trial snapshots)
     lat2 = host_api_latency(eng, p, args.trials, synth.config2) if rank == 0 and args.trials > 0 else None
+    eng.service_stop()
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
     cpu = None
@@ -325,6 +357,7 @@ def main() -> None:
                     "host_api_resident": host_api_latency(eng, pc, 200)}
             if cfg in (3, 5):
                 line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
+            eng.service_stop()
             if world == 1 and args.cpu_seconds > 0:
                 from oracle import oracle as O
                 for th in sorted({1, T}):
@@ -408,7 +441,7 @@ def main() -> None:
             "dtype": "u32",
             "data": "synthetic",
             "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery; one step "
-                                   "= one host-API jsp_place (runs H2D, assign[] D2H)",
+                                   "= one host-API jsp_place (run list in, assign[] back in the caller's host buffer)",
                        "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J,
                        "pods_per_job": p.classes[0].pods, "classes": len(p.classes),
                        "shape": SHAPES[shape], "parallelism": f"replicas{world}"},
@@ -420,6 +453,7 @@ def main() -> None:
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
                          "note": "latency-bound: one launch moving 0.43 MB; see DESIGN.md §8"},
+            "service": svc,
             "p50_recovery_us": lat2["p50_us"] if lat2 else None,
             "p99_recovery_us": lat2["p99_us"] if lat2 else None,
             "recovery_trials": lat2["n"] if lat2 else 0,

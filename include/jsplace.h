@@ -231,6 +231,11 @@ int jsp_engine_set_fused(jsp_engine* e, int mode);
 int jsp_engine_set_service(jsp_engine* e, int mode);
 /* Stops the resident service (if running) and waits for its workgroups to leave. */
 int jsp_engine_service_stop(jsp_engine* e);
+/* With timing on: the last service request's 100 MHz device-clock stamps, 8
+ * per tile (0 request seen, 1 after the acquire, 2 tallied, 3 feasible count
+ * scanned, 4 look-back done, 5 assign[] drained; 6-7 unused). Copies up to
+ * cap/8 tiles; *n_tiles = how many (0 when no timed request is held). */
+int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

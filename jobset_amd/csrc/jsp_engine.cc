@@ -148,11 +148,12 @@ struct jsp_engine {
         bool running = false;
         hipStream_t stream = nullptr;
         HostBuf box;     // [0] request word: (J << 32) | seq
-        HostBuf words;   // done[nb] | stats[2] | err[1] | clk[2 nb]
+        HostBuf words;   // done[nb] | stats[2] | err[1] | clk[kSvcClkSlots nb]
         HostBuf assign;  // [cap]
         DevBuf granules;
-        uint32_t cap = 0, nb = 0, seq = 0, err_ack = 0;
+        uint32_t cap = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
         bool clk = false;
+        bool resume = false;  // an upload stopped it: start it again once the engine is ready
         std::chrono::steady_clock::time_point last{};
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
@@ -464,7 +465,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
 // the host restarts the service when its own last request is older than half
 // of that, so it never posts into an exit (and if it ever did, the dead
 // service is seen by a stream query and the request re-posted once).
-constexpr uint32_t kSvcMaxBlocks = 256;  // one tile per workgroup, all co-resident (<= one per CU)
+constexpr uint32_t kSvcMaxBlocks = 255;  // one tile per workgroup + the dispatcher, all co-resident (<= one per CU)
 constexpr int kSvcGone = 1;
 
 double svc_idle_ms() {
@@ -477,7 +478,8 @@ double svc_idle_ms() {
 }
 
 bool svc_ok(jsp_engine* e) {
-    return e->svc_mode == JSP_SERVICE_AUTO && compact_ok(e) && e->n_blocks <= kSvcMaxBlocks;
+    return e->svc_mode == JSP_SERVICE_AUTO && e->have_topo && e->have_snap && e->have_cls && compact_ok(e) &&
+           e->n_blocks <= kSvcMaxBlocks;
 }
 
 int svc_stop(jsp_engine* e) {
@@ -489,6 +491,22 @@ int svc_stop(jsp_engine* e) {
     return JSP_OK;
 }
 
+// Uploads stop the service (it holds the old buffers and geometry) and start
+// it again at their end when it was running, so the next jsp_place -- the
+// recovery path: post-delete snapshot uploaded, then placed -- finds it ready.
+int svc_suspend(jsp_engine* e) {
+    e->svc.resume |= e->svc.running;
+    return svc_stop(e);
+}
+
+int svc_start(jsp_engine* e, uint32_t J);
+void svc_resume(jsp_engine* e) {
+    if (e->svc.resume && svc_ok(e)) {
+        e->svc.resume = false;
+        (void)svc_start(e, 0);  // a failure here resurfaces at the next jsp_place
+    }
+}
+
 int svc_start(jsp_engine* e, uint32_t J) {
     auto& v = e->svc;
     if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
@@ -498,10 +516,12 @@ int svc_start(jsp_engine* e, uint32_t J) {
         HIP_TRY(v.assign.reserve((size_t)cap * 4));
         v.cap = cap;
     }
-    HIP_TRY(v.words.reserve((size_t)(3 * nb + 3) * 4));
-    std::memset(v.words.p, 0, (size_t)(3 * nb + 3) * 4);  // done words: seq 0 is never posted
+    const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * nb + 3;
+    HIP_TRY(v.words.reserve(nw * 4));
+    std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
     HIP_TRY(v.box.reserve(64));
-    HIP_TRY(v.granules.reserve((size_t)8 * std::max<uint32_t>(nb, 1)));
+    const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
+    HIP_TRY(v.granules.reserve(gpad + 128));  // granules, then the bell on a line of its own
     // after everything the engine enqueued on any stream (the last stream's
     // event), without making later calls wait for the service
     if (e->have_last) {
@@ -509,12 +529,16 @@ int svc_start(jsp_engine* e, uint32_t J) {
         HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
         HIP_TRY(hipStreamWaitEvent(v.stream, e->ev_switch, 0));
     }
-    HIP_TRY(hipMemsetAsync(v.granules.p, 0, (size_t)8 * std::max<uint32_t>(nb, 1), v.stream));
+    HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 128, v.stream));
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
+    v.gen = v.gen % 0x7FFFFFFFu + 1u;
+    uint32_t* ready = v.box.as<uint32_t>() + 2;
+    __atomic_store_n(ready, 0u, __ATOMIC_RELEASE);
     uint32_t* w = v.words.as<uint32_t>();
     jsp::ServiceArgs a{};
     a.mailbox = v.box.as<unsigned long long>();
     a.granules = v.granules.as<unsigned long long>();
+    a.bell = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad);
     a.pods = e->cls_h[0].pods;
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();
@@ -524,13 +548,27 @@ int svc_start(jsp_engine* e, uint32_t J) {
     a.clk = e->timing ? w + nb + 3 : nullptr;
     a.spin_limit = e->spin_limit;
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
+    a.ready = ready;
+    a.gen = v.gen;
     v.err_ack = 0;
     v.nb = nb;
     v.clk = e->timing;
     HIP_TRY(jsp::launch_service(tally_args(e, nullptr, nullptr, e->L_total), a, v.stream));
     v.running = true;
-    v.last = std::chrono::steady_clock::now();
     e->acc.svc_starts += 1;
+    // return once the dispatcher polls: a request posted now is answered
+    // without waiting for the launch
+    for (uint64_t spins = 1; __atomic_load_n(ready, __ATOMIC_ACQUIRE) != v.gen; ++spins) {
+        if ((spins & 255) == 0) {
+            const hipError_t q = hipStreamQuery(v.stream);
+            if (q != hipErrorNotReady) {
+                v.running = false;
+                return set_err(JSP_EHIP, "placement service ended before it started polling: %s",
+                               hipGetErrorString(q));
+            }
+        }
+    }
+    v.last = std::chrono::steady_clock::now();
     return JSP_OK;
 }
 
@@ -598,8 +636,8 @@ int svc_place(jsp_engine* e, uint32_t J, int32_t* assign_out, uint32_t* placed) 
         const uint32_t ref = clk[0];
         int32_t lo = 0, hi = 0;
         for (uint32_t t = 0; t < v.nb; ++t) {
-            lo = std::min(lo, (int32_t)(clk[2 * t] - ref));
-            hi = std::max(hi, (int32_t)(clk[2 * t + 1] - ref));
+            lo = std::min(lo, (int32_t)(clk[jsp::kSvcClkSlots * t] - ref));
+            hi = std::max(hi, (int32_t)(clk[jsp::kSvcClkSlots * t + 5] - ref));
         }
         e->acc.svc_us += (double)(hi - lo) / 100.0;
     }
@@ -717,7 +755,7 @@ void jsp_engine_destroy(jsp_engine* e) {
 int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
-    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
+    if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!t) return set_err(JSP_EINVAL, "topology is NULL");
     // a failed upload leaves the engine without topology (buffers may be gone)
     e->have_topo = e->have_snap = e->have_cls = false;
@@ -790,7 +828,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
 int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
-    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
+    if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (!nd || !nd->leaf_start) return set_err(JSP_EINVAL, "nodes / leaf_start is NULL");
     e->have_snap = false;  // until every column is resident again
@@ -886,6 +924,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
                 return set_err(JSP_ERANGE, "pods x rows per leaf overflows 32-bit tallies; re-upload classes");
             }
     }
+    svc_resume(e);
     return JSP_OK;
 }
 
@@ -917,7 +956,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
 int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
-    if (int rc = svc_stop(e)) return rc;  // it holds the old buffers and geometry
+    if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
     if (C > (uint32_t)jsp::kMaxClasses) return set_err(JSP_ERANGE, "%u classes exceed the limit of %d", C, jsp::kMaxClasses);
     if (C > 0 && !classes) return set_err(JSP_EINVAL, "classes is NULL");
@@ -958,6 +997,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
     e->C = C;
     e->feas_words = woff[C];
     e->have_cls = true;
+    svc_resume(e);
     return JSP_OK;
 }
 
@@ -1168,15 +1208,31 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO) return set_err(JSP_EINVAL, "service mode %d", mode);
     if (mode == JSP_SERVICE_OFF) {
+        e->svc.resume = false;
         if (int rc = svc_stop(e)) return rc;
     }
     e->svc_mode = mode;
     return JSP_OK;
 }
 
+int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (!n_tiles) return set_err(JSP_EINVAL, "n_tiles is NULL");
+    *n_tiles = 0;
+    const auto& v = e->svc;
+    if (!v.clk || !v.words.p) return JSP_OK;
+    const uint32_t n = std::min<uint32_t>(cap / jsp::kSvcClkSlots, v.nb);
+    if (n > 0 && !out) return set_err(JSP_EINVAL, "out is NULL");
+    std::memcpy(out, v.words.as<uint32_t>() + v.nb + 3, (size_t)n * jsp::kSvcClkSlots * 4);
+    *n_tiles = n;
+    return JSP_OK;
+}
+
 int jsp_engine_service_stop(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
+    e->svc.resume = false;
     return svc_stop(e);
 }
 

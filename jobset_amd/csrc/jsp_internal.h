@@ -125,18 +125,22 @@ struct CompactArgs {
 // on the GPU between host-API placements, fed through a host-mapped request
 // word instead of a launch.
 constexpr uint32_t kSvcStop = 0xFFFFFFFFu;  // request word's low half: every workgroup leaves
+constexpr uint32_t kSvcClkSlots = 8;        // per tile: seen, acquired, tallied, scanned, looked back, drained
 struct ServiceArgs {
     const unsigned long long* mailbox;  // host-mapped: (J << 32) | seq, seq != 0; written last by the host
     unsigned long long* granules;       // [n_blocks] the service's own look-back granules (tag = seq)
+    unsigned long long* bell;           // device word: the dispatcher's copy of the request word (sc1)
     uint32_t pods;
     uint32_t seq0;                      // the request word's seq at launch (already answered)
     int32_t* assign;                    // host-mapped [capacity >= J of every request]
     uint32_t* stats;                    // host-mapped [2]: runs (1), placed
     uint32_t* done;                     // host-mapped [n_blocks]: seq of the last answered request
     uint32_t* err;                      // host-mapped: a tile whose look-back timed out writes its epoch
-    uint32_t* clk;                      // host-mapped [2 n_blocks] {seen, done} 100 MHz stamps, or null
+    uint32_t* clk;                      // host-mapped [kSvcClkSlots n_blocks] 100 MHz phase stamps, or null
     uint32_t spin_limit;
     unsigned long long idle_ticks;      // 100 MHz ticks without a request before a workgroup leaves
+    uint32_t* ready;                    // host-mapped: the dispatcher writes gen once it polls
+    uint32_t gen;                       // service launch number
 };
 
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }

@@ -172,6 +172,18 @@ __device__ __forceinline__ uint32_t leaf_search(const uint32_t* ls, uint32_t n, 
     return lo;
 }
 
+constexpr uint32_t kSvcStaggerTicks = 50;  // 100 MHz ticks between the dispatcher's polling waves
+
+// Request phase stamp of the resident service (timing on): thread 0 stores the
+// 100 MHz clock into the tile's host-mapped clock slots (posted system-scope
+// stores; nothing waits on them). Slots: 0 request seen, 1 request broadcast
+// to the workgroup, 2 tallied, 3 feasible count scanned, 4 look-back done,
+// 5 assign[] drained, 6 row pass done, 7 leaf pass done.
+__device__ __forceinline__ void svc_stamp(uint32_t* clk, int slot) {
+    if (clk && threadIdx.x == 0)
+        __hip_atomic_store(clk + slot, (uint32_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ----------------------------------------------------------------- A8 tally (one workgroup)
 // LDS carve (uint32 words), sized per launch by nv = classes in this pass + 1:
 //   [classes nc x DevClass][acc nv x la][wsum nv x 4]
@@ -210,9 +222,37 @@ struct RowRegs {
     int32_t ex[4];
 };
 
-template <int W, int R>
+// 16 bytes of a column at byte offset `off`, `sc1` (agent scope): bypasses
+// this CU's L1, so rows another launch patched since this workgroup last read
+// them are never served from stale L1 lines (the resident service has no
+// kernel-start invalidate between requests). Offsets are 32-bit: the service
+// runs for <= 255 tiles (~261k rows).
+__device__ __forceinline__ uint4 load16_sc1(const void* base, uint32_t off) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                                                       0x7FFFFFF0, 0x00020000);
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+template <int W, int R, bool SC1 = false>
 __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool any, RowRegs<W, R>& x) {
-    if (any) {
+    if (SC1 && any) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+            const uint64_t* col = a.labels + (size_t)w * a.npad;
+            const uint4 u = load16_sc1(col, row * 8u), v = load16_sc1(col, row * 8u + 16u);
+            x.lab[w][0] = ((uint64_t)u.y << 32) | u.x; x.lab[w][1] = ((uint64_t)u.w << 32) | u.z;
+            x.lab[w][2] = ((uint64_t)v.y << 32) | v.x; x.lab[w][3] = ((uint64_t)v.w << 32) | v.z;
+        }
+        const uint4 t4 = load16_sc1(a.taints, row * 4u);
+        x.tn[0] = t4.x; x.tn[1] = t4.y; x.tn[2] = t4.z; x.tn[3] = t4.w;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint4 f4 = load16_sc1(a.freer + (size_t)r * a.npad, row * 4u);
+            x.fr[r][0] = f4.x; x.fr[r][1] = f4.y; x.fr[r][2] = f4.z; x.fr[r][3] = f4.w;
+        }
+        const uint4 e4 = load16_sc1(a.excl, row * 4u);
+        x.ex[0] = (int32_t)e4.x; x.ex[1] = (int32_t)e4.y; x.ex[2] = (int32_t)e4.z; x.ex[3] = (int32_t)e4.w;
+    } else if (any) {
 #pragma unroll
         for (int w = 0; w < W; ++w) {
             const ulonglong2* p = reinterpret_cast<const ulonglong2*>(a.labels + (size_t)w * a.npad + row);
@@ -275,8 +315,13 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
     return k;
 }
 
-template <int W, int R>
-__device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds) {
+// STAGED (resident service): the class records and the tile's leaf starts are
+// already in LDS (staged once per service lifetime: they change only with an
+// upload, which restarts the service) and `bt` is the tile's geometry, so the
+// first chunk's row loads are the request's first memory access.
+template <int W, int R, bool STAGED = false>
+__device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds,
+                                            uint4 bt_staged = make_uint4(0, 0, 0, 0), uint32_t* clk = nullptr) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
     DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
@@ -287,7 +332,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     uint32_t* s_pre = lds + tally_pre_off(nc, nv, la);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint4 bt = a.blk[blk];  // {first leaf, end leaf, first row, end row}
+    const uint4 bt = STAGED ? bt_staged : a.blk[blk];  // {first leaf, end leaf, first row, end row}
     const uint32_t l0 = bt.x, nl = bt.y - bt.x, r0 = bt.z, r1 = bt.w;
 
     // Every global load a workgroup needs before its first barrier is issued
@@ -298,8 +343,8 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
     static_assert(kTallyClasses * kClsVec <= kTallyThreads, "one class vector per thread");
     static_assert(kMaxBlkLeaves + 1 <= 2 * kTallyThreads, "two leaf starts per thread");
-    const bool st_cls = tid < nc * kClsVec;
-    const bool st_ls0 = (uint32_t)tid <= nl, st_ls1 = (uint32_t)tid + kTallyThreads <= nl;
+    const bool st_cls = !STAGED && tid < nc * kClsVec;
+    const bool st_ls0 = !STAGED && (uint32_t)tid <= nl, st_ls1 = !STAGED && (uint32_t)tid + kTallyThreads <= nl;
     uint4 cls_v = make_uint4(0, 0, 0, 0);
     uint32_t ls0 = 0, ls1 = 0;
     if (st_cls) cls_v = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
@@ -313,7 +358,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     RowRegs<W, R> cur;
     {
         const uint32_t row = base0 + 4u * tid;
-        load_rows<W, R>(a, row, (row < r1) && (row + 3 >= r0), cur);
+        load_rows<W, R, STAGED>(a, row, (row < r1) && (row + 3 >= r0), cur);
     }
     for (int i = tid; i < nv * la; i += kTallyThreads) s_acc[i] = 0;
     if (st_cls) reinterpret_cast<uint4*>(s_cls)[tid] = cls_v;
@@ -331,7 +376,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         RowRegs<W, R> nxt;
         if (more) {
             const uint32_t nrow = row + kChunkRows;
-            load_rows<W, R>(a, nrow, (nrow < r1) && (nrow + 3 >= r0), nxt);
+            load_rows<W, R, STAGED>(a, nrow, (nrow < r1) && (nrow + 3 >= r0), nxt);
         }
         const auto& lab = cur.lab;
         const auto& tn = cur.tn;
@@ -377,6 +422,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         }
         __syncthreads();
         JSP_STAMP(blk, 6);
+        svc_stamp(clk, 6);
 
         // ---- leaf pass: one thread per leaf folds its rows of this chunk.
         // Chunk prefix at row x = wave-local prefix + the totals of the waves
@@ -405,6 +451,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     }
     __syncthreads();
     JSP_STAMP(blk, 7);
+    svc_stamp(clk, 7);
     if (a.cap_out == nullptr) return;  // the caller keeps the sums in LDS (compaction without tally output)
     for (uint32_t li = tid; li < nl; li += kTallyThreads) {
         const uint32_t leaf = a.leaf_base + l0 + li;
@@ -1664,22 +1711,23 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoc
 // for the feasible leaves before it, scatter its jobs' domains. `sys`: assign[]
 // and stats are in pinned host memory (system-scope stores). s_x: the small
 // LDS words after the tally carve ([2] prefix [3] timeout [4..16] scan).
-template <int W, int R>
-__device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint32_t epoch, uint32_t pods,
+template <int W, int R, bool STAGED = false>
+__device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
-                                             uint32_t* s_x) {
+                                             uint32_t* s_x, uint32_t* clk = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63;
-    tally_block<W, R>(a, tile, lds);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+    tally_block<W, R, STAGED>(a, tile, lds, bt, clk);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     JSP_STAMP(tile, 2);
+    svc_stamp(clk, 2);
 
     const uint32_t* s_acc = lds + tally_acc_off(1);
-    const uint4 bt = a.blk[tile];
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
     const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
     uint32_t total;
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
     JSP_STAMP(tile, 3);
+    svc_stamp(clk, 3);
     if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total);
     if (tid < 64) {  // wave 0: look back
         uint32_t prefix = 0, spins = 0;
@@ -1716,6 +1764,7 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     }
     __syncthreads();
     JSP_STAMP(tile, 4);
+    svc_stamp(clk, 4);
     const uint32_t prefix = s_x[2];
     const bool failed = s_x[3] != 0;
     if (!failed) {
@@ -1747,8 +1796,8 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
     if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
     JSP_STAMP(tile, 0);
     const bool sys = f.done != nullptr;  // host path: assign[] and stats are in pinned host memory
-    compact_tile<W, R>(a, tile, f.epoch, f.pods, f.J, f.n_runs, f.granules, f.spin_limit, f.assign, f.stats, f.err,
-                       sys, lds, s_x);
+    compact_tile<W, R>(a, tile, a.blk[tile], f.epoch, f.pods, f.J, f.n_runs, f.granules, f.spin_limit, f.assign,
+                       f.stats, f.err, sys, lds, s_x);
     if (sys) signal_host(f.done + tile, f.epoch, false);
     JSP_STAMP(tile, 5);
 }
@@ -1762,20 +1811,96 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
 // seq. Every workgroup leaves on kSvcStop or after idle_ticks of the 100 MHz
 // clock without a request, so the grid always drains; a tile whose look-back
 // partner left (the host posted into an exit) times out and reports it.
+// Dispatcher workgroup of the service (the grid's last block): lane 0 of
+// each of its 4 waves polls the host request word, one system-scope load in
+// flight each, the waves a quarter of a host-link round trip apart, so a
+// request is seen ~1/4 round trip after it lands. It rings the device bell
+// (one sc1 8-byte store, tag = seq), which the tiles poll close by. Only this
+// workgroup reads host memory: tiles polling it themselves see a request up
+// to a whole round trip apart and load the link with reads.
+__device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t* s_p) {
+    const uint32_t w = threadIdx.x >> 6;
+    uint32_t seq = v.seq0;
+    if (threadIdx.x == 0) {
+        s_p[0] = 0;
+        s_p[2] = 0;
+        __hip_atomic_store(v.ready, v.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    __syncthreads();
+    unsigned long long* mb = const_cast<unsigned long long*>(v.mailbox);
+    while (true) {
+        if ((threadIdx.x & 63) == 0) {
+            const uint64_t t0 = wall_clock64();
+            while (wall_clock64() - t0 < (uint64_t)w * kSvcStaggerTicks) __builtin_amdgcn_s_sleep(1);
+            while (true) {
+                if (__hip_atomic_load(s_p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 ||
+                    __hip_atomic_load(s_p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
+                    break;
+                const unsigned long long m = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                const uint32_t q = (uint32_t)m;
+                if (q == kSvcStop) {
+                    __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (q != seq && q != 0) {
+                    // ring at once (the first wave to see it; a second ringer writes the same word)
+                    __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+                if (w == 0 && wall_clock64() - t0 > v.idle_ticks) {
+                    __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        const uint32_t q = s_p[0];
+        if (q == 0) {  // stop or idle: every tile leaves too
+            if (threadIdx.x == 0)
+                __hip_atomic_store(v.bell, (unsigned long long)kSvcStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return;
+        }
+        seq = q;
+        // the next request comes only after every tile has answered this one
+        // (the host waits for all done words), so polling may resume at once
+        __syncthreads();
+        if (threadIdx.x == 0) s_p[0] = 0;
+        __syncthreads();
+    }
+}
+
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs a, ServiceArgs v) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* s_x = lds + tally_lds_words(a);  // compact_tile's words, then [16] request seq [17] J
     const uint32_t tile = blockIdx.x;
+    if (tile == a.n_blocks) {
+        service_dispatch(v, s_x + 16);
+        return;
+    }
     uint32_t seq = v.seq0;
+    // the tile's constants, staged once: geometry, class record, leaf starts
+    const uint4 bt = a.blk[tile];
+    {
+        constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
+        const int tid = threadIdx.x;
+        const uint32_t nl = bt.y - bt.x;
+        const int la = (int)a.la;
+        if (tid < kClsVec) reinterpret_cast<uint4*>(lds)[tid] = reinterpret_cast<const uint4*>(a.cls)[tid];
+        uint32_t* s_ls = lds + tally_ls_off(1, 2, la);
+        for (uint32_t i = tid; i <= nl; i += kTallyThreads) s_ls[i] = a.leaf_start[bt.x + i];
+    }
+    __syncthreads();
     while (true) {
         if (threadIdx.x == 0) {
+            // the bell (device memory, sc1 loads: the dispatcher stores it sc1);
+            // a tile also leaves on its own after twice the idle time, in case
+            // the dispatcher never ran
             uint32_t next = 0, J = 0;  // next == 0: leave
-            uint64_t t0 = wall_clock64();
+            const uint64_t t0 = wall_clock64();
             while (true) {
-                const unsigned long long m =
-                    __hip_atomic_load(const_cast<unsigned long long*>(v.mailbox), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_SYSTEM);
+                const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t q = (uint32_t)m;
                 if (q == kSvcStop) break;
                 if (q != seq && q != 0) {
@@ -1783,37 +1908,34 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
                     J = (uint32_t)(m >> 32);
                     break;
                 }
-                const uint64_t t = wall_clock64();
-                if (t - t0 > v.idle_ticks) break;
-                __builtin_amdgcn_s_sleep(2);
+                if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
             }
-            // the snapshot may have been patched since this workgroup's last
-            // request (another launch, other XCDs): drop this CU's stale lines
-            // before any of this request's loads (one lane; the barrier below
-            // holds the other waves until the invalidate has completed)
-            if (next != 0) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
+            if (next != 0 && v.clk)
+                __hip_atomic_store(v.clk + kSvcClkSlots * tile, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
             s_x[16] = next;
             s_x[17] = J;
-            if (next != 0 && v.clk) __hip_atomic_store(v.clk + 2 * tile, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_SYSTEM);
         }
         __syncthreads();
         const uint32_t next = s_x[16], J = s_x[17];
         if (next == 0) return;
+        uint32_t* clk = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
+        svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
-        compact_tile<W, R>(a, tile, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit, v.assign,
-                           v.stats, v.err, true, lds, s_x);
-        if (v.clk) {
+        compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
+                                 v.assign, v.stats, v.err, true, lds, s_x, clk);
+        if (clk) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
-            if (threadIdx.x == 0)
-                __hip_atomic_store(v.clk + 2 * tile + 1, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            svc_stamp(clk, 5);
         }
         signal_host(v.done + tile, next, false);
+        // The host may patch the snapshot before its next request (another
+        // launch): drop this CU's L1 lines now, off the request path -- no
+        // snapshot load happens until the next request, which the host posts
+        // after the patch has finished.
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         seq = next;
         __syncthreads();  // s_x[16..17] and the tally carve are rewritten by the next request
     }
@@ -1940,7 +2062,7 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 
 template <int W, int R>
 static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
-    hipLaunchKernelGGL((place_service_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads), compact_lds_bytes(a.la),
+    hipLaunchKernelGGL((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), compact_lds_bytes(a.la),
                        s, a, v);
     return hipGetLastError();
 }

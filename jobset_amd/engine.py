@@ -215,6 +215,14 @@ class Engine:
         """Stop the resident service now (before a device-wide synchronize)."""
         check(self._lib.jsp_engine_service_stop(self._h))
 
+    def service_clock(self) -> np.ndarray:
+        """The last timed service request's per-tile 100 MHz stamps [tiles, 8]
+        (jsp_engine_service_clock); empty when none is held."""
+        out = np.zeros(256 * 8, dtype=np.uint32)
+        n = ctypes.c_uint32(0)
+        check(self._lib.jsp_engine_service_clock(self._h, _p(out), out.shape[0], ctypes.byref(n)))
+        return out[:n.value * 8].reshape(n.value, 8)
+
     # ---------------------------------------------------------------- webhook / reconciler batches
     def resolve_leader_domains(self, leader_rows: np.ndarray, levels: np.ndarray) -> np.ndarray:
         rows = np.ascontiguousarray(leader_rows, dtype=np.int32)

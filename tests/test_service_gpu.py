@@ -163,3 +163,31 @@ def test_service_timing_stamps(svc_engine):
     assert t.svc_calls == 100
     per = t.svc_us / t.svc_calls
     assert 0.0 < per < float(np.median(walls))
+
+
+def test_service_after_device_path_and_patch(svc_engine):
+    """A device-path placement (caller's stream, other CUs' L1s fill with the
+    old rows), then a patch, then a service request: the service sees the
+    patched rows (its acquire drops stale L1 lines; L2 is coherent)."""
+    import torch
+    p = synth.config2()
+    svc_engine.load(p)
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+    side = torch.cuda.Stream()
+    rng = np.random.default_rng(11)
+    for step in range(40):
+        np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, O.place_c(p)[0])
+        for _ in range(4):
+            svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
+                                    side.cuda_stream)
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=200, replace=False)).astype(np.uint32)
+        free = rng.integers(0, 4000, size=(p.nodes.free.shape[0], 200)).astype(np.uint32)
+        svc_engine.patch_rows(rows, free=free)
+        p.nodes.free[:, rows] = free
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    svc_engine.check()

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Where a resident-service placement's time goes: per host-API
+call, the host wall time beside the service's 100 MHz device stamps (timing
+on): request seen -> acquire -> tallied -> scanned -> looked back -> assign[]
+drained, each phase taken at its slowest tile relative to the first tile that
+saw the request. Diagnostic only."""
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    import torch  # noqa: F401  (one HIP runtime)
+    from jobset_amd import synth
+    from jobset_amd.engine import Engine
+    from jobset_amd.snapshot import job_runs
+    reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
+    eng = Engine(0)
+    for cfg in (1, 2):
+        p = synth.CONFIGS[cfg]()
+        eng.load(p)
+        call = eng.host_placer(*job_runs(p.job_class))
+        for timed in (False, True):
+            eng.set_timing(timed)
+            for _ in range(100):
+                call()
+            walls, phases = [], []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                call()
+                walls.append((time.perf_counter() - t0) * 1e6)
+                if timed:
+                    c = eng.service_clock().astype(np.int64)
+                    ref = c[:, 0].min()
+                    phases.append([(c[:, k].max() - ref) * 10 for k in (0, 1, 6, 7, 2, 3, 4, 5)])
+            w = np.array(walls)
+            line = f"cfg{cfg} timing={'on ' if timed else 'off'}: wall p50 {np.median(w):.2f} us p99 {np.percentile(w, 99):.2f}"
+            if timed:
+                ph = np.median(np.array(phases), axis=0)
+                line += " | device (ns from first tile seeing the request, slowest tile): " + " ".join(
+                    f"{n} {v:.0f}" for n, v in zip(("seen", "bcast", "rowpass", "leafpass", "tally", "scan", "lookback", "drained"), ph))
+            print(line, flush=True)
+        eng.set_timing(False)
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()
