@@ -992,6 +992,50 @@ __device__ void reg_flush(RegState& s, uint32_t K, const TopoDev& topo, uint64_t
     s.pend = -1;
 }
 
+// Scalar chain of a dense word, unrolled: packed lane k (< n) holds the k-th
+// visiting job's class word (bits 0..62); job k takes the lowest bit of it not
+// yet taken, and its lane of `res` gets the bit (-1: none). Lanes >= n hold 0:
+// their s_ff1 gives -1 and the s_bitset1 after it sets bit 63, which no job's
+// word holds (the caller clears it and settles bit 63 itself).
+#define JSP_CHAIN_STEP(K)                                                                                 \
+    do {                                                                                                  \
+        const uint64_t g_ = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh, (K)) << 32) |         \
+                            (uint32_t)__builtin_amdgcn_readlane((int)gl, (K));                            \
+        uint64_t t_;                                                                                      \
+        int32_t b_;                                                                                       \
+        asm("s_andn2_b64 %[t], %[g], %[tk]\n\t"                                                          \
+            "s_ff1_i32_b64 %[b], %[t]\n\t"                                                               \
+            "s_bitset1_b64 %[tk], %[b]"                                                                   \
+            : [tk] "+s"(taken), [t] "=&s"(t_), [b] "=&s"(b_)                                              \
+            : [g] "s"(g_)                                                                                 \
+            : "scc");                                                                                     \
+        asm("v_writelane_b32 %0, %1, %2" : "+v"(res) : "s"(b_), "i"(K));                                  \
+    } while (0)
+#define JSP_CHAIN_8(B)                                                                                    \
+    JSP_CHAIN_STEP((B) + 0); JSP_CHAIN_STEP((B) + 1); JSP_CHAIN_STEP((B) + 2); JSP_CHAIN_STEP((B) + 3);   \
+    JSP_CHAIN_STEP((B) + 4); JSP_CHAIN_STEP((B) + 5); JSP_CHAIN_STEP((B) + 6); JSP_CHAIN_STEP((B) + 7)
+
+__device__ __forceinline__ void chain_unrolled(uint32_t gl, uint32_t gh, uint32_t n, uint64_t& taken, int32_t& res) {
+    JSP_CHAIN_8(0);
+    if (n <= 8) return;
+    JSP_CHAIN_8(8);
+    if (n <= 16) return;
+    JSP_CHAIN_8(16);
+    if (n <= 24) return;
+    JSP_CHAIN_8(24);
+    if (n <= 32) return;
+    JSP_CHAIN_8(32);
+    if (n <= 40) return;
+    JSP_CHAIN_8(40);
+    if (n <= 48) return;
+    JSP_CHAIN_8(48);
+    if (n <= 56) return;
+    JSP_CHAIN_8(56);
+}
+#undef JSP_CHAIN_8
+#undef JSP_CHAIN_STEP
+constexpr uint32_t kChainUnrollMin = 12;  // visiting jobs from which a word takes the unrolled chain
+
 // Runs walk (A7). Requires stage_meta (+ stage_topo when TOPO_LDS) and a
 // barrier first, s_taken zeroed, and `feas` holding every class's bitmap words
 // (LDS or global). Jobs are taken in global order, run by run; a run of class
@@ -1172,8 +1216,30 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     const uint32_t dbg_row = 4020u + (nbatch - 1u) * 4u + (w - (d0 >> 6));  // diag build only
                     (void)dbg_row;
                     if (nbatch <= 4u && w - (d0 >> 6) < 4u) JSP_CLK(dbg_row, 0);
-                    uint64_t V = V0, taken = 0;
+                    uint64_t taken = 0;
                     int32_t wres = -1;
+                    const uint32_t nv = (uint32_t)__popcll(V0);
+                    if (nv >= kChainUnrollMin) {
+                        // Dense word: the visiting jobs' class words are packed into
+                        // lanes 0..nv-1 (job order), then an unrolled chain reads
+                        // them with constant-lane readlanes and writes each result
+                        // into its packed lane: per job two readlanes, and-not,
+                        // lowest-bit, bit-set and one writelane -- half the
+                        // instructions of the loop below, no loop control.
+                        // (the permutes run on every lane: a source lane outside a
+                        // branch's exec mask would read as 0)
+                        const uint32_t src = (uint32_t)lane < nv ? select_bit(V0, (uint32_t)lane) : 0u;
+                        const uint32_t pgl = (uint32_t)__shfl((int)gl, (int)src);
+                        const uint32_t pgh = (uint32_t)__shfl((int)gh62, (int)src);
+                        const uint32_t cgl = (uint32_t)lane < nv ? pgl : 0u;
+                        const uint32_t cgh = (uint32_t)lane < nv ? pgh : 0u;
+                        int32_t cres = -1;
+                        chain_unrolled(cgl, cgh, nv, taken, cres);
+                        const uint32_t pos = mbcnt64(V0);
+                        const int32_t back = __shfl(cres, (int)(pos & 63u));
+                        if ((V0 >> lane) & 1ull) wres = back;
+                    } else {
+                    uint64_t V = V0;
                     // software-pipelined: the next job's class word is read (two
                     // readlanes) before the current job's scalar chain runs. Measured
                     // ~100 shader cycles per job visit (tools/stamps_words.py): about
@@ -1209,6 +1275,7 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                         if ((int32_t)jn < 0) break;
                         j = jn;
                         gc = gn;
+                    }
                     }
                     if (nbatch <= 4u && w - (d0 >> 6) < 4u) {
                         JSP_CLK(dbg_row, 1);
