@@ -51,8 +51,10 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
 SHAPES = {0: "three launches (tally -> feas -> assign + expand)", 1: "fused single launch",
           2: "single-class compaction, one launch",
-          3: "single-class compaction answered by the resident service (no launch per placement)"}
-KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel"}
+          3: "single-class compaction answered by the resident service (no launch per placement)",
+          4: "fused shape answered by the resident service (no launch per placement)"}
+KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel",
+          4: "place_fused_kernel"}
 
 
 def tally_bytes(p) -> int:
@@ -101,7 +103,10 @@ def pmc_traffic(kernel: str, cfg: int):
                 if name.startswith(kernel):
                     vals.append(float(row["Counter_Value"]))
         return sum(vals) / len(vals) if vals else None
-    for d in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+    dirs = []
+    for r in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        dirs += [os.path.join(r, sub) for sub in ("final", "mid", "baseline", "")]  # newest evidence first
+    for d in dirs:
         fp, wp = os.path.join(d, f"pmc_fetch_cfg{cfg}.csv"), os.path.join(d, f"pmc_write_cfg{cfg}.csv")
         if os.path.exists(fp) and os.path.exists(wp):
             fa, wa = avg(fp), avg(wp)
@@ -298,7 +303,7 @@ def main() -> None:
     # the persistent kernel, which HIP events cannot bracket per request: the
     # roofline is the launch-path compaction kernel's, the service's own
     # per-request device time is under "service".
-    if shape in (1, 2, 3):
+    if shape in (1, 2, 3, 4):
         dom_us = event_loop_us(step, args.steps, stream)
         tb = compact_bytes(p) if shape in (2, 3) else tally_bytes(p) + placement_tail_bytes(p)
     else:

@@ -121,7 +121,8 @@ typedef struct jsp_stats {
     uint32_t placed;           /* assign[j] != -1 */
     uint32_t runs;             /* replicated-job runs the assignment walked */
     uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction,
-                                  3 one-class compaction answered by the resident service */
+                                  3 one-class compaction answered by the resident service,
+                                  4 fused shape answered by the resident service */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
@@ -151,10 +152,10 @@ typedef struct jsp_timing {
                                  for one leaf-level class, the fused tail for small snapshots */
 
 /* jsp_engine_set_service modes. With AUTO, a host-API jsp_place of the
- * one-class compaction shape (no tallies requested) is answered by a
- * resident service kernel: one workgroup per tile stays on the GPU, polls a
- * request word in pinned host memory, and writes assign[] back into pinned
- * memory -- no launch per placement. It is started by the first such
+ * one-class compaction shape or of the fused shape (no tallies requested) is
+ * answered by a resident service kernel: one workgroup per tile stays on the
+ * GPU, a dispatcher workgroup polls a request word in pinned host memory, and
+ * assign[] goes back into pinned memory -- no launch per placement. It is started by the first such
  * jsp_place, stopped by every upload, jsp_engine_set_service/set_fused and
  * jsp_engine_destroy, and leaves by itself after JSP_SERVICE_IDLE_MS
  * (default 50 ms) without a request; jsp_place restarts it when needed.

@@ -147,11 +147,14 @@ struct jsp_engine {
     struct Service {
         bool running = false;
         hipStream_t stream = nullptr;
-        HostBuf box;     // [0] request word: (J << 32) | seq
+        HostBuf box;     // request: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; u32 [8] ready
         HostBuf words;   // done[nb] | stats[2] | err[1] | clk[kSvcClkSlots nb]
         HostBuf assign;  // [cap]
-        DevBuf granules;
-        uint32_t cap = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
+        HostBuf runs;    // fused shape: run_class[cap_runs] | run_len[cap_runs]
+        DevBuf granules; // compaction granules | bell | counter | n_runs, one 128-B line each after the granules
+        DevBuf tally;    // fused shape: the service's own cap[C][L] | occ[L] (device-path launches use e->cap)
+        uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
+        int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         std::chrono::steady_clock::time_point last{};
@@ -373,6 +376,45 @@ bool compact_ok(jsp_engine* e) {
            e->leaf_begin == 0 && e->n_leaves == e->L_total;
 }
 
+// Launch arguments of the fused shape (the launch path and the resident
+// service); sets a.sc1_out, the tallies' write-through hand-off to the tail.
+jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_run_class, const uint32_t* d_run_len,
+                          uint32_t n_runs, uint32_t J, int32_t* d_assign, uint32_t* stats) {
+    jsp::FusedArgs f{};
+    f.ticket = e->ticket.as<unsigned long long>();
+    f.tile_base = e->tile_draws;
+    f.done_base = e->done_draws;
+    f.C = e->C;
+    f.topo = e->topo;
+    f.t_off = e->t_off.as<uint32_t>();
+    f.t_words = e->t_off_h[e->K];
+    f.word_off = e->word_off.as<uint32_t>();
+    f.feas_words = e->feas_words;
+    f.run_class = d_run_class;
+    f.run_len = d_run_len;
+    f.n_runs = n_runs;
+    f.J = J;
+    f.assign = d_assign;
+    f.stats = stats;
+    const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
+    f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
+    f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
+    {
+        uint32_t lv[jsp::kMaxClasses];
+        for (uint32_t c = 0; c < e->C; ++c) lv[c] = e->cls_h[c].level;
+        f.fscr_words = jsp::fused_scratch_words(e->K, e->topo.D, lv, e->C);
+        bool upper = false;
+        for (uint32_t c = 0; c < e->C; ++c) upper |= lv[c] + 1 < e->K;
+        // write-through hand-off of the tallies to the tail (no release/acquire
+        // fences) unless the tail's per-wave upper-class path, which reads them
+        // with plain loads, will run
+        a.sc1_out = (!upper || f.fscr_words != 0) && !std::getenv("JSP_FENCED_HANDOFF") ? 1 : 0;
+    }
+    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
+                                       f.topo_in_lds ? topo_words : 0u, f.fscr_words);
+    return f;
+}
+
 // Whole placement on the engine's own tally buffers: one compaction launch for
 // a single leaf-level class, one fused launch when the snapshot is small, else
 // tally -> feas -> assign. `signal`: the single-launch shapes write host
@@ -414,38 +456,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
                            n_runs, J, d_assign, s);
     }
     jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
-    jsp::FusedArgs f{};
-    f.ticket = e->ticket.as<unsigned long long>();
-    f.tile_base = e->tile_draws;
-    f.done_base = e->done_draws;
-    f.C = e->C;
-    f.topo = e->topo;
-    f.t_off = e->t_off.as<uint32_t>();
-    f.t_words = e->t_off_h[e->K];
-    f.word_off = e->word_off.as<uint32_t>();
-    f.feas_words = e->feas_words;
-    f.run_class = d_run_class;
-    f.run_len = d_run_len;
-    f.n_runs = n_runs;
-    f.J = J;
-    f.assign = d_assign;
-    f.stats = stats_ptr(e);
-    const uint32_t topo_words = e->K > 1 ? jsp::topo_table_words(e->K, e->topo.D) : 0u;
-    f.topo_in_lds = topo_words > 0 && topo_words <= jsp::kFusedTopoMax ? 1u : 0u;
-    f.topo_lds_words = f.topo_in_lds ? topo_words : 0u;
-    {
-        uint32_t lv[jsp::kMaxClasses];
-        for (uint32_t c = 0; c < e->C; ++c) lv[c] = e->cls_h[c].level;
-        f.fscr_words = jsp::fused_scratch_words(e->K, e->topo.D, lv, e->C);
-        bool upper = false;
-        for (uint32_t c = 0; c < e->C; ++c) upper |= lv[c] + 1 < e->K;
-        // write-through hand-off of the tallies to the tail (no release/acquire
-        // fences) unless the tail's per-wave upper-class path, which reads them
-        // with plain loads, will run
-        a.sc1_out = (!upper || f.fscr_words != 0) && !std::getenv("JSP_FENCED_HANDOFF") ? 1 : 0;
-    }
-    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
-                                       f.topo_in_lds ? topo_words : 0u, f.fscr_words);
+    jsp::FusedArgs f = fused_args(e, a, d_run_class, d_run_len, n_runs, J, d_assign, stats_ptr(e));
     f.done = signal ? e->h_done.as<uint32_t>() : nullptr;
     f.epoch = e->epoch;
     if (n_signals && signal) *n_signals = 1;
@@ -477,10 +488,17 @@ double svc_idle_ms() {
     return ms;
 }
 
-bool svc_ok(jsp_engine* e) {
-    return e->svc_mode == JSP_SERVICE_AUTO && e->have_topo && e->have_snap && e->have_cls && compact_ok(e) &&
-           e->n_blocks <= kSvcMaxBlocks;
+// The shape the service would run for the engine's current state (2
+// compaction, 1 fused), 0 = none.
+int svc_shape(jsp_engine* e) {
+    if (e->svc_mode != JSP_SERVICE_AUTO || !e->have_topo || !e->have_snap || !e->have_cls ||
+        e->n_blocks > kSvcMaxBlocks)
+        return 0;
+    if (compact_ok(e)) return 2;
+    if (fused_ok(e) && !std::getenv("JSP_SERVICE_NO_FUSED")) return 1;
+    return 0;
 }
+bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
 int svc_stop(jsp_engine* e) {
     auto& v = e->svc;
@@ -499,15 +517,15 @@ int svc_suspend(jsp_engine* e) {
     return svc_stop(e);
 }
 
-int svc_start(jsp_engine* e, uint32_t J);
+int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs);
 void svc_resume(jsp_engine* e) {
     if (e->svc.resume && svc_ok(e)) {
         e->svc.resume = false;
-        (void)svc_start(e, 0);  // a failure here resurfaces at the next jsp_place
+        (void)svc_start(e, 0, 0);  // a failure here resurfaces at the next jsp_place
     }
 }
 
-int svc_start(jsp_engine* e, uint32_t J) {
+int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     auto& v = e->svc;
     if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
     const uint32_t nb = e->n_blocks;
@@ -516,12 +534,18 @@ int svc_start(jsp_engine* e, uint32_t J) {
         HIP_TRY(v.assign.reserve((size_t)cap * 4));
         v.cap = cap;
     }
+    const int shape = svc_shape(e);
+    if (shape == 1 && (n_runs > v.cap_runs || !v.runs.p)) {
+        const uint32_t cr = std::max<uint32_t>(1024, n_runs + n_runs / 2);
+        HIP_TRY(v.runs.reserve((size_t)cr * 8));
+        v.cap_runs = cr;
+    }
     const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * nb + 3;
     HIP_TRY(v.words.reserve(nw * 4));
     std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
     HIP_TRY(v.box.reserve(64));
     const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
-    HIP_TRY(v.granules.reserve(gpad + 128));  // granules, then the bell on a line of its own
+    HIP_TRY(v.granules.reserve(gpad + 3 * 128));  // granules, then bell, counter, n_runs on lines of their own
     // after everything the engine enqueued on any stream (the last stream's
     // event), without making later calls wait for the service
     if (e->have_last) {
@@ -529,23 +553,26 @@ int svc_start(jsp_engine* e, uint32_t J) {
         HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
         HIP_TRY(hipStreamWaitEvent(v.stream, e->ev_switch, 0));
     }
-    HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 128, v.stream));
+    HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
+    __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)v.seq, __ATOMIC_RELEASE);
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
     v.gen = v.gen % 0x7FFFFFFFu + 1u;
-    uint32_t* ready = v.box.as<uint32_t>() + 2;
+    uint32_t* ready = v.box.as<uint32_t>() + 8;
     __atomic_store_n(ready, 0u, __ATOMIC_RELEASE);
     uint32_t* w = v.words.as<uint32_t>();
     jsp::ServiceArgs a{};
     a.mailbox = v.box.as<unsigned long long>();
     a.granules = v.granules.as<unsigned long long>();
     a.bell = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad);
+    a.counter = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128);
+    a.nruns = shape == 1 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 256) : nullptr;
     a.pods = e->cls_h[0].pods;
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();
     a.done = w;
     a.stats = w + nb;
     a.err = w + nb + 2;
-    a.clk = e->timing ? w + nb + 3 : nullptr;
+    a.clk = e->timing && shape == 2 ? w + nb + 3 : nullptr;
     a.spin_limit = e->spin_limit;
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
     a.ready = ready;
@@ -553,7 +580,18 @@ int svc_start(jsp_engine* e, uint32_t J) {
     v.err_ack = 0;
     v.nb = nb;
     v.clk = e->timing;
-    HIP_TRY(jsp::launch_service(tally_args(e, nullptr, nullptr, e->L_total), a, v.stream));
+    v.shape = shape;
+    if (shape == 2) {
+        HIP_TRY(jsp::launch_service(tally_args(e, nullptr, nullptr, e->L_total), a, v.stream));
+    } else {
+        const size_t cl = (size_t)std::max<uint32_t>(e->C, 1) * std::max<uint32_t>(e->L_total, 1);
+        HIP_TRY(v.tally.reserve((cl + std::max<uint32_t>(e->L_total, 1)) * 4));
+        uint32_t* cap = v.tally.as<uint32_t>();
+        jsp::TallyArgs ta = tally_args(e, cap, cap + cl, e->L_total);
+        uint32_t* rc = v.runs.as<uint32_t>();
+        jsp::FusedArgs f = fused_args(e, ta, rc, rc + v.cap_runs, 0, 0, v.assign.as<int32_t>(), w + nb);
+        HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
+    }
     v.running = true;
     e->acc.svc_starts += 1;
     // return once the dispatcher polls: a request posted now is answered
@@ -577,14 +615,15 @@ int svc_start(jsp_engine* e, uint32_t J) {
 int svc_wait(jsp_engine* e, uint32_t seq) {
     auto& v = e->svc;
     const uint32_t* words = v.words.as<uint32_t>();
+    const uint32_t n = v.shape == 1 ? 1u : v.nb;  // fused: the tail's one word
     uint32_t i = 0;
     for (uint64_t spins = 1;; ++spins) {
-        while (i < v.nb && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) ++i;
-        if (i == v.nb) return JSP_OK;
+        while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) ++i;
+        if (i == n) return JSP_OK;
         if ((spins & 255) == 0) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {
-                for (; i < v.nb; ++i)
+                for (; i < n; ++i)
                     if (__atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq) return kSvcGone;
                 return JSP_OK;
             }
@@ -594,21 +633,31 @@ int svc_wait(jsp_engine* e, uint32_t seq) {
 }
 
 // One placement through the service: J jobs of the engine's one class.
-int svc_place(jsp_engine* e, uint32_t J, int32_t* assign_out, uint32_t* placed) {
+int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
+              int32_t* assign_out, uint32_t* placed) {
     auto& v = e->svc;
     const auto now = std::chrono::steady_clock::now();
-    bool restart = !v.running || J > v.cap || v.clk != e->timing || v.nb != e->n_blocks ||
+    const int shape = svc_shape(e);
+    bool restart = !v.running || J > v.cap || v.clk != e->timing || v.nb != e->n_blocks || v.shape != shape ||
+                   (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
     uint32_t seq = 0;
     for (int attempt = 0;; ++attempt) {
         if (restart) {
             if (int rc = svc_stop(e)) return rc;
-            if (int rc = svc_start(e, J)) return rc;
+            if (int rc = svc_start(e, J, n_runs)) return rc;
+        }
+        if (shape == 1 && n_runs > 0) {  // the tail reads the runs from pinned memory
+            std::memcpy(v.runs.as<uint32_t>(), run_class, (size_t)n_runs * 4);
+            std::memcpy(v.runs.as<uint32_t>() + v.cap_runs, run_len, (size_t)n_runs * 4);
         }
         seq = v.seq + 1;
         if (seq == 0 || seq == jsp::kSvcStop) seq = 1;
         v.seq = seq;
         v.last = std::chrono::steady_clock::now();
+        // second half first: the dispatcher reads both halves in one 16-byte load
+        __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq,
+                         __ATOMIC_RELEASE);
         __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)J << 32) | seq, __ATOMIC_RELEASE);
         const int rc = svc_wait(e, seq);
         if (rc == kSvcGone && attempt == 0) {
@@ -631,7 +680,7 @@ int svc_place(jsp_engine* e, uint32_t J, int32_t* assign_out, uint32_t* placed) 
     if (J > 0) std::memcpy(assign_out, v.assign.p, (size_t)J * 4);
     *placed = __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
     e->acc.svc_calls += 1;
-    if (v.clk && v.nb > 0) {
+    if (v.clk && v.shape == 2 && v.nb > 0) {
         const uint32_t* clk = w + v.nb + 3;
         const uint32_t ref = clk[0];
         int32_t lo = 0, hi = 0;
@@ -1058,14 +1107,14 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (!want_tally && svc_ok(e)) {
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
-        if (int rc = svc_place(e, J, assign_out, &placed)) return rc;
+        if (int rc = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed)) return rc;
         const auto t2 = std::chrono::steady_clock::now();
-        e->last_shape = 3;
+        e->last_shape = e->svc.shape == 1 ? 4 : 3;
         if (stats) {
             stats->jobs = J;
             stats->runs = n_runs;
             stats->placed = n_runs > 0 ? placed : 0;
-            stats->fused = 3;
+            stats->fused = e->last_shape;
             stats->wall_us = std::chrono::duration<double, std::micro>(t2 - t0).count();
         }
         using us = std::chrono::duration<double, std::micro>;

@@ -127,7 +127,7 @@ struct CompactArgs {
 constexpr uint32_t kSvcStop = 0xFFFFFFFFu;  // request word's low half: every workgroup leaves
 constexpr uint32_t kSvcClkSlots = 8;        // per tile: seen, acquired, tallied, scanned, looked back, drained
 struct ServiceArgs {
-    const unsigned long long* mailbox;  // host-mapped: (J << 32) | seq, seq != 0; written last by the host
+    const unsigned long long* mailbox;  // host-mapped 16 B: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; [1] first
     unsigned long long* granules;       // [n_blocks] the service's own look-back granules (tag = seq)
     unsigned long long* bell;           // device word: the dispatcher's copy of the request word (sc1)
     uint32_t pods;
@@ -141,6 +141,8 @@ struct ServiceArgs {
     unsigned long long idle_ticks;      // 100 MHz ticks without a request before a workgroup leaves
     uint32_t* ready;                    // host-mapped: the dispatcher writes gen once it polls
     uint32_t gen;                       // service launch number
+    uint32_t* nruns;                    // device word: the request's run count (fused shape), or null
+    unsigned long long* counter;        // device: finished tiles over all requests (fused shape)
 };
 
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }
@@ -180,6 +182,7 @@ hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);
+hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
                        uint32_t topo_words, uint32_t fscr_words);

@@ -319,7 +319,7 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 // already in LDS (staged once per service lifetime: they change only with an
 // upload, which restarts the service) and `bt` is the tile's geometry, so the
 // first chunk's row loads are the request's first memory access.
-template <int W, int R, bool STAGED = false>
+template <int W, int R, bool STAGED = false, bool SC1 = STAGED>
 __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds,
                                             uint4 bt_staged = make_uint4(0, 0, 0, 0), uint32_t* clk = nullptr) {
     const int nc = (int)a.nc;
@@ -358,7 +358,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     RowRegs<W, R> cur;
     {
         const uint32_t row = base0 + 4u * tid;
-        load_rows<W, R, STAGED>(a, row, (row < r1) && (row + 3 >= r0), cur);
+        load_rows<W, R, SC1>(a, row, (row < r1) && (row + 3 >= r0), cur);
     }
     for (int i = tid; i < nv * la; i += kTallyThreads) s_acc[i] = 0;
     if (st_cls) reinterpret_cast<uint4*>(s_cls)[tid] = cls_v;
@@ -376,7 +376,7 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         RowRegs<W, R> nxt;
         if (more) {
             const uint32_t nrow = row + kChunkRows;
-            load_rows<W, R, STAGED>(a, nrow, (nrow < r1) && (nrow + 3 >= r0), nxt);
+            load_rows<W, R, SC1>(a, nrow, (nrow < r1) && (nrow + 3 >= r0), nxt);
         }
         const auto& lab = cur.lab;
         const auto& tn = cur.tn;
@@ -1034,7 +1034,7 @@ __device__ __forceinline__ void chain_unrolled(uint32_t gl, uint32_t gh, uint32_
 }
 #undef JSP_CHAIN_8
 #undef JSP_CHAIN_STEP
-constexpr uint32_t kChainUnrollMin = 12;  // visiting jobs from which a word takes the unrolled chain
+constexpr uint32_t kChainUnrollMin = 6;  // visiting jobs from which a word takes the unrolled chain
 
 // Runs walk (A7). Requires stage_meta (+ stage_topo when TOPO_LDS) and a
 // barrier first, s_taken zeroed, and `feas` holding every class's bitmap words
@@ -1196,11 +1196,15 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 // class word, and-not / lowest-bit / or on the word's taken mask, one
                 // select into the job's lane -- so its cost is a dozen instructions of one
                 // wave, whatever the classes' feasibility patterns.
-                for (uint32_t w = d0 >> 6; w < nwl && R != 0ull; ++w) {
+                // class lanes' feasibility word, one word ahead: the next word's
+                // load is in flight while this word's chain runs
+                uint64_t fcur = cl && (d0 >> 6) < nwl ? feas[my_woff + (d0 >> 6)] : 0ull, fnx = 0ull;
+                for (uint32_t w = d0 >> 6; w < nwl && R != 0ull; ++w, fcur = fnx) {
+                    fnx = cl && w + 1 < nwl ? feas[my_woff + w + 1] : 0ull;
                     const uint64_t tw =
                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(rs.T >> 32), (int)(tl + w)) << 32) |
                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rs.T, (int)(tl + w));
-                    const uint64_t g = cl ? feas[my_woff + w] & ~tw : 0ull;  // lane c: class c's free feasible bits
+                    const uint64_t g = cl ? fcur & ~tw : 0ull;  // lane c: class c's free feasible bits
                     // job lane j: its class's word
                     const uint32_t gl = (uint32_t)__shfl((int)(uint32_t)g, (int)cls);
                     const uint32_t gh = (uint32_t)__shfl((int)(uint32_t)(g >> 32), (int)cls);
@@ -1602,34 +1606,11 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
 // counts finished tiles. Both 64-bit counters are zeroed at snapshot upload
 // and the host adds every launch's draws to its bases, so "my tile" =
 // old - tile_base and "last" = old + 1 - done_base == n_blocks.
+// The fused kernel's tail, run by the workgroup whose tile finished last: the
+// feasibility bitmaps of every class into LDS from the tiles' published sums,
+// then the assignment walk; f.done (host path) gets f.epoch at the end.
 template <int W, int R>
-__global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a, FusedArgs f) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* s_flag = lds + tally_lds_words(a);
-    if (threadIdx.x == 0)
-        *s_flag = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
-                             f.tile_base);
-    __syncthreads();
-    const uint32_t tile = *s_flag;
-    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
-    JSP_STAMP(tile, 0);
-    tally_block<W, R>(a, tile, lds);
-
-    // publish. With sc1_out the sums went out write-through, so every storing
-    // wave's wait and the barrier order them before the ticket add (G16 R1: no
-    // release fence); otherwise the agent release writes this XCD's L2 back.
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (!a.sc1_out) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned long long old =
-            __hip_atomic_fetch_add(f.ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = (old + 1 - f.done_base) == a.n_blocks ? 1u : 0u;
-    }
-    __syncthreads();
-    JSP_STAMP(tile, 5);
-    if (*s_flag == 0) return;
+__device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& f, uint32_t* lds) {
     JSP_STAMP(4000u, 1);
     // the tail: small tables first (independent of the other workgroups' sums)
     uint64_t* s_taken = reinterpret_cast<uint64_t*>(lds);
@@ -1757,6 +1738,37 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     JSP_CLK(4090u, 2);
     JSP_STAMP(4090u, 3);
     if (f.done) signal_host(f.done, f.epoch, true);
+}
+
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a, FusedArgs f) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* s_flag = lds + tally_lds_words(a);
+    if (threadIdx.x == 0)
+        *s_flag = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
+                             f.tile_base);
+    __syncthreads();
+    const uint32_t tile = *s_flag;
+    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
+    JSP_STAMP(tile, 0);
+    tally_block<W, R>(a, tile, lds);
+
+    // publish. With sc1_out the sums went out write-through, so every storing
+    // wave's wait and the barrier order them before the ticket add (G16 R1: no
+    // release fence); otherwise the agent release writes this XCD's L2 back.
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!a.sc1_out) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned long long old =
+            __hip_atomic_fetch_add(f.ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = (old + 1 - f.done_base) == a.n_blocks ? 1u : 0u;
+    }
+    __syncthreads();
+    JSP_STAMP(tile, 5);
+    if (*s_flag == 0) return;
+    fused_tail<W, R>(a, f, lds);
 }
 
 // ----------------------------------------------------------------- single-class compaction
@@ -1903,14 +1915,24 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
                 if (__hip_atomic_load(s_p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 ||
                     __hip_atomic_load(s_p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
                     break;
-                const unsigned long long m = __hip_atomic_load(mb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                const uint32_t q = (uint32_t)m;
+                // the 16-byte request {seq, J, seq, n_runs} in one load (the host
+                // writes the second half first; a torn read shows two seqs)
+                uint4 x;
+                asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                             : "=v"(x) : "v"(mb) : "memory");
+                const uint32_t q = x.x;
                 if (q == kSvcStop) {
                     __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
-                if (q != seq && q != 0) {
-                    // ring at once (the first wave to see it; a second ringer writes the same word)
+                if (q != seq && q != 0 && x.z == q) {
+                    const unsigned long long m = ((unsigned long long)x.y << 32) | q;
+                    // n_runs first (the tail reads it after the bell), then ring at
+                    // once (the first wave to see it; a second ringer writes the same words)
+                    if (v.nruns) {
+                        __hip_atomic_store(v.nruns, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    }
                     __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
@@ -2005,6 +2027,71 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         seq = next;
         __syncthreads();  // s_x[16..17] and the tally carve are rewritten by the next request
+    }
+}
+
+// The fused shape kept resident (cfg3, cfg5: several classes or levels, a
+// small snapshot): one workgroup per tally tile + the dispatcher, all with the
+// fused launch's LDS. Per request each tile tallies its leaves (sc1 row
+// loads), publishes its sums as the fused kernel does and adds to a device
+// counter; the tile whose add completes the request's count runs fused_tail
+// (runs, assign[], stats and the done word in pinned host memory).
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(TallyArgs a, FusedArgs f, ServiceArgs v) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t tile = blockIdx.x;
+    if (tile == a.n_blocks) {
+        service_dispatch(v, lds);
+        return;
+    }
+    uint32_t* s_x = lds + tally_lds_words(a);  // [0] request seq [1] J [2] last-arriver flag
+    uint32_t seq = v.seq0;
+    while (true) {
+        if (threadIdx.x == 0) {
+            uint32_t next = 0, J = 0;  // next == 0: leave
+            const uint64_t t0 = wall_clock64();
+            while (true) {
+                const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t q = (uint32_t)m;
+                if (q == kSvcStop) break;
+                if (q != seq && q != 0) {
+                    next = q;
+                    J = (uint32_t)(m >> 32);
+                    break;
+                }
+                if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_x[0] = next;
+            s_x[1] = J;
+        }
+        __syncthreads();
+        const uint32_t next = s_x[0], J = s_x[1];
+        if (next == 0) return;
+        tally_block<W, R, false, true>(a, tile, lds);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            if (!a.sc1_out) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned long long old =
+                __hip_atomic_fetch_add(v.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_x[2] = (old + 1) % a.n_blocks == 0 ? 1u : 0u;  // requests never overlap: the host waits
+        }
+        __syncthreads();
+        if (s_x[2] != 0) {
+            FusedArgs g = f;
+            g.J = J;
+            g.n_runs = __hip_atomic_load(v.nruns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            g.epoch = next;
+            g.done = v.done;
+            fused_tail<W, R>(a, g, lds);
+        }
+        // drop this CU's L1 lines before the next request (patches come from
+        // other launches), off the request path
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        seq = next;
+        __syncthreads();  // s_x and the tally carve are rewritten by the next request
     }
 }
 
@@ -2136,6 +2223,18 @@ static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hi
 
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
     JSP_DISPATCH_WR(launch_service_wr, a, v, s)
+}
+
+template <int W, int R>
+static hipError_t launch_fused_service_wr(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v,
+                                          hipStream_t s) {
+    hipLaunchKernelGGL((place_fused_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), f.lds_bytes,
+                       s, a, f, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_fused_service_wr, a, f, v, s)
 }
 
 size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }

@@ -33,7 +33,7 @@ class PlaceResult:
     placed: int
     runs: int
     wall_us: float
-    fused: int = 0               # launch shape: 0 three launches, 1 fused tail, 2 one-class compaction
+    fused: int = 0               # launch shape: 0 three launches, 1 fused tail, 2 one-class compaction, 3/4 the resident service (compaction / fused)
 
 
 class Engine:

@@ -191,3 +191,64 @@ def test_service_after_device_path_and_patch(svc_engine):
         assert got.fused == 3
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
     svc_engine.check()
+
+
+# ---------------------------------------------------------------- fused shape (cfg3, cfg5)
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_fused_service_configs(svc_engine, cfg):
+    """The fused shape resident: several classes / levels, runs through pinned
+    memory, the tail on the tile that finished last; 100 requests each."""
+    p = synth.CONFIGS[cfg]()
+    svc_engine.load(p)
+    a = O.place_c(p)[0]
+    call = svc_engine.host_placer(*job_runs(p.job_class))
+    for _ in range(100):
+        st = call()
+        assert st.fused == 4
+        np.testing.assert_array_equal(call.assign, a)
+        assert st.placed == int((a >= 0).sum())
+    rc, rl = job_runs(p.job_class)
+    assert st.runs == rc.shape[0]
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_fused_service_random_parity(svc_engine, seed):
+    """Ragged random snapshots in their own shape (the fused service when the
+    snapshot is small enough), the job order changing between requests."""
+    p = synth.random_problem(seed)
+    svc_engine.load(p)
+    a = O.place_c(p)[0]
+    for _ in range(3):
+        got = svc_engine.place(p.job_class)
+        np.testing.assert_array_equal(got.assign, a)
+    rng = np.random.default_rng(seed)
+    q = dataclasses.replace(p, job_class=rng.permutation(p.job_class))
+    got = svc_engine.place(q.job_class)
+    np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
+    ref = svc_engine.place(p.job_class, want_tally=True)  # launch path (tallies requested)
+    np.testing.assert_array_equal(ref.assign, a)
+
+
+def test_fused_service_patch_and_device_path(svc_engine):
+    """cfg5 resident while device-path launches (their own tally buffers) and
+    patches interleave with its requests."""
+    import torch
+    p = synth.config5()
+    svc_engine.load(p)
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+    side = torch.cuda.Stream()
+    rng = np.random.default_rng(5)
+    for step in range(20):
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 4
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+        svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
+                                side.cuda_stream)
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=64, replace=False)).astype(np.uint32)
+        taints = (rng.integers(0, 2, size=64) << rng.integers(0, 4, size=64)).astype(np.uint32)
+        svc_engine.patch_rows(rows, taints=taints)
+        p.nodes.taints[rows] = taints
+    svc_engine.check()
