@@ -233,6 +233,14 @@ __device__ __forceinline__ uint4 load16_sc1(const void* base, uint32_t off) {
     return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
 }
 
+// The same with a bound: bytes at offsets >= n_bytes read as 0 (the
+// descriptor's range check, per dword).
+__device__ __forceinline__ uint4 load16_sc1_n(const void* base, uint32_t off, uint32_t n_bytes) {
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0,
+                                                                       (int)n_bytes, 0x00020000);
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
 template <int W, int R, bool SC1 = false>
 __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool any, RowRegs<W, R>& x) {
     if (SC1 && any) {
@@ -1525,20 +1533,37 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
         }
     }
     JSP_STAMP(4008u, 3);
-    for (uint32_t q = threadIdx.x; q * 4u < L; q += kTallyThreads) {
+    // wave-uniform trip count (lanes past L run with masked values): the
+    // leaf-level classes' words are formed by a DPP OR across each 16-lane row
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t qb = threadIdx.x - lane; qb * 4u < L; qb += kTallyThreads) {
+        const uint32_t q = qb + lane;
         const uint32_t l0 = q * 4u;
         // every load at a clamped index (classes past npc repeat the last one,
         // leaves past L the last leaf) and masked afterwards: straight-line
         // code, so all of them are in flight before the first wait
-        uint32_t ix[4], ov[4], cv[NG][4];
+        // one 16-B sc1 buffer load per row and thread (its 4 leaves; rows
+        // need not be 16-B aligned), bounded by the row's end
+        uint32_t ov[4], cv[NG][4];
+        if (l0 + 4u <= L) {
+            const uint4 o4 = load16_sc1_n(t.occ, l0 * 4u, L * 4u);
+            ov[0] = o4.x; ov[1] = o4.y; ov[2] = o4.z; ov[3] = o4.w;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ix[i] = l0 + i < L ? l0 + i : L - 1;
+            for (int u = 0; u < NG; ++u) {
+                const uint4 c4 = load16_sc1_n(crow[u], l0 * 4u, L * 4u);
+                cv[u][0] = c4.x; cv[u][1] = c4.y; cv[u][2] = c4.z; cv[u][3] = c4.w;
+            }
+        } else {  // the last, partial chunk (and lanes past L): clamped dword loads
+            uint32_t ix[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ov[i] = load_handoff(t.occ + ix[i]);
+            for (int i = 0; i < 4; ++i) ix[i] = l0 + i < L ? l0 + i : L - 1;
 #pragma unroll
-        for (int u = 0; u < NG; ++u)
+            for (int i = 0; i < 4; ++i) ov[i] = load_handoff(t.occ + ix[i]);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) cv[u][i] = load_handoff(crow[u] + ix[i]);
+            for (int u = 0; u < NG; ++u)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) cv[u][i] = load_handoff(crow[u] + ix[i]);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const bool in = l0 + i < L;
@@ -1563,26 +1588,43 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
             }
         }
         JSP_STAMP(4008u, 2);
+        uint32_t dl[4] = {0u, 0u, 0u, 0u}, dl_lvl = 0xFFFFFFFFu;  // wave-uniform level of dl
 #pragma unroll
         for (int u = 0; u < NG; ++u) {
             if ((uint32_t)u >= npc) continue;
             const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)t.c_pods, (int)cid[u]);
             if ((t.leaf_cls >> cid[u]) & 1ull) {
+                // a 16-lane row covers one 64-leaf word: OR the lanes' nibbles
+                // across the row (DPP row_shr 1/2/4/8), its last lane stores it
                 const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)t.c_beg, (int)cid[u]);
-                uint64_t bits = 0;
+                uint32_t nib = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) bits |= (cv[u][i] >= pods && ov[i] == 0u) ? (1ull << i) : 0ull;
-                if (bits) atomicOr(reinterpret_cast<unsigned long long*>(&t.s_feas[wo + (l0 >> 6)]),
-                                   (unsigned long long)(bits << (l0 & 63u)));
+                for (int i = 0; i < 4; ++i) nib |= (cv[u][i] >= pods && ov[i] == 0u) ? (1u << i) : 0u;
+                const uint32_t sh = 4u * (lane & 7u);
+                uint32_t lo = (lane & 8u) ? 0u : nib << sh, hi = (lane & 8u) ? nib << sh : 0u;
+                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x111, 0xf, 0xf, true);  // row_shr:1
+                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x111, 0xf, 0xf, true);
+                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x112, 0xf, 0xf, true);  // row_shr:2
+                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x112, 0xf, 0xf, true);
+                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x114, 0xf, 0xf, true);  // row_shr:4
+                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x114, 0xf, 0xf, true);
+                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x118, 0xf, 0xf, true);  // row_shr:8
+                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x118, 0xf, 0xf, true);
+                if ((lane & 15u) == 15u && (l0 & ~63u) < L) t.s_feas[wo + (l0 >> 6)] = ((uint64_t)hi << 32) | lo;
             } else {
                 const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)t.c_lvl, (int)cid[u]);
                 uint64_t* sum = t.s_usum + (uint32_t)__builtin_amdgcn_readlane((int)t.c_uoff, (int)cid[u]);
-                uint32_t dcur = tail_up_dom(t, l0, lvl);
+                if (lvl != dl_lvl) {  // the 4 leaves' domains at this level, shared by its classes
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) dl[i] = l0 + i < L ? tail_up_dom(t, l0 + i, lvl) : 0u;
+                    dl_lvl = lvl;
+                }
+                uint32_t dcur = dl[0];  // lanes past L add nothing (the loop below stops at once)
                 uint64_t acc = 0;
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     if (l0 + i >= L) break;
-                    const uint32_t d = i == 0 ? dcur : tail_up_dom(t, l0 + i, lvl);
+                    const uint32_t d = dl[i];
                     if (d != dcur) {
                         if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(&sum[dcur]), (unsigned long long)acc);
                         acc = 0;

@@ -252,3 +252,26 @@ def test_fused_service_patch_and_device_path(svc_engine):
         svc_engine.patch_rows(rows, taints=taints)
         p.nodes.taints[rows] = taints
     svc_engine.check()
+
+
+def test_two_engines_with_services(svc_engine):
+    """Two engines on one GPU, each with its own resident service (compaction
+    on one, fused on the other), requests interleaved; destroying one while
+    its service runs leaves the other answering."""
+    from jobset_amd.engine import Engine
+    p2, q5 = synth.config2(), synth.config5()
+    a2, a5 = O.place_c(p2)[0], O.place_c(q5)[0]
+    svc_engine.load(p2)
+    e2 = Engine(0)
+    try:
+        e2.load(q5)
+        for _ in range(50):
+            g2 = svc_engine.place(p2.job_class)
+            g5 = e2.place(q5.job_class)
+            assert g2.fused == 3 and g5.fused == 4
+            np.testing.assert_array_equal(g2.assign, a2)
+            np.testing.assert_array_equal(g5.assign, a5)
+    finally:
+        e2.close()  # its service is running: destroy stops it
+    for _ in range(10):
+        np.testing.assert_array_equal(svc_engine.place(p2.job_class).assign, a2)
