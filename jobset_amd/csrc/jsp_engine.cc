@@ -110,6 +110,7 @@ struct jsp_engine {
     uint32_t blk_leaves = 4;  // most leaves any tally workgroup owns, rounded up to 4 (LDS tally stride)
     DevBuf labels, taints, freer, excl, leaf_start, blk;
     uint32_t n_blocks = 0;
+    uint32_t fast_res = 0;  // bit r: every free[r] < 2^31 (upload: computed; patches only clear bits)
     uint32_t epoch = 0;  // compaction launches so far (granule tags)
 
     // classes
@@ -324,6 +325,7 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
     a.c0 = 0;
     a.nc = std::min<uint32_t>(e->C, jsp::kTallyClasses);
     a.do_occ = 1;
+    a.fast_res = std::getenv("JSP_NO_FAST_DIV") ? 0u : e->fast_res;
     return a;
 }
 
@@ -727,6 +729,26 @@ void divisor_magic(uint32_t d, uint32_t* magic, uint32_t* shift) {
     *shift = L;
 }
 
+// The 2-op form for dividends below 2^31: floor(n / d) = mulhi(n, m) >> s.
+// d = 2^L: m = 2^31, s = L - 1. Otherwise, with L = floor(log2 d) and
+// l = L + 1 = ceil(log2 d): m = ceil(2^(31+l) / d) < 2^32, s = L; the error
+// e = m d - 2^(31+l) < d adds less than n e / (d 2^(31+l)) < 2^-l <= 1/d to
+// n / d for n < 2^31, which never crosses an integer.
+void divisor_magic31(uint32_t d, uint32_t* magic, uint32_t* shift) {
+    *magic = 0;
+    *shift = 0;
+    if (d <= 1) return;  // identity / not requested: the kernel never takes this form
+    const uint32_t L = 31 - (uint32_t)__builtin_clz(d);
+    if ((d & (d - 1)) == 0) {
+        *magic = 1u << 31;
+        *shift = L - 1;
+        return;
+    }
+    const uint64_t num = 1ull << (32 + L);
+    *magic = (uint32_t)((num + d - 1) / d);
+    *shift = L;
+}
+
 int ready(jsp_engine* e, bool need_cls) {
     if (!e->have_topo) return set_err(JSP_ESTATE, "no topology uploaded");
     if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
@@ -953,6 +975,12 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     e->npad = npad;
     e->W = W;
     e->R = R;
+    e->fast_res = 0;
+    for (uint32_t r = 0; r < R; ++r) {
+        bool small = true;
+        for (uint32_t i = 0; i < N && small; ++i) small = nd->free_res[(size_t)r * N + i] < (1u << 31);
+        if (small) e->fast_res |= 1u << r;
+    }
     e->leaf_begin = nd->leaf_begin;
     e->n_leaves = NL;
     e->max_leaf_rows = max_rows;
@@ -986,6 +1014,15 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
+    if (free_res) {  // a patched value >= 2^31 turns the 2-op division off for its resource
+        const uint32_t before = e->fast_res;
+        for (uint32_t r = 0; r < e->R; ++r)
+            for (uint32_t i = 0; i < n; ++i)
+                if (free_res[(size_t)r * n + i] >= (1u << 31)) e->fast_res &= ~(1u << r);
+        if (e->fast_res != before) {  // the resident service holds the old flags: restart it
+            if (int rc = svc_suspend(e)) return rc;
+        }
+    }
     hipStream_t s = e->stream;
     if (int rc = enter_stream(e, s)) return rc;
     HIP_TRY(upload(e->tmp_a, rows, n, s));
@@ -999,6 +1036,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
                               excl_owner ? e->tmp_e.as<int32_t>() : nullptr, e->labels.as<uint64_t>(),
                               e->taints.as<uint32_t>(), e->freer.as<uint32_t>(), e->excl.as<int32_t>(), s));
     HIP_TRY(hipStreamSynchronize(s));
+    svc_resume(e);
     return JSP_OK;
 }
 
@@ -1031,6 +1069,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
         for (int r = 0; r < 4; ++r) {
             d.res[r] = x.req_res[r];
             divisor_magic(x.req_res[r], &d.magic[r], &d.shift[r]);
+            divisor_magic31(x.req_res[r], &d.magic31[r], &d.shift31[r]);
         }
         woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
     }

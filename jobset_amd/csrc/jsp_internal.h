@@ -32,6 +32,8 @@ struct alignas(16) DevClass {
     uint32_t res[4];      // per-pod request, 0 = none
     uint32_t magic[4];    // floor(n / res) = (((n - mulhi(n, magic)) >> 1) + mulhi(n, magic)) >> shift
     uint32_t shift[4];    // kDivIdentity marks res == 1
+    uint32_t magic31[4];  // floor(n / res) = mulhi(n, magic31) >> shift31, exact for n < 2^31
+    uint32_t shift31[4];  //   (TallyArgs::fast_res: every free value of the resource is below 2^31)
 };
 constexpr uint32_t kDivIdentity = 0xFFFFFFFFu;
 
@@ -71,6 +73,7 @@ struct TallyArgs {
     uint32_t ld, leaf_base;
     int W, R;
     int sc1_out;                // write cap/occ write-through (sc1): the fused kernel's hand-off to its tail
+    uint32_t fast_res;          // bit r: every free[r] of the snapshot < 2^31 (the 2-op division applies)
 };
 
 // Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks

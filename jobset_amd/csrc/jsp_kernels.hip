@@ -296,7 +296,7 @@ __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool
 template <int W, int R>
 struct ClassRegs {
     uint64_t req[W], mask[W];
-    uint32_t tol_inv, pods, res[R], magic[R], shift[R];
+    uint32_t tol_inv, pods, res[R], magic[R], shift[R], magic31[R], shift31[R];
 };
 
 __device__ __forceinline__ uint32_t to_sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
@@ -319,6 +319,8 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
         k.res[r] = to_sgpr(d.res[r]);
         k.magic[r] = to_sgpr(d.magic[r]);
         k.shift[r] = to_sgpr(d.shift[r]);
+        k.magic31[r] = to_sgpr(d.magic31[r]);
+        k.shift31[r] = to_sgpr(d.shift31[r]);
     }
     return k;
 }
@@ -403,6 +405,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
                     if (k.shift[r] == kDivIdentity) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], fr[r][i]);
+                    } else if ((a.fast_res >> r) & 1u) {  // every free value < 2^31: two ops
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(fr[r][i], k.magic31[r]) >> k.shift31[r]);
                     } else {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) {

@@ -250,6 +250,37 @@ def test_exact_division_boundaries(engine):
     np.testing.assert_array_equal(cap, exp)
 
 
+def test_exact_division_fast_path(engine):
+    """Every free value below 2^31: the tally takes the 2-op division
+    (mulhi + shift); it must equal floor(free/req) at the 2^31 edge and for
+    divisors up to 2^32-1 -- and stay exact after a patch brings a value
+    >= 2^31 in (the engine falls back to the 3-step form)."""
+    rng = np.random.default_rng(31)
+    vals = np.concatenate([np.array([0, 1, 2, 3, (1 << 31) - 1, (1 << 31) - 2, 1 << 30, (1 << 24) + 1,
+                                     123456789, 999_999_937, 96_000, 1_024_000], dtype=np.uint64),
+                           rng.integers(0, 1 << 31, size=52, dtype=np.uint64)])
+    reqs = [2, 3, 7, 1000, 1024, 4097, 24_000, 200_000, (1 << 20) + 3, 65521, 1 << 30, (1 << 31) - 1,
+            (1 << 31) + 1, 4_000_000_001, (1 << 32) - 1]
+    N = vals.shape[0]
+    topo = Topology(level_keys=["k"], n_domains=[N], first_leaf=[np.arange(N + 1, dtype=np.uint32)])
+    nodes = Nodes(leaf_start=np.arange(N + 1, dtype=np.uint32), labels=np.zeros((1, N), dtype=np.uint64),
+                  taints=np.zeros(N, dtype=np.uint32), free=vals.astype(np.uint32)[None, :],
+                  excl=np.full(N, -1, dtype=np.int32))
+    classes = [JobClass(pods=1 << 22, req_res=(r,)) for r in reqs]
+    p = Problem(topology=topo, nodes=nodes, classes=classes, job_class=np.zeros(0, dtype=np.uint32))
+    got, a, cap, occ = run_both(engine, p)
+    exp = np.minimum(vals[None, :] // np.array(reqs, dtype=np.uint64)[:, None], 1 << 22).astype(np.uint32)
+    np.testing.assert_array_equal(got.cap, exp)
+    np.testing.assert_array_equal(cap, exp)
+    big = np.array([(1 << 32) - 1, 1 << 31, 3_000_000_001], dtype=np.uint64)
+    rows = np.array([0, 5, 9], dtype=np.uint32)
+    engine.patch_rows(rows, free=big.astype(np.uint32)[None, :])
+    vals[rows] = big
+    got = engine.place(p.job_class, want_tally=True)
+    exp = np.minimum(vals[None, :] // np.array(reqs, dtype=np.uint64)[:, None], 1 << 22).astype(np.uint32)
+    np.testing.assert_array_equal(got.cap, exp)
+
+
 def test_patch_then_place(engine):
     p = synth.config2()
     engine.load(p)
