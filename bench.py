@@ -115,6 +115,31 @@ def pmc_traffic(kernel: str, cfg: int):
     return None
 
 
+def trace_avg_us(kernel: str):
+    """Median duration (µs) of `kernel` in the newest committed rocprofv3
+    kernel-trace summary under profiles/ (this bench run under the profiler),
+    taken at the grid size with the most dispatches (the timed cfg2 loop):
+    the cross-check of the event-timed average, which also counts the gap
+    between back-to-back launches."""
+    for r in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
+        for sub in ("final", "mid", "baseline"):
+            f = os.path.join(r, sub, "summary.txt")
+            if not os.path.exists(f):
+                continue
+            best = None
+            for line in open(f):
+                t = line.split()
+                if not t or not t[0].startswith(kernel) or "median_ns=" not in line:
+                    continue
+                n = int(line.split("n=")[1].split()[0])
+                med = int(line.split("median_ns=")[1].split()[0])
+                if best is None or n > best[0]:
+                    best = (n, med)
+            if best:
+                return round(best[1] / 1e3, 3), os.path.relpath(f, ROOT)
+    return None, None
+
+
 def event_loop_us(fn, k: int, stream) -> float:
     """Average µs per call of `fn` over k back-to-back calls, HIP events on
     the launch stream around the whole loop."""
@@ -313,6 +338,8 @@ def main() -> None:
         tb = tally_bytes(p)
     eng.check()
     achieved = tb / (dom_us * 1e-6) / 1e9
+    # the same kernel's dispatch-only duration from the committed rocprofv3 trace of this bench (cfg2 grid)
+    tr_us, tr_src = trace_avg_us(KERNEL[shape])
     traffic = pmc_traffic(KERNEL[shape], 2)
 
     # ------------------------------------------------ p50/p99 recovery latency (host API, trial snapshots)
@@ -457,6 +484,7 @@ def main() -> None:
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
                          "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
+                         "trace_median_us": tr_us, "trace_source": tr_src,
                          "note": "latency-bound: one launch moving 0.43 MB; see DESIGN.md §8"},
             "service": svc,
             "p50_recovery_us": lat2["p50_us"] if lat2 else None,
