@@ -412,7 +412,17 @@ jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_ru
         // with plain loads, will run
         a.sc1_out = (!upper || f.fscr_words != 0) && !std::getenv("JSP_FENCED_HANDOFF") ? 1 : 0;
     }
-    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, a.nc, a.nc + a.do_occ, a.la,
+    // class groups: a small snapshot's tiles are VALU-bound over many classes;
+    // splitting the classes over up to 4 groups of >= 2 multiplies the tiles
+    // (each row block read once per group), within 128 tiles
+    f.groups = 1;
+    if (e->C > 2 && !std::getenv("JSP_NO_CLASS_GROUPS")) {
+        const uint32_t by_c = std::min<uint32_t>(4, (e->C + 1) / 2);
+        const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
+        f.groups = std::max<uint32_t>(1, std::min(by_c, by_t));
+    }
+    f.cpg = (a.nc + f.groups - 1) / f.groups;
+    f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, f.cpg, f.cpg + a.do_occ, a.la,
                                        f.topo_in_lds ? topo_words : 0u, f.fscr_words);
     return f;
 }
@@ -465,8 +475,8 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     EvPair* p = ev_begin(e, 3, s);
     HIP_TRY(jsp::launch_fused(a, f, s));
     ev_end(p, s);
-    e->tile_draws += e->n_blocks + jsp::kSpareBlocks;
-    e->done_draws += e->n_blocks;
+    e->tile_draws += e->n_blocks * f.groups + jsp::kSpareBlocks;
+    e->done_draws += e->n_blocks * f.groups;
     return JSP_OK;
 }
 

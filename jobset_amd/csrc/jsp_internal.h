@@ -106,7 +106,24 @@ struct FusedArgs {
     uint32_t fscr_words;         // LDS scratch (u64) for upper-level domain sums + occupancy bits, 0 = none
     uint32_t* done;              // host-mapped completion word (host path) or null
     uint32_t epoch;              // value written to *done when the tail has finished
+    uint32_t groups;             // class groups: tile t tallies row block t / groups, classes of group t % groups
+    uint32_t cpg;                // classes per group (group 0 also counts occupancy)
 };
+
+// A fused tile's share: row block and class range.
+struct FusedTile {
+    uint32_t blk, c0, nc;
+    int do_occ;
+};
+__host__ __device__ inline FusedTile fused_tile(uint32_t t, uint32_t groups, uint32_t cpg, uint32_t C) {
+    FusedTile x;
+    x.blk = t / groups;
+    const uint32_t g = t % groups;
+    x.c0 = g * cpg;
+    x.nc = C > x.c0 ? (C - x.c0 < cpg ? C - x.c0 : cpg) : 0u;
+    x.do_occ = g == 0 ? 1 : 0;
+    return x;
+}
 
 // Single-class leaf-level placement as one compaction pass (decoupled look-back).
 struct CompactArgs {

@@ -1787,18 +1787,32 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
     if (f.done) signal_host(f.done, f.epoch, true);
 }
 
+// Small words after a fused tile's tally carve (sized for class group 0).
+__device__ __forceinline__ uint32_t* fused_flags(uint32_t* lds, const TallyArgs& a, const FusedArgs& f) {
+    return lds + tally_lds_words((int)f.cpg, (int)f.cpg + 1, (int)a.la);
+}
+
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a, FusedArgs f) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    uint32_t* s_flag = lds + tally_lds_words(a);
+    uint32_t* s_flag = fused_flags(lds, a, f);
     if (threadIdx.x == 0)
         *s_flag = (uint32_t)(__hip_atomic_fetch_add(f.ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) -
                              f.tile_base);
     __syncthreads();
     const uint32_t tile = *s_flag;
-    if (tile >= a.n_blocks) return;  // a spare workgroup: every tile is taken
+    const uint32_t n_tiles = a.n_blocks * f.groups;
+    if (tile >= n_tiles) return;  // a spare workgroup: every tile is taken
     JSP_STAMP(tile, 0);
-    tally_block<W, R>(a, tile, lds);
+    {
+        // this tile's row block and class group (the LDS carve is sized for group 0)
+        const FusedTile ft = fused_tile(tile, f.groups, f.cpg, f.C);
+        TallyArgs ag = a;
+        ag.c0 = ft.c0;
+        ag.nc = ft.nc;
+        ag.do_occ = ft.do_occ;
+        tally_block<W, R>(ag, ft.blk, lds);
+    }
 
     // publish. With sc1_out the sums went out write-through, so every storing
     // wave's wait and the barrier order them before the ticket add (G16 R1: no
@@ -1810,7 +1824,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned long long old =
             __hip_atomic_fetch_add(f.ticket + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = (old + 1 - f.done_base) == a.n_blocks ? 1u : 0u;
+        *s_flag = (old + 1 - f.done_base) == n_tiles ? 1u : 0u;
     }
     __syncthreads();
     JSP_STAMP(tile, 5);
@@ -2087,11 +2101,17 @@ template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(TallyArgs a, FusedArgs f, ServiceArgs v) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     const uint32_t tile = blockIdx.x;
-    if (tile == a.n_blocks) {
+    const uint32_t n_tiles = a.n_blocks * f.groups;
+    if (tile == n_tiles) {
         service_dispatch(v, lds);
         return;
     }
-    uint32_t* s_x = lds + tally_lds_words(a);  // [0] request seq [1] J [2] last-arriver flag
+    uint32_t* s_x = fused_flags(lds, a, f);  // [0] request seq [1] J [2] last-arriver flag
+    const FusedTile ft = fused_tile(tile, f.groups, f.cpg, f.C);
+    TallyArgs ag = a;
+    ag.c0 = ft.c0;
+    ag.nc = ft.nc;
+    ag.do_occ = ft.do_occ;
     uint32_t seq = v.seq0;
     while (true) {
         if (threadIdx.x == 0) {
@@ -2115,7 +2135,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
         __syncthreads();
         const uint32_t next = s_x[0], J = s_x[1];
         if (next == 0) return;
-        tally_block<W, R, false, true>(a, tile, lds);
+        tally_block<W, R, false, true>(ag, ft.blk, lds);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -2123,7 +2143,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned long long old =
                 __hip_atomic_fetch_add(v.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_x[2] = (old + 1) % a.n_blocks == 0 ? 1u : 0u;  // requests never overlap: the host waits
+            s_x[2] = (old + 1) % n_tiles == 0 ? 1u : 0u;  // requests never overlap: the host waits
         }
         __syncthreads();
         if (s_x[2] != 0) {
@@ -2217,7 +2237,7 @@ static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
 
 template <int W, int R>
 static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
+    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks * f.groups + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
                        s, a, f);
     return hipGetLastError();
 }
@@ -2275,7 +2295,7 @@ hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t 
 template <int W, int R>
 static hipError_t launch_fused_service_wr(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v,
                                           hipStream_t s) {
-    hipLaunchKernelGGL((place_fused_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), f.lds_bytes,
+    hipLaunchKernelGGL((place_fused_service_kernel<W, R>), dim3(a.n_blocks * f.groups + 1), dim3(kTallyThreads), f.lds_bytes,
                        s, a, f, v);
     return hipGetLastError();
 }
