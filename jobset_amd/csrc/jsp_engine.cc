@@ -422,6 +422,7 @@ jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_ru
         f.groups = std::max<uint32_t>(1, std::min(by_c, by_t));
     }
     f.cpg = (a.nc + f.groups - 1) / f.groups;
+    f.pipe = jsp::pipe_walk_enabled() ? 1u : 0u;
     f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, f.cpg, f.cpg + a.do_occ, a.la,
                                        f.topo_in_lds ? topo_words : 0u, f.fscr_words);
     return f;

@@ -108,7 +108,9 @@ struct FusedArgs {
     uint32_t epoch;              // value written to *done when the tail has finished
     uint32_t groups;             // class groups: tile t tallies row block t / groups, classes of group t % groups
     uint32_t cpg;                // classes per group (group 0 also counts occupancy)
+    uint32_t pipe;               // pipelined batch walk allowed
 };
+bool pipe_walk_enabled();
 
 // A fused tile's share: row block and class range.
 struct FusedTile {

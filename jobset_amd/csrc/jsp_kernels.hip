@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+
 #include "jsp_internal.h"
 
 namespace jsp {
@@ -1047,7 +1049,100 @@ __device__ __forceinline__ void chain_unrolled(uint32_t gl, uint32_t gh, uint32_
 }
 #undef JSP_CHAIN_8
 #undef JSP_CHAIN_STEP
-constexpr uint32_t kChainUnrollMin = 6;  // visiting jobs from which a word takes the unrolled chain
+constexpr uint32_t kChainUnrollMin = 6;
+constexpr uint32_t kPipeWaves = 4;                 // waves of the pipelined batch walk
+constexpr uint32_t kPipeSpinLimit = 1u << 24;      // bounded wait on an earlier batch's progress  // visiting jobs from which a word takes the unrolled chain
+
+// One word of a batch (wave-wide): lane c holds class c's free feasible bits
+// `g` of word w; the batch's jobs still without a domain (R; lane j = job j of
+// class `cls`) take, in job order, the lowest free bit of their class's word.
+// Job lanes that took one get res = 64 w + bit and leave R; returns the bits
+// taken.
+__device__ __forceinline__ uint64_t walk_word(uint64_t g, uint32_t cls, bool job, uint64_t& R, int32_t& res, uint32_t w,
+                                              int lane) {
+    // job lane j: its class's word
+    const uint32_t gl = (uint32_t)__shfl((int)(uint32_t)g, (int)cls);
+    const uint32_t gh = (uint32_t)__shfl((int)(uint32_t)(g >> 32), (int)cls);
+    const uint64_t gj = ((uint64_t)gh << 32) | gl;
+    const uint64_t V0 = R & __ballot(job && gj != 0ull);  // jobs that can take something here
+    if (V0 == 0ull) return 0ull;
+    // The chain runs on bits 0..62: s_ff1 of an empty word is -1, and the
+    // s_bitset1 that follows then sets bit 63, which the chain never reads.
+    // Bit 63 goes afterwards to the first visited job left without a domain
+    // whose class has it (job order inside the word: it is the word's last
+    // domain, so only jobs that found nothing below it can want it).
+    const uint32_t gh62 = gh & 0x7FFFFFFFu;
+    uint64_t taken = 0;
+    int32_t wres = -1;
+    const uint32_t nv = (uint32_t)__popcll(V0);
+    if (nv >= kChainUnrollMin) {
+        // Dense word: the visiting jobs' class words are packed into
+        // lanes 0..nv-1 (job order), then an unrolled chain reads
+        // them with constant-lane readlanes and writes each result
+        // into its packed lane: per job two readlanes, and-not,
+        // lowest-bit, bit-set and one writelane -- half the
+        // instructions of the loop below, no loop control.
+        // (the permutes run on every lane: a source lane outside a
+        // branch's exec mask would read as 0)
+        const uint32_t src = (uint32_t)lane < nv ? select_bit(V0, (uint32_t)lane) : 0u;
+        const uint32_t pgl = (uint32_t)__shfl((int)gl, (int)src);
+        const uint32_t pgh = (uint32_t)__shfl((int)gh62, (int)src);
+        const uint32_t cgl = (uint32_t)lane < nv ? pgl : 0u;
+        const uint32_t cgh = (uint32_t)lane < nv ? pgh : 0u;
+        int32_t cres = -1;
+        chain_unrolled(cgl, cgh, nv, taken, cres);
+        const uint32_t pos = mbcnt64(V0);
+        const int32_t back = __shfl(cres, (int)(pos & 63u));
+        if ((V0 >> lane) & 1ull) wres = back;
+    } else {
+    uint64_t V = V0;
+    // software-pipelined: the next job's class word is read (two
+    // readlanes) before the current job's scalar chain runs. Measured
+    // ~100 shader cycles per job visit (tools/stamps_words.py): about
+    // 7 per instruction of the 14-instruction loop on one wave; a
+    // two-job unroll compiled to the same count per job.
+    uint32_t j;  // current job: lowest bit of V, cleared
+    asm("s_ff1_i32_b64 %[j], %[V]\n\t"
+        "s_bitset0_b64 %[V], %[j]"
+        : [V] "+s"(V), [j] "=&s"(j));
+    uint64_t gc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)j) << 32) |
+                  (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)j);
+    while (true) {
+        uint32_t jn;  // next job (-1: none; V stays 0)
+        asm("s_ff1_i32_b64 %[j], %[V]\n\t"
+            "s_bitset0_b64 %[V], %[j]"
+            : [V] "+s"(V), [j] "=&s"(jn));
+        const uint64_t gn =
+            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)(jn & 63u)) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)(jn & 63u));
+        uint64_t t;
+        int32_t bpos;
+        // taken |= lowest bit of (gc & ~taken); job j's lane gets its
+        // position (-1: none). SALU only, plus one writelane whose lane
+        // select (m0) a SALU move wrote three instructions earlier.
+        asm("s_mov_b32 m0, %[j]\n\t"
+            "s_andn2_b64 %[t], %[g], %[tk]\n\t"
+            "s_ff1_i32_b64 %[b], %[t]\n\t"
+            "s_bitset1_b64 %[tk], %[b]\n\t"
+            "v_writelane_b32 %[w], %[b], m0"
+            : [tk] "+s"(taken), [w] "+v"(wres), [t] "=&s"(t), [b] "=&s"(bpos)
+            : [g] "s"(gc), [j] "s"(j)
+            : "m0", "scc");  // s_andn2 sets SCC
+        if ((int32_t)jn < 0) break;
+        j = jn;
+        gc = gn;
+    }
+    }
+    taken &= ~(1ull << 63);
+    const uint64_t m63 = __ballot(((V0 >> lane) & 1ull) && wres < 0 && (gh >> 31) != 0u);
+    if (m63 != 0ull) {
+        if ((uint32_t)lane == (uint32_t)__builtin_ctzll(m63)) wres = 63;
+        taken |= 1ull << 63;
+    }
+    if (wres >= 0) res = (int32_t)(w * 64u + (uint32_t)wres);
+    R &= ~__ballot(wres >= 0);
+    return taken;
+}
 
 // Runs walk (A7). Requires stage_meta (+ stage_topo when TOPO_LDS) and a
 // barrier first, s_taken zeroed, and `feas` holding every class's bitmap words
@@ -1061,9 +1156,11 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
                              uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
                              uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs,
-                             uint32_t* __restrict__ rec_count) {
+                             uint32_t* __restrict__ rec_count, uint32_t pipe_allowed) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t K = topo.K;
+    // the pipelined walk keeps its batch table and progress words in the stage
+    const bool pipe_ok = pipe_allowed != 0 && NT >= 64 * (int)kPipeWaves && stage_cap >= 4u * NT + 2u * kPipeWaves + 8u;
     // wave 0: class state in registers, lane c = class c (C <= kMaxClasses = 64)
     uint32_t my_cur = 0, my_lvl = 0, my_woff = 0, my_D = 0, my_toff = 0;
     if (wid == 0 && (uint32_t)lane < C) {
@@ -1112,7 +1209,164 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
         if (is_long) m.s_long[lrank] = (uint32_t)tid;
         __syncthreads();
         const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
-        if (wid == 0 && regmode) {
+        // Pipelined batches (a tile of short leaf-level runs, no long run): batch
+        // b runs on wave b % kPipeWaves and may take word w as soon as every
+        // earlier batch has passed w (words go in increasing order), so a
+        // batch's sparse words and setup overlap the previous batch's dense word.
+        bool pipe = false;
+        if (regmode && pipe_ok) {
+            const bool ok_run = ri >= n_runs || len == 0 ||
+                                (rc < C && len <= kWaveRunMax && (((dead >> rc) & 1ull) || m.s_lvl[rc] + 1 == K));
+            uint32_t n_bad;  // block count of runs outside the pipelined form (no static LDS of __syncthreads_and)
+            (void)block_excl_scan<NT>(ok_run ? 0u : 1u, m.s_w, &n_bad);
+            pipe = n_bad == 0 && n_long == 0;
+        }
+        if (pipe) {
+            uint32_t* s_desc = s_stage;  // [4 per batch] {first run, runs, first job, jobs}
+            unsigned long long* s_prog = reinterpret_cast<unsigned long long*>(
+                (reinterpret_cast<uintptr_t>(s_stage + 4 * NT) + 7) & ~static_cast<uintptr_t>(7));
+            uint32_t* s_pcnt = reinterpret_cast<uint32_t*>(s_prog + kPipeWaves);
+            if (wid == 0) {
+                if ((uint32_t)lane < t_words) s_taken[lane] = rs.T;
+                if ((uint32_t)lane < C) m.s_cursor[lane] = my_cur;
+                uint32_t q = 0, nbat = 0;
+                while (q < nr) {
+                    const uint32_t rk = q + (uint32_t)lane;
+                    const bool in = rk < nr;
+                    const uint32_t rc_v = in ? m.s_rc[rk] : 0xFFFFFFFFu;
+                    const uint32_t ro_v = in ? m.s_ro[rk] : tile_total;
+                    const uint32_t re_v = rk + 1 < nr ? m.s_ro[rk + 1] : tile_total;
+                    const uint32_t o0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ro_v);
+                    const uint32_t o1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)re_v);
+                    const uint32_t j0 = jbase + o0;
+                    const uint32_t jend = jbase + o1 < J ? jbase + o1 : J;
+                    if (j0 >= jend) {
+                        ++q;
+                        continue;
+                    }
+                    // every run of the tile is short and valid; a batch ends within 64 jobs of o0
+                    const bool ok_v = in && rc_v < C && re_v - o0 <= 64u;
+                    const uint64_t okm = __ballot(ok_v);
+                    const uint32_t nrb = ~okm == 0ull ? 64u : (uint32_t)__builtin_ctzll(~okm);
+                    uint32_t nb = (uint32_t)__builtin_amdgcn_readlane((int)re_v, (int)nrb - 1) - o0;
+                    if (j0 + nb > J) nb = J - j0;
+                    if (lane == 0) {
+                        s_desc[4 * nbat + 0] = q;
+                        s_desc[4 * nbat + 1] = nrb;
+                        s_desc[4 * nbat + 2] = j0;
+                        s_desc[4 * nbat + 3] = nb;
+                    }
+                    q += nrb;
+                    ++nbat;
+                }
+                if (lane == 0) {
+                    m.s_misc[0] = nbat;
+                    *s_pcnt = 0;
+                }
+                if (lane < (int)kPipeWaves) s_prog[lane] = 0ull;
+            }
+            __syncthreads();
+            const uint32_t nbat = m.s_misc[0];
+            const uint32_t lvl = K - 1;
+            const uint32_t D = m.s_D[lvl], tl = m.s_toff[lvl], nwl = (D + 63) >> 6;
+            const uint32_t w_woff = (uint32_t)lane < C ? m.s_woff[lane] : 0u;
+            uint32_t* s_bc = m.s_long + 64 * wid;  // this wave's job offset -> class table
+            uint32_t my_placed = 0;
+            for (uint32_t bi = (uint32_t)wid; wid < (int)kPipeWaves && bi < nbat; bi += kPipeWaves) {
+                const uint32_t bid = bi + 1;  // progress words hold batch index + 1 (0: none yet)
+                const uint32_t q = s_desc[4 * bi], nrb = s_desc[4 * bi + 1], j0 = s_desc[4 * bi + 2],
+                               nb = s_desc[4 * bi + 3];
+                const uint32_t rk = q + (uint32_t)lane, o0 = j0 - jbase;
+                const bool inr = (uint32_t)lane < nrb;
+                const uint32_t rc_v = inr ? m.s_rc[rk] : 0u;
+                const uint32_t ro_v = inr ? m.s_ro[rk] : 0u;
+                const uint32_t re_v = inr ? (rk + 1 < nr ? m.s_ro[rk + 1] : tile_total) : 0u;
+                const bool starts = inr && re_v > ro_v;
+                if (starts) s_bc[ro_v - o0] = rc_v;
+                const uint64_t smask = wave_or64(starts ? 1ull << (ro_v - o0) : 0ull);
+                const uint64_t le = (uint32_t)lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+                const bool job = (uint32_t)lane < nb;
+                const uint32_t my_start = job ? 63u - (uint32_t)__builtin_clzll(smask & le) : 0u;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const uint32_t cls = job ? s_bc[my_start] : 0u;
+                const uint64_t cmask = wave_or64(job ? 1ull << cls : 0ull) & ~dead;
+                const bool cl = (uint32_t)lane < C && ((cmask >> lane) & 1ull);
+                const uint32_t curc = cl ? __hip_atomic_load(m.s_cursor + lane, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP)
+                                         : D;  // a stale (lower) cursor only widens the scan
+                const uint32_t d0 = wave_min_u32(curc);
+                uint64_t R = __ballot(job);
+                int32_t res = -1;
+                uint32_t w = d0 >> 6 < nwl ? d0 >> 6 : nwl;
+                if (lane == 0)
+                    __hip_atomic_store(s_prog + wid, ((unsigned long long)bid << 32) | w, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                // words each of the previous kPipeWaves - 1 batches is known to have
+                // passed (0xFFFFFFFF: finished); polled only when a word needs it
+                uint32_t known[kPipeWaves - 1];
+#pragma unroll
+                for (uint32_t k = 0; k + 1 < kPipeWaves; ++k) known[k] = k + 1 < bid ? 0u : 0xFFFFFFFFu;
+                uint64_t fcur = cl && w < nwl ? feas[w_woff + w] : 0ull;
+                for (; w < nwl && R != 0ull; ++w) {
+                    const uint64_t fnx = cl && w + 1 < nwl ? feas[w_woff + w + 1] : 0ull;  // static: prefetch
+                    // every earlier batch has passed word w: the previous kPipeWaves - 1
+                    // batches by their progress words (older ones ran on this wave,
+                    // or on a wave whose newer batch waited for them)
+#pragma unroll
+                    for (uint32_t k = 1; k < kPipeWaves; ++k) {
+                        if (known[k - 1] > w) continue;
+                        const uint32_t a = bid - k;
+                        unsigned long long* pw = s_prog + (a - 1) % kPipeWaves;
+                        for (uint32_t spins = 0;; ++spins) {
+                            const unsigned long long x =
+                                __hip_atomic_load(pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const uint32_t pb = (uint32_t)(x >> 32), pr = (uint32_t)x;
+                            known[k - 1] = pb > a ? 0xFFFFFFFFu : pb == a ? pr : 0u;
+                            if (known[k - 1] > w) break;
+                            if (spins > kPipeSpinLimit) break;  // never waits forever (a bug shows as a parity failure)
+                            __builtin_amdgcn_s_sleep(1);
+                        }
+                    }
+                    const uint64_t tw = s_taken[tl + w];
+                    const uint64_t g = cl ? fcur & ~tw : 0ull;
+                    fcur = fnx;
+                    const uint64_t taken = walk_word(g, cls, job, R, res, w, lane);
+                    if (lane == 0) {
+                        if (taken) s_taken[tl + w] = tw | taken;
+                        __hip_atomic_store(s_prog + wid, ((unsigned long long)bid << 32) | (w + 1), __ATOMIC_RELEASE,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                if (lane == 0)
+                    __hip_atomic_store(s_prog + wid, ((unsigned long long)bid << 32) | 0xFFFFFFFFull, __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (job) assign[j0 + lane] = res;
+                my_placed += (uint32_t)__popcll(__ballot(job && res >= 0));
+                uint64_t cm = cmask;
+                while (cm != 0ull) {
+                    const uint32_t cc = (uint32_t)__builtin_ctzll(cm);
+                    cm &= cm - 1ull;
+                    const uint64_t lanes_c = __ballot(job && cls == cc);
+                    const int32_t last = __builtin_amdgcn_readlane(res, 63 - __builtin_clzll(lanes_c));
+                    if ((uint32_t)lane == cc) atomicMax(m.s_cursor + cc, last < 0 ? D : (uint32_t)last + 1u);
+                }
+            }
+            if (lane == 0 && my_placed) atomicAdd(s_pcnt, my_placed);
+            __syncthreads();
+            if (wid == 0) {
+                const uint64_t Tn = (uint32_t)lane < t_words ? s_taken[lane] : rs.T;
+                const uint64_t fresh = Tn & ~rs.T;
+                if (lvl >= 1 && __ballot(fresh != 0ull) != 0ull) {
+                    rs.P |= fresh;
+                    rs.pend = rs.pend > (int)lvl ? rs.pend : (int)lvl;
+                }
+                rs.T = Tn;
+                if ((uint32_t)lane < C) my_cur = m.s_cursor[lane];
+            }
+            if (tid == 0) placed += *s_pcnt;
+        } else if (wid == 0 && regmode) {
             // Short runs are taken in batches: up to 64 consecutive jobs (lane = job)
             // of short runs at one level. Within a batch the lowest-index greedy
             // ("each job in order takes its lowest free feasible domain") equals the
@@ -1219,98 +1473,8 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rs.T, (int)(tl + w));
                     const uint64_t g = cl ? fcur & ~tw : 0ull;  // lane c: class c's free feasible bits
                     // job lane j: its class's word
-                    const uint32_t gl = (uint32_t)__shfl((int)(uint32_t)g, (int)cls);
-                    const uint32_t gh = (uint32_t)__shfl((int)(uint32_t)(g >> 32), (int)cls);
-                    const uint64_t gj = ((uint64_t)gh << 32) | gl;
-                    const uint64_t V0 = R & __ballot(job && gj != 0ull);  // jobs that can take something here
-                    if (V0 == 0ull) continue;
-                    // The chain runs on bits 0..62: s_ff1 of an empty word is -1, and the
-                    // s_bitset1 that follows then sets bit 63, which the chain never reads.
-                    // Bit 63 goes afterwards to the first visited job left without a domain
-                    // whose class has it (job order inside the word: it is the word's last
-                    // domain, so only jobs that found nothing below it can want it).
-                    const uint32_t gh62 = gh & 0x7FFFFFFFu;
-                    const uint32_t dbg_row = 4020u + (nbatch - 1u) * 4u + (w - (d0 >> 6));  // diag build only
-                    (void)dbg_row;
-                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) JSP_CLK(dbg_row, 0);
-                    uint64_t taken = 0;
-                    int32_t wres = -1;
-                    const uint32_t nv = (uint32_t)__popcll(V0);
-                    if (nv >= kChainUnrollMin) {
-                        // Dense word: the visiting jobs' class words are packed into
-                        // lanes 0..nv-1 (job order), then an unrolled chain reads
-                        // them with constant-lane readlanes and writes each result
-                        // into its packed lane: per job two readlanes, and-not,
-                        // lowest-bit, bit-set and one writelane -- half the
-                        // instructions of the loop below, no loop control.
-                        // (the permutes run on every lane: a source lane outside a
-                        // branch's exec mask would read as 0)
-                        const uint32_t src = (uint32_t)lane < nv ? select_bit(V0, (uint32_t)lane) : 0u;
-                        const uint32_t pgl = (uint32_t)__shfl((int)gl, (int)src);
-                        const uint32_t pgh = (uint32_t)__shfl((int)gh62, (int)src);
-                        const uint32_t cgl = (uint32_t)lane < nv ? pgl : 0u;
-                        const uint32_t cgh = (uint32_t)lane < nv ? pgh : 0u;
-                        int32_t cres = -1;
-                        chain_unrolled(cgl, cgh, nv, taken, cres);
-                        const uint32_t pos = mbcnt64(V0);
-                        const int32_t back = __shfl(cres, (int)(pos & 63u));
-                        if ((V0 >> lane) & 1ull) wres = back;
-                    } else {
-                    uint64_t V = V0;
-                    // software-pipelined: the next job's class word is read (two
-                    // readlanes) before the current job's scalar chain runs. Measured
-                    // ~100 shader cycles per job visit (tools/stamps_words.py): about
-                    // 7 per instruction of the 14-instruction loop on one wave; a
-                    // two-job unroll compiled to the same count per job.
-                    uint32_t j;  // current job: lowest bit of V, cleared
-                    asm("s_ff1_i32_b64 %[j], %[V]\n\t"
-                        "s_bitset0_b64 %[V], %[j]"
-                        : [V] "+s"(V), [j] "=&s"(j));
-                    uint64_t gc = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)j) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)j);
-                    while (true) {
-                        uint32_t jn;  // next job (-1: none; V stays 0)
-                        asm("s_ff1_i32_b64 %[j], %[V]\n\t"
-                            "s_bitset0_b64 %[V], %[j]"
-                            : [V] "+s"(V), [j] "=&s"(jn));
-                        const uint64_t gn =
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)gh62, (int)(jn & 63u)) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)gl, (int)(jn & 63u));
-                        uint64_t t;
-                        int32_t bpos;
-                        // taken |= lowest bit of (gc & ~taken); job j's lane gets its
-                        // position (-1: none). SALU only, plus one writelane whose lane
-                        // select (m0) a SALU move wrote three instructions earlier.
-                        asm("s_mov_b32 m0, %[j]\n\t"
-                            "s_andn2_b64 %[t], %[g], %[tk]\n\t"
-                            "s_ff1_i32_b64 %[b], %[t]\n\t"
-                            "s_bitset1_b64 %[tk], %[b]\n\t"
-                            "v_writelane_b32 %[w], %[b], m0"
-                            : [tk] "+s"(taken), [w] "+v"(wres), [t] "=&s"(t), [b] "=&s"(bpos)
-                            : [g] "s"(gc), [j] "s"(j)
-                            : "m0", "scc");  // s_andn2 sets SCC
-                        if ((int32_t)jn < 0) break;
-                        j = jn;
-                        gc = gn;
-                    }
-                    }
-                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) {
-                        JSP_CLK(dbg_row, 1);
-                        JSP_DBGV(dbg_row, 3, __popcll(V0));
-                    }
-                    taken &= ~(1ull << 63);
-                    const uint64_t m63 = __ballot(((V0 >> lane) & 1ull) && wres < 0 && (gh >> 31) != 0u);
-                    if (m63 != 0ull) {
-                        if ((uint32_t)lane == (uint32_t)__builtin_ctzll(m63)) wres = 63;
-                        taken |= 1ull << 63;
-                    }
-                    if (wres >= 0) res = (int32_t)(w * 64u + (uint32_t)wres);
-                    R &= ~__ballot(wres >= 0);
+                    const uint64_t taken = walk_word(g, cls, job, R, res, w, lane);
                     if ((uint32_t)lane == tl + w) tookv |= taken;
-                    if (nbatch <= 4u && w - (d0 >> 6) < 4u) {
-                        JSP_CLK(dbg_row, 2);
-                        JSP_DBGV(dbg_row, 4, __popcll(taken));
-                    }
                 }
                 JSP_STAMP(sb, 2);
                 if (job) assign[j0 + lane] = res;
@@ -1439,7 +1603,7 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     uint32_t C, TopoDev topo, const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
     uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats, uint32_t feas_words,
     uint32_t feas_in_lds, uint32_t topo_in_lds, uint32_t topo_words, uint32_t stage_cap, AssignRec* __restrict__ recs,
-    uint32_t* __restrict__ rec_count) {
+    uint32_t* __restrict__ rec_count, uint32_t pipe) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const uint32_t tw = taken_words(topo);
     uint64_t* s_win = s_dyn + tw;
@@ -1460,10 +1624,10 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     const uint64_t* F = feas_in_lds ? s_feas : feas;
     if (topo_in_lds)
         assign_block<kAssignThreads, true>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m, s_topo,
-                                           s_win, s_stage, stage_cap, recs, rec_count);
+                                           s_win, s_stage, stage_cap, recs, rec_count, pipe);
     else
         assign_block<kAssignThreads, false>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m,
-                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count);
+                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count, pipe);
 }
 
 // Expansion of assign_kernel's records (grid-stride, one wave per record):
@@ -1778,10 +1942,12 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
     JSP_STAMP(4090u, 1);
     if (f.topo_in_lds)
         assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
-                                          f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
+                                          f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
+                                          f.pipe);
     else
         assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
-                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr);
+                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
+                                           f.pipe);
     JSP_CLK(4090u, 2);
     JSP_STAMP(4090u, 3);
     if (f.done) signal_host(f.done, f.epoch, true);
@@ -2356,6 +2522,15 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
     return hipGetLastError();
 }
 
+// The pipelined batch walk (assign_block); JSP_NO_PIPE=1 turns it off (A/B runs).
+bool pipe_walk_enabled() {
+    static const bool on = [] {
+        const char* v = std::getenv("JSP_NO_PIPE");
+        return !(v && v[0] == '1');
+    }();
+    return on;
+}
+
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
@@ -2365,7 +2540,7 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
     if (p.lds_bytes == 0) return hipErrorInvalidValue;
     hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
                        run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
-                       topo_words, p.stage_cap, recs, rec_count);
+                       topo_words, p.stage_cap, recs, rec_count, pipe_walk_enabled() ? 1u : 0u);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
     // records never outnumber the placed jobs (each taken domain is in one record)
     const uint32_t waves = J < 8192u ? J : 8192u;
