@@ -1050,7 +1050,10 @@ __device__ __forceinline__ void chain_unrolled(uint32_t gl, uint32_t gh, uint32_
 #undef JSP_CHAIN_8
 #undef JSP_CHAIN_STEP
 constexpr uint32_t kChainUnrollMin = 6;
-constexpr uint32_t kPipeWaves = 4;                 // waves of the pipelined batch walk
+#ifndef JSP_PIPE_WAVES
+#define JSP_PIPE_WAVES 4
+#endif
+constexpr uint32_t kPipeWaves = JSP_PIPE_WAVES;    // waves of the pipelined batch walk
 constexpr uint32_t kPipeSpinLimit = 1u << 24;      // bounded wait on an earlier batch's progress  // visiting jobs from which a word takes the unrolled chain
 
 // One word of a batch (wave-wide): lane c holds class c's free feasible bits
