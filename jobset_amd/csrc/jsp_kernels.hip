@@ -59,6 +59,15 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
 #endif
 
 // ----------------------------------------------------------------- helpers
+// LDS pointers typed as such: where LDS tables are reached through a struct or
+// a carved-up generic pointer the compiler can lose their address space and
+// emit flat loads and atomics (each waiting on both the vector and the LDS
+// counters; a release or acquire on one also drains global traffic)
+#define JSP_LDS __attribute__((address_space(3)))
+template <typename T>
+__device__ __forceinline__ JSP_LDS T* lds_ptr(T* p) {
+    return (JSP_LDS T*)p;
+}
 // Inclusive wave64 prefix sum on the VALU with DPP (no LDS traffic):
 // row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry the
 // row totals across rows (GFX9/CDNA DPP controls).
@@ -1226,9 +1235,10 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
         }
         if (pipe) {
             uint32_t* s_desc = s_stage;  // [4 per batch] {first run, runs, first job, jobs}
-            unsigned long long* s_prog = reinterpret_cast<unsigned long long*>(
-                (reinterpret_cast<uintptr_t>(s_stage + 4 * NT) + 7) & ~static_cast<uintptr_t>(7));
-            uint32_t* s_pcnt = reinterpret_cast<uint32_t*>(s_prog + kPipeWaves);
+            JSP_LDS unsigned long long* s_prog = lds_ptr(reinterpret_cast<unsigned long long*>(
+                (reinterpret_cast<uintptr_t>(s_stage + 4 * NT) + 7) & ~static_cast<uintptr_t>(7)));
+            JSP_LDS uint32_t* s_pcnt = reinterpret_cast<JSP_LDS uint32_t*>(s_prog + kPipeWaves);
+            JSP_LDS uint32_t* s_cur = lds_ptr(m.s_cursor);
             if (wid == 0) {
                 if ((uint32_t)lane < t_words) s_taken[lane] = rs.T;
                 if ((uint32_t)lane < C) m.s_cursor[lane] = my_cur;
@@ -1296,7 +1306,7 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 const uint32_t cls = job ? s_bc[my_start] : 0u;
                 const uint64_t cmask = wave_or64(job ? 1ull << cls : 0ull) & ~dead;
                 const bool cl = (uint32_t)lane < C && ((cmask >> lane) & 1ull);
-                const uint32_t curc = cl ? __hip_atomic_load(m.s_cursor + lane, __ATOMIC_RELAXED,
+                const uint32_t curc = cl ? __hip_atomic_load(s_cur + lane, __ATOMIC_RELAXED,
                                                              __HIP_MEMORY_SCOPE_WORKGROUP)
                                          : D;  // a stale (lower) cursor only widens the scan
                 const uint32_t d0 = wave_min_u32(curc);
@@ -1321,7 +1331,7 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     for (uint32_t k = 1; k < kPipeWaves; ++k) {
                         if (known[k - 1] > w) continue;
                         const uint32_t a = bid - k;
-                        unsigned long long* pw = s_prog + (a - 1) % kPipeWaves;
+                        JSP_LDS unsigned long long* pw = s_prog + (a - 1) % kPipeWaves;
                         for (uint32_t spins = 0;; ++spins) {
                             const unsigned long long x =
                                 __hip_atomic_load(pw, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1353,10 +1363,13 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                     cm &= cm - 1ull;
                     const uint64_t lanes_c = __ballot(job && cls == cc);
                     const int32_t last = __builtin_amdgcn_readlane(res, 63 - __builtin_clzll(lanes_c));
-                    if ((uint32_t)lane == cc) atomicMax(m.s_cursor + cc, last < 0 ? D : (uint32_t)last + 1u);
+                    if ((uint32_t)lane == cc)
+                        __hip_atomic_fetch_max(s_cur + cc, last < 0 ? D : (uint32_t)last + 1u, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
-            if (lane == 0 && my_placed) atomicAdd(s_pcnt, my_placed);
+            if (lane == 0 && my_placed)
+                __hip_atomic_fetch_add(s_pcnt, my_placed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __syncthreads();
             if (wid == 0) {
                 const uint64_t Tn = (uint32_t)lane < t_words ? s_taken[lane] : rs.T;
@@ -1670,6 +1683,7 @@ struct TailFeasArgs {
 };
 static_assert(kMaxLevels == 4, "TailFeasArgs spells out the levels");
 
+
 __device__ __forceinline__ uint32_t tail_ooff(const TailFeasArgs& t, uint32_t k) {
     const uint32_t o0 = t.ooff0, o1 = t.ooff1, o2 = t.ooff2;  // values: a conditional of lvalues would select
     return k == 0 ? o0 : k == 1 ? o1 : o2;                    // field addresses and keep t in scratch
@@ -1677,9 +1691,14 @@ __device__ __forceinline__ uint32_t tail_ooff(const TailFeasArgs& t, uint32_t k)
 
 // ancestor at level lvl of leaf l (hierarchy tables from LDS when staged)
 __device__ __forceinline__ uint32_t tail_up_dom(const TailFeasArgs& t, uint32_t l, uint32_t lvl) {
+    if (t.s_topo) {
+        JSP_LDS const uint32_t* st = lds_ptr(t.s_topo);
+        JSP_LDS const uint32_t* po = lds_ptr(t.s_poff);
+        for (uint32_t k = t.K - 1; k > lvl; --k) l = st[po[k] + l];
+        return l;
+    }
     const int32_t *p1 = t.par1, *p2 = t.par2, *p3 = t.par3;  // values, as in tail_ooff
-    for (uint32_t k = t.K - 1; k > lvl; --k)
-        l = t.s_topo ? t.s_topo[t.s_poff[k] + l] : (uint32_t)(k == 1 ? p1 : k == 2 ? p2 : p3)[l];
+    for (uint32_t k = t.K - 1; k > lvl; --k) l = (uint32_t)(k == 1 ? p1 : k == 2 ? p2 : p3)[l];
     return l;
 }
 
@@ -1754,38 +1773,59 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
                 if (l0 + i >= L || ov[i] == 0u) continue;
                 for (uint32_t k = 0; k + 1 < t.K; ++k) {
                     const uint32_t d = tail_up_dom(t, l0 + i, k);
-                    atomicOr(reinterpret_cast<unsigned long long*>(&t.s_uocc[tail_ooff(t, k) + (d >> 6)]),
-                             (unsigned long long)(1ull << (d & 63u)));
+                    __hip_atomic_fetch_or(lds_ptr(t.s_uocc) + tail_ooff(t, k) + (d >> 6), 1ull << (d & 63u),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
             }
         }
         JSP_STAMP(4008u, 2);
-        uint32_t dl[4] = {0u, 0u, 0u, 0u}, dl_lvl = 0xFFFFFFFFu;  // wave-uniform level of dl
+        // leaf-level classes, unrolled: a 16-lane row covers one 64-leaf word;
+        // OR the lanes' nibbles across the row (DPP row_shr 1/2/4/8), its last
+        // lane stores it
 #pragma unroll
         for (int u = 0; u < NG; ++u) {
-            if ((uint32_t)u >= npc) continue;
+            if ((uint32_t)u >= npc || ((t.leaf_cls >> cid[u]) & 1ull) == 0ull) continue;
+            if (u < 8) JSP_STAMP(4009u, u);
             const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)t.c_pods, (int)cid[u]);
-            if ((t.leaf_cls >> cid[u]) & 1ull) {
-                // a 16-lane row covers one 64-leaf word: OR the lanes' nibbles
-                // across the row (DPP row_shr 1/2/4/8), its last lane stores it
-                const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)t.c_beg, (int)cid[u]);
-                uint32_t nib = 0;
+            const uint32_t wo = (uint32_t)__builtin_amdgcn_readlane((int)t.c_beg, (int)cid[u]);
+            uint32_t nib = 0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) nib |= (cv[u][i] >= pods && ov[i] == 0u) ? (1u << i) : 0u;
-                const uint32_t sh = 4u * (lane & 7u);
-                uint32_t lo = (lane & 8u) ? 0u : nib << sh, hi = (lane & 8u) ? nib << sh : 0u;
-                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x111, 0xf, 0xf, true);  // row_shr:1
-                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x111, 0xf, 0xf, true);
-                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x112, 0xf, 0xf, true);  // row_shr:2
-                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x112, 0xf, 0xf, true);
-                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x114, 0xf, 0xf, true);  // row_shr:4
-                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x114, 0xf, 0xf, true);
-                lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x118, 0xf, 0xf, true);  // row_shr:8
-                hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x118, 0xf, 0xf, true);
-                if ((lane & 15u) == 15u && (l0 & ~63u) < L) t.s_feas[wo + (l0 >> 6)] = ((uint64_t)hi << 32) | lo;
-            } else {
-                const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)t.c_lvl, (int)cid[u]);
-                uint64_t* sum = t.s_usum + (uint32_t)__builtin_amdgcn_readlane((int)t.c_uoff, (int)cid[u]);
+            for (int i = 0; i < 4; ++i) nib |= (cv[u][i] >= pods && ov[i] == 0u) ? (1u << i) : 0u;
+            const uint32_t sh = 4u * (lane & 7u);
+            uint32_t lo = (lane & 8u) ? 0u : nib << sh, hi = (lane & 8u) ? nib << sh : 0u;
+            lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x111, 0xf, 0xf, true);  // row_shr:1
+            hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x111, 0xf, 0xf, true);
+            lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x112, 0xf, 0xf, true);  // row_shr:2
+            hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x112, 0xf, 0xf, true);
+            lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x114, 0xf, 0xf, true);  // row_shr:4
+            hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x114, 0xf, 0xf, true);
+            lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x118, 0xf, 0xf, true);  // row_shr:8
+            hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x118, 0xf, 0xf, true);
+            if ((lane & 15u) == 15u && (l0 & ~63u) < L) lds_ptr(t.s_feas)[wo + (l0 >> 6)] = ((uint64_t)hi << 32) | lo;
+        }
+        JSP_STAMP(4008u, 5);
+        // upper-level classes (few), in a rolled loop so that the pass's code
+        // stays small: the tail runs once per launch on whichever CU drew the
+        // last ticket, from a cold instruction cache. Each class's 4 values are
+        // picked from the unrolled registers by its slot in the pass.
+        if (t.scr) {
+            uint32_t dl[4] = {0u, 0u, 0u, 0u}, dl_lvl = 0xFFFFFFFFu;  // wave-uniform level of dl
+            uint64_t um = t.pass_cls & ~t.leaf_cls;
+            while (um != 0ull) {
+                const uint32_t c = (uint32_t)__builtin_ctzll(um);
+                um &= um - 1ull;
+                const uint32_t u = (uint32_t)__popcll(t.pass_cls & ((1ull << c) - 1ull));  // slot in the pass
+                uint32_t v[4] = {cv[0][0], cv[0][1], cv[0][2], cv[0][3]};
+#pragma unroll
+                for (int k = 1; k < NG; ++k)
+                    if (u == (uint32_t)k) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) v[i] = cv[k][i];
+                    }
+                const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)t.c_pods, (int)c);
+                const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)t.c_lvl, (int)c);
+                JSP_LDS uint64_t* sum =
+                    lds_ptr(t.s_usum) + (uint32_t)__builtin_amdgcn_readlane((int)t.c_uoff, (int)c);
                 if (lvl != dl_lvl) {  // the 4 leaves' domains at this level, shared by its classes
 #pragma unroll
                     for (int i = 0; i < 4; ++i) dl[i] = l0 + i < L ? tail_up_dom(t, l0 + i, lvl) : 0u;
@@ -1798,15 +1838,16 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
                     if (l0 + i >= L) break;
                     const uint32_t d = dl[i];
                     if (d != dcur) {
-                        if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(&sum[dcur]), (unsigned long long)acc);
+                        if (acc) __hip_atomic_fetch_add(sum + dcur, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         acc = 0;
                         dcur = d;
                     }
-                    acc += cv[u][i] < pods ? cv[u][i] : pods;
+                    acc += v[i] < pods ? v[i] : pods;
                 }
-                if (acc) atomicAdd(reinterpret_cast<unsigned long long*>(&sum[dcur]), (unsigned long long)acc);
+                if (acc) __hip_atomic_fetch_add(sum + dcur, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
         }
+        JSP_STAMP(4008u, 4);
     }
 }
 
