@@ -1863,9 +1863,10 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
 // old - tile_base and "last" = old + 1 - done_base == n_blocks.
 // The fused kernel's tail, run by the workgroup whose tile finished last: the
 // feasibility bitmaps of every class into LDS from the tiles' published sums,
-// then the assignment walk; f.done (host path) gets f.epoch at the end.
+// then the assignment walk; done (host path) gets epoch at the end.
 template <int W, int R>
-__device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& f, uint32_t* lds) {
+__device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& f, uint32_t* lds, uint32_t J,
+                                           uint32_t n_runs, uint32_t epoch, uint32_t* done) {
     JSP_STAMP(4000u, 1);
     // the tail: small tables first (independent of the other workgroups' sums)
     uint64_t* s_taken = reinterpret_cast<uint64_t*>(lds);
@@ -1985,16 +1986,16 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
     JSP_CLK(4090u, 0);
     JSP_STAMP(4090u, 1);
     if (f.topo_in_lds)
-        assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
+        assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, n_runs, J, f.assign,
                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
                                           f.pipe);
     else
-        assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, f.n_runs, f.J, f.assign,
+        assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, n_runs, J, f.assign,
                                            f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
                                            f.pipe);
     JSP_CLK(4090u, 2);
     JSP_STAMP(4090u, 3);
-    if (f.done) signal_host(f.done, f.epoch, true);
+    if (done) signal_host(done, epoch, true);
 }
 
 // Small words after a fused tile's tally carve (sized for class group 0).
@@ -2039,7 +2040,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
     __syncthreads();
     JSP_STAMP(tile, 5);
     if (*s_flag == 0) return;
-    fused_tail<W, R>(a, f, lds);
+    fused_tail<W, R>(a, f, lds, f.J, f.n_runs, f.epoch, f.done);
 }
 
 // ----------------------------------------------------------------- single-class compaction
@@ -2357,12 +2358,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
         }
         __syncthreads();
         if (s_x[2] != 0) {
-            FusedArgs g = f;
-            g.J = J;
-            g.n_runs = __hip_atomic_load(v.nruns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            g.epoch = next;
-            g.done = v.done;
-            fused_tail<W, R>(a, g, lds);
+            // the request's fields are passed apart: a modified copy of f would
+            // live in scratch (its arrays are indexed at run time)
+            fused_tail<W, R>(a, f, lds, J, __hip_atomic_load(v.nruns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                             next, v.done);
         }
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
