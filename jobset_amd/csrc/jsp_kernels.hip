@@ -1918,7 +1918,7 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
     uint64_t* s_uocc = s_usum + (uint32_t)__builtin_amdgcn_readlane((int)uincl, 63);
     const uint32_t ooff0 = 0, ooff1 = (f.topo.D[0] + 63) >> 6, ooff2 = ooff1 + ((f.topo.D[1] + 63) >> 6);
     if (scr) {
-        for (uint32_t i = threadIdx.x; i < f.fscr_words; i += kTallyThreads) s_usum[i] = 0;
+        for (uint32_t i = threadIdx.x; i < f.fscr_words; i += kTallyThreads) lds_ptr(s_usum)[i] = 0;
         __syncthreads();
     }
     // every thread takes 4-leaf chunks, loads occupancy once and the capacities
@@ -1949,12 +1949,13 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
             const uint32_t we = (uint32_t)__builtin_amdgcn_readlane((int)c_end, (int)c);
             const uint32_t lvl = (uint32_t)__builtin_amdgcn_readlane((int)c_lvl, (int)c);
             const uint32_t pods = (uint32_t)__builtin_amdgcn_readlane((int)c_pods, (int)c);
-            const uint64_t* sum = s_usum + (uint32_t)__builtin_amdgcn_readlane((int)c_uoff, (int)c);
+            JSP_LDS const uint64_t* sum = lds_ptr(s_usum) + (uint32_t)__builtin_amdgcn_readlane((int)c_uoff, (int)c);
+            JSP_LDS const uint64_t* uocc = lds_ptr(s_uocc);
             const uint32_t D = f.topo.D[lvl];
             for (uint32_t gw = wb + (wid + kTallyWaves - base % kTallyWaves) % kTallyWaves; gw < we;
                  gw += kTallyWaves) {
                 const uint32_t d = (gw - wb) * 64u + (uint32_t)lane;
-                const bool ok = d < D && sum[d] >= pods && ((s_uocc[(lvl == 0 ? ooff0 : lvl == 1 ? ooff1 : ooff2) + (d >> 6)] >> (d & 63u)) & 1ull) == 0ull;
+                const bool ok = d < D && sum[d] >= pods && ((uocc[(lvl == 0 ? ooff0 : lvl == 1 ? ooff1 : ooff2) + (d >> 6)] >> (d & 63u)) & 1ull) == 0ull;
                 const uint64_t word = __ballot(ok);
                 if (lane == 0) s_feas[gw] = word;
             }
