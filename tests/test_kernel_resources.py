@@ -7,50 +7,65 @@ struct whose arrays are indexed at run time, or a runtime-indexed local array,
 would land in scratch ("code-generation rules").
 """
 import os
-import re
-import shutil
-import subprocess
+import struct
 
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "jobset_amd", "libjsplace.so")
-LLVM = "/opt/rocm/lib/llvm/bin"
 
 
-def _kernel_notes(tmp_path):
-    bundler = os.path.join(LLVM, "clang-offload-bundler")
-    readelf = os.path.join(LLVM, "llvm-readelf")
-    if not (os.path.exists(LIB) and shutil.which("objcopy") and os.path.exists(bundler)
-            and os.path.exists(readelf)):
-        pytest.skip("library or ROCm LLVM tools absent")
-    fat = tmp_path / "fatbin.bin"
-    co = tmp_path / "gfx950.co"
-    subprocess.run(["objcopy", f"--dump-section=.hip_fatbin={fat}", LIB], check=True)
-    subprocess.run([bundler, "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--input={fat}",
-                    f"--output={co}", "--unbundle"], check=True)
-    notes = subprocess.run([readelf, "--notes", str(co)], check=True, capture_output=True, text=True).stdout
-    kernels = {}
-    cur = None
-    for line in notes.splitlines():
-        m = re.match(r"\s+\.name:\s+(\S+)", line)
-        if m:
-            cur = m.group(1)
-            kernels[cur] = {}
+# Pure-Python reading (no child processes: forking after the HIP runtime is
+# loaded by an earlier test has crashed the test process later).
+def _elf_sections(blob):
+    shoff, = struct.unpack_from("<Q", blob, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", blob, 0x3A)
+    heads = [struct.unpack_from("<IIQQQQIIQQ", blob, shoff + i * shentsize) for i in range(shnum)]
+    stro = heads[shstrndx][4]
+    for h in heads:
+        end = blob.index(b"\0", stro + h[0])
+        yield blob[stro + h[0]:end].decode(), h[1], blob[h[4]:h[4] + h[5]]
+
+
+def _kernel_notes():
+    msgpack = pytest.importorskip("msgpack")
+    if not os.path.exists(LIB):
+        pytest.skip("library not built")
+    with open(LIB, "rb") as f:
+        lib = f.read()
+    fat = next(data for name, _, data in _elf_sections(lib) if name == ".hip_fatbin")
+    assert fat[:24] == b"__CLANG_OFFLOAD_BUNDLE__", "uncompressed offload bundle expected"
+    n, = struct.unpack_from("<Q", fat, 24)
+    pos, co = 32, None
+    for _ in range(n):
+        off, size, tlen = struct.unpack_from("<QQQ", fat, pos)
+        triple = fat[pos + 24:pos + 24 + tlen].decode()
+        pos += 24 + tlen
+        if triple.endswith("gfx950"):
+            co = fat[off:off + size]
+    assert co is not None, "no gfx950 code object in the library"
+    for _, typ, data in _elf_sections(co):
+        if typ != 7:  # SHT_NOTE
             continue
-        m = re.match(r"\s+\.(private_segment_fixed_size|vgpr_spill_count|uses_dynamic_stack):\s+(\S+)", line)
-        if m and cur is not None:
-            kernels[cur][m.group(1)] = m.group(2)
-    return kernels
+        q = 0
+        while q + 12 <= len(data):
+            namesz, descsz, ntype = struct.unpack_from("<III", data, q)
+            name = data[q + 12:q + 12 + namesz].rstrip(b"\0")
+            d0 = q + 12 + ((namesz + 3) & ~3)
+            if name == b"AMDGPU" and ntype == 32:  # NT_AMDGPU_METADATA (msgpack)
+                meta = msgpack.unpackb(data[d0:d0 + descsz], raw=False)
+                return {k[".name"]: k for k in meta["amdhsa.kernels"]}
+            q = d0 + ((descsz + 3) & ~3)
+    raise AssertionError("no AMDGPU metadata note")
 
 
-def test_no_kernel_uses_scratch(tmp_path):
-    kernels = _kernel_notes(tmp_path)
+def test_no_kernel_uses_scratch():
+    kernels = _kernel_notes()
     # every kernel family of the engine is in the library
     for fam in ("tally_kernel", "feas_kernel", "assign_kernel", "expand_kernel", "place_compact_kernel",
                 "place_fused_kernel", "place_service_kernel", "place_fused_service_kernel"):
         assert any(fam in k for k in kernels), fam
     bad = {k: v for k, v in kernels.items()
-           if v.get("private_segment_fixed_size") != "0" or v.get("vgpr_spill_count") != "0"
-           or v.get("uses_dynamic_stack") != "false"}
+           if v.get(".private_segment_fixed_size") != 0 or v.get(".vgpr_spill_count") != 0
+           or v.get(".uses_dynamic_stack") is not False}
     assert not bad, bad
