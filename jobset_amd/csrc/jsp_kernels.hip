@@ -1712,7 +1712,6 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
     // the pass's classes and their capacity rows, wave-uniform (SGPRs): each
     // load below is one instruction on a scalar base and a shared lane offset
     uint32_t cid[NG];
-    const uint32_t* crow[NG];
     {
         uint64_t m = t.pass_cls;
 #pragma unroll
@@ -1720,9 +1719,14 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
             const uint32_t c = (uint32_t)__builtin_ctzll(m);  // past npc: the last class again
             if ((uint32_t)u + 1 < npc) m &= m - 1ull;
             cid[u] = to_sgpr(c);
-            crow[u] = t.cap + (size_t)cid[u] * t.ld;
         }
     }
+    // one buffer resource over the capacity rows of classes 0..highest of the
+    // pass (a resource or a pointer per row would cost 4 or 2 SGPRs each, and
+    // this kernel already spills SGPRs)
+    const uint32_t n_rows = 64u - (uint32_t)__builtin_clzll(t.pass_cls);
+    const __amdgpu_buffer_rsrc_t cap_r =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t*>(t.cap), (short)0, (int)(n_rows * t.ld * 4u), 0x00020000);
     JSP_STAMP(4008u, 3);
     // wave-uniform trip count (lanes past L run with masked values): the
     // leaf-level classes' words are formed by a DPP OR across each 16-lane row
@@ -1741,7 +1745,8 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
             ov[0] = o4.x; ov[1] = o4.y; ov[2] = o4.z; ov[3] = o4.w;
 #pragma unroll
             for (int u = 0; u < NG; ++u) {
-                const uint4 c4 = load16_sc1_n(crow[u], l0 * 4u, L * 4u);
+                const uint4 c4 = __builtin_bit_cast(
+                    uint4, __builtin_amdgcn_raw_buffer_load_b128(cap_r, cid[u] * t.ld * 4u + l0 * 4u, 0, 16));
                 cv[u][0] = c4.x; cv[u][1] = c4.y; cv[u][2] = c4.z; cv[u][3] = c4.w;
             }
         } else {  // the last, partial chunk (and lanes past L): clamped dword loads
@@ -1753,7 +1758,7 @@ __device__ __forceinline__ void tail_leaf_pass(const TailFeasArgs& t) {
 #pragma unroll
             for (int u = 0; u < NG; ++u)
 #pragma unroll
-                for (int i = 0; i < 4; ++i) cv[u][i] = load_handoff(crow[u] + ix[i]);
+                for (int i = 0; i < 4; ++i) cv[u][i] = load_handoff(t.cap + (size_t)cid[u] * t.ld + ix[i]);
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
