@@ -32,9 +32,11 @@ oracle:
 	$(MAKE) -s -C oracle
 
 # diagnostic build with in-kernel phase stamps (tools/stamps.py); never the product library
-diag: tools/diag/libjsplace.so tools/diag/dispatch_probe tools/diag/stream_ceiling
-tools/diag/dispatch_probe: tools/dispatch_probe.hip
-	@mkdir -p tools/diag
+diag: tools/diag/libjsplace.so tools/bin/dispatch_probe tools/bin/stream_ceiling
+# probes that run on the GPU box live in tools/bin (shipped); the diagnostic
+# library stays in tools/diag (.gpurunignore: 4 MB per push)
+tools/bin/dispatch_probe: tools/dispatch_probe.hip
+	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -o $@ $<
 tools/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip jobset_amd/csrc/jsp_engine.cc $(HOST_SRC) $(HDR) $(HOST_HDR)
 	@mkdir -p build/diag tools/diag
@@ -64,6 +66,6 @@ clean:
 .PHONY: all oracle clean diag sanitize
 
 # achievable streaming ceiling (read-only and copy, cold and warm) at the placement kernels' byte counts
-tools/diag/stream_ceiling: tools/stream_ceiling.hip
-	@mkdir -p tools/diag
+tools/bin/stream_ceiling: tools/stream_ceiling.hip
+	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<

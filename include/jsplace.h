@@ -144,6 +144,9 @@ typedef struct jsp_timing {
     uint64_t svc_starts;       /* service launches (first use, after uploads, idle exits, restarts) */
     double svc_us;             /* summed in-kernel request time (first tile saw the request -> last tile
                                   done, 100 MHz device clock); accumulated while timing is on */
+    uint64_t svc_fallbacks;    /* jsp_place calls the service could not answer (its grid does not fit the
+                                  CUs, it left, or a request failed on the device): answered by the launch
+                                  path instead; the service stays off until the next upload */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */

@@ -413,7 +413,7 @@ bool engineTopology(Cache& c, const std::string& node, const std::string& key, i
     if (!c.eng) return false;
     if (c.planner) {
         const int lk = c.planner->level_of(key);
-        if (lk < 0 || !c.planner->synced() || !c.planner->row_of(node, row)) return false;
+        if (lk < 0 || !c.planner->serving() || !c.planner->row_of(node, row)) return false;
         *level = (uint32_t)lk;
         return true;
     }
@@ -1080,13 +1080,21 @@ Json dispatch(const std::string& m, const Json& q) {
     std::lock_guard<std::mutex> g(c.mu);
     if (m == "cache.add") {  // watch Added / Modified
         const Json& o = q.get("object");
-        if (q.get("kind").as_string() == "Node") c.nodes[name_of(o)] = o;
-        else c.pods[ns_of(o) + "/" + name_of(o)] = o;
+        if (q.get("kind").as_string() == "Node") {
+            c.nodes[name_of(o)] = o;
+            if (c.planner) c.planner->note_node_event();  // its labels may have moved it to another domain
+        } else {
+            c.pods[ns_of(o) + "/" + name_of(o)] = o;
+        }
         return ok(true);
     }
     if (m == "cache.remove") {  // watch Deleted
-        if (q.get("kind").as_string() == "Node") c.nodes.erase(q.get("name").as_string());
-        else c.pods.erase(q.get("namespace").as_string() + "/" + q.get("name").as_string());
+        if (q.get("kind").as_string() == "Node") {
+            c.nodes.erase(q.get("name").as_string());
+            if (c.planner) c.planner->note_node_event();  // a Node Get now answers NotFound -> ""
+        } else {
+            c.pods.erase(q.get("namespace").as_string() + "/" + q.get("name").as_string());
+        }
         return ok(true);
     }
     if (m == "planner.new") {

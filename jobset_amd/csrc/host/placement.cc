@@ -362,6 +362,7 @@ Err2 Planner::sync(const std::map<std::string, Json>& nodes, const std::map<std:
     const std::vector<uint32_t> old_tb = taint_bits_, old_fr = free_;
     const std::vector<int32_t> old_ex = excl_;
     if (Err2 e = rebuild(nodes, pods); !e.ok()) return e;
+    nodes_dirty_ = false;  // the rebuilt host columns reflect every Node event so far
     const uint32_t N = (uint32_t)row_node_.size(), R = (uint32_t)res_.size();
     const bool same = synced_ && !preds_dirty_ && old_rows == row_node_ && old_fl == first_leaf_ &&
                       old_ls == leaf_start_ && old_taints == taints_ && old_W == W_;
@@ -396,8 +397,13 @@ Err2 Planner::sync(const std::map<std::string, Json>& nodes, const std::map<std:
                 dt[j] = taint_bits_[i];
                 de[j] = excl_[i];
             }
-            if (jsp_snapshot_patch(eng_, rows.data(), n, dl.data(), dt.data(), df.data(), de.data()) != JSP_OK)
+            if (jsp_snapshot_patch(eng_, rows.data(), n, dl.data(), dt.data(), df.data(), de.data()) != JSP_OK) {
+                // the host columns are already the new ones: without this the
+                // next sync would find nothing to patch and the engine would
+                // keep the old rows for good; a full upload repairs it
+                synced_ = false;
                 return {std::string("placement engine: ") + jsp_last_error()};
+            }
             upload = "patch";
             patched = n;
         }

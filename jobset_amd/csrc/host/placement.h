@@ -103,6 +103,12 @@ public:
     const std::string& row_node(uint32_t row) const { return row_node_[row]; }
     jsp_engine* engine() const { return eng_; }
     bool synced() const { return synced_; }
+    // A Node was added, modified or removed in the cache since the last sync:
+    // the snapshot's row -> domain answers may be stale, so the webhook and
+    // reconciler lookups take the reference's Node Get path until the next
+    // sync (serving() false). Pod events do not change a row's domain.
+    void note_node_event() { nodes_dirty_ = true; }
+    bool serving() const { return synced_ && !nodes_dirty_; }
     // the host copy of the columns (tests compare a patched engine with a re-ingest)
     Json columns() const;
 
@@ -117,6 +123,7 @@ private:
     bool preds_dirty_ = true;
     std::vector<TaintKey> taints_;    // sorted dictionary
     bool synced_ = false;
+    bool nodes_dirty_ = false;
     // structure
     std::vector<std::string> row_node_;
     std::map<std::string, int32_t> node_row_;

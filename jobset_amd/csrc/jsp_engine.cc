@@ -91,6 +91,7 @@ struct EvPair {
 
 struct jsp_engine {
     int device = 0;
+    int n_cu = 0;  // compute units (multiProcessorCount)
     hipStream_t stream = nullptr;
     std::mutex mu;
 
@@ -137,10 +138,15 @@ struct jsp_engine {
     uint32_t spin_limit = 1u << 22;
 
     // stream ordering: work is enqueued on the engine stream or a caller's;
-    // the first call on a different stream waits for the previous one
-    hipStream_t last_stream = nullptr;
+    // the first call on a different stream waits for the previous one. A
+    // caller's stream is touched only inside the call that was given it: the
+    // call records ev_last on it before returning, and later calls wait on
+    // that engine-owned event (the caller may destroy its stream meanwhile).
+    hipStream_t last_stream = nullptr;  // compared, never used after its call returned
     bool have_last = false;
-    hipEvent_t ev_switch = nullptr;
+    bool last_foreign = false;          // the last call enqueued on a caller's stream
+    hipEvent_t ev_switch = nullptr;     // recorded on the engine stream
+    hipEvent_t ev_last = nullptr;       // recorded on the last caller stream, at the end of its call
 
     // resident placement service: the compaction shape kept on the GPU
     // between host-API placements (place_service_kernel), fed by a host-mapped
@@ -158,6 +164,8 @@ struct jsp_engine {
         int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
+        bool broken = false;  // a start or a request failed on this geometry: the launch path answers until
+                              // the next upload (every upload clears it)
         std::chrono::steady_clock::time_point last{};
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
@@ -175,6 +183,7 @@ struct jsp_engine {
             if (p.b) (void)hipEventDestroy(p.b);
         }
         if (ev_switch) (void)hipEventDestroy(ev_switch);
+        if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.stream) (void)hipStreamDestroy(svc.stream);
     }
@@ -202,19 +211,46 @@ constexpr size_t kMaxEvents = 3 * 4096;
 // runs feasibility + assignment on one 256-thread workgroup.
 constexpr uint32_t kFusedMaxBlocks = 256;
 
-// Order work on stream s after everything the engine enqueued before on
-// another stream (uploads and jsp_place use the engine stream, the device
-// entry points the caller's): the first call on a new stream records an event
-// on the previous one and makes s wait for it. Calls on one stream cost nothing.
-int enter_stream(jsp_engine* e, hipStream_t s) {
-    if (e->have_last && e->last_stream != s) {
+// Make stream s wait for everything the engine enqueued before (on any
+// stream): the engine stream's work through an event recorded on it now, a
+// caller stream's through ev_last, recorded at the end of the call that used
+// it (that stream itself is never touched again: it may be gone).
+int wait_prior(jsp_engine* e, hipStream_t s) {
+    if (!e->have_last) return JSP_OK;
+    if (e->last_foreign) {
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
+    } else {
         if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
+        HIP_TRY(hipEventRecord(e->ev_switch, e->stream));
         HIP_TRY(hipStreamWaitEvent(s, e->ev_switch, 0));
     }
+    return JSP_OK;
+}
+
+// Order work on stream s after everything the engine enqueued before on
+// another stream (uploads and jsp_place use the engine stream, the device
+// entry points the caller's). Calls on one stream cost nothing here.
+int enter_stream(jsp_engine* e, hipStream_t s) {
+    if (e->have_last && e->last_stream != s) return wait_prior(e, s);
+    return JSP_OK;
+}
+
+// After a call enqueued its work on s: a caller's stream gets ev_last
+// recorded on it while the handle is known to be valid.
+int leave_stream(jsp_engine* e, hipStream_t s) {
     e->last_stream = s;
     e->have_last = true;
+    e->last_foreign = s != e->stream;
+    if (e->last_foreign) HIP_TRY(hipEventRecord(e->ev_last, s));
     return JSP_OK;
+}
+
+// Entry of a call that enqueues on the engine's own stream: ordered after
+// earlier caller-stream work, and later calls order after it by an event on
+// the engine stream (no HIP call needed at its end).
+int use_engine_stream(jsp_engine* e) {
+    if (int rc = enter_stream(e, e->stream)) return rc;
+    return leave_stream(e, e->stream);
 }
 
 // Non-blocking: a compaction launch whose look-back timed out has written its
@@ -505,7 +541,7 @@ double svc_idle_ms() {
 // compaction, 1 fused), 0 = none.
 int svc_shape(jsp_engine* e) {
     if (e->svc_mode != JSP_SERVICE_AUTO || !e->have_topo || !e->have_snap || !e->have_cls ||
-        e->n_blocks > kSvcMaxBlocks)
+        e->n_blocks > kSvcMaxBlocks || e->svc.broken)
         return 0;
     if (compact_ok(e)) return 2;
     if (fused_ok(e) && !std::getenv("JSP_SERVICE_NO_FUSED")) return 1;
@@ -527,6 +563,7 @@ int svc_stop(jsp_engine* e) {
 // recovery path: post-delete snapshot uploaded, then placed -- finds it ready.
 int svc_suspend(jsp_engine* e) {
     e->svc.resume |= e->svc.running;
+    e->svc.broken = false;  // new geometry: the service may fit again
     return svc_stop(e);
 }
 
@@ -561,11 +598,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     HIP_TRY(v.granules.reserve(gpad + 3 * 128));  // granules, then bell, counter, n_runs on lines of their own
     // after everything the engine enqueued on any stream (the last stream's
     // event), without making later calls wait for the service
-    if (e->have_last) {
-        if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(e->ev_switch, e->last_stream));
-        HIP_TRY(hipStreamWaitEvent(v.stream, e->ev_switch, 0));
-    }
+    if (int rc = wait_prior(e, v.stream)) return rc;
     HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
     __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)v.seq, __ATOMIC_RELEASE);
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
@@ -594,21 +627,46 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     v.nb = nb;
     v.clk = e->timing;
     v.shape = shape;
+    // Every workgroup of the grid must be resident at once (tiles wait on each
+    // other and on the dispatcher): check the grid against what the CUs hold
+    // at this LDS size before launching; a service that cannot fit is not
+    // started and the launch path answers instead.
+    const jsp::TallyArgs ta0 = tally_args(e, nullptr, nullptr, e->L_total);
+    size_t lds = 0;
+    uint32_t grid = 0;
+    jsp::FusedArgs f{};
+    jsp::TallyArgs ta{};
     if (shape == 2) {
-        HIP_TRY(jsp::launch_service(tally_args(e, nullptr, nullptr, e->L_total), a, v.stream));
+        lds = jsp::compact_lds_bytes(e->blk_leaves);
+        grid = nb + 1;
     } else {
         const size_t cl = (size_t)std::max<uint32_t>(e->C, 1) * std::max<uint32_t>(e->L_total, 1);
         HIP_TRY(v.tally.reserve((cl + std::max<uint32_t>(e->L_total, 1)) * 4));
         uint32_t* cap = v.tally.as<uint32_t>();
-        jsp::TallyArgs ta = tally_args(e, cap, cap + cl, e->L_total);
+        ta = tally_args(e, cap, cap + cl, e->L_total);
         uint32_t* rc = v.runs.as<uint32_t>();
-        jsp::FusedArgs f = fused_args(e, ta, rc, rc + v.cap_runs, 0, 0, v.assign.as<int32_t>(), w + nb);
-        HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
+        f = fused_args(e, ta, rc, rc + v.cap_runs, 0, 0, v.assign.as<int32_t>(), w + nb);
+        lds = f.lds_bytes;
+        grid = nb * f.groups + 1;
     }
+    {
+        int per_cu = 0;
+        HIP_TRY(jsp::service_occupancy(ta0, shape, lds, &per_cu));
+        // the API answer can be one workgroup per CU high at high SGPR counts
+        // (MI355X_MICROARCH.md, Residency): keep that margin
+        const int64_t fit = (int64_t)std::max(per_cu > 1 ? per_cu - 1 : per_cu, 0) * e->n_cu;
+        if ((int64_t)grid > fit)
+            return set_err(JSP_ERANGE, "placement service needs %u co-resident workgroups; %d CUs hold %lld at %zu B "
+                                       "of LDS each", grid, e->n_cu, (long long)fit, lds);
+    }
+    if (shape == 2) HIP_TRY(jsp::launch_service(ta0, a, v.stream));
+    else HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
     v.running = true;
     e->acc.svc_starts += 1;
     // return once the dispatcher polls: a request posted now is answered
-    // without waiting for the launch
+    // without waiting for the launch (bounded: a dispatcher that cannot get a
+    // CU within 2 s means the grid is not co-resident)
+    const auto t_start = std::chrono::steady_clock::now();
     for (uint64_t spins = 1; __atomic_load_n(ready, __ATOMIC_ACQUIRE) != v.gen; ++spins) {
         if ((spins & 255) == 0) {
             const hipError_t q = hipStreamQuery(v.stream);
@@ -616,6 +674,10 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
                 v.running = false;
                 return set_err(JSP_EHIP, "placement service ended before it started polling: %s",
                                hipGetErrorString(q));
+            }
+            if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(2)) {
+                (void)svc_stop(e);
+                return set_err(JSP_EHIP, "placement service did not start polling within 2 s");
             }
         }
     }
@@ -645,6 +707,17 @@ int svc_wait(jsp_engine* e, uint32_t seq) {
     }
 }
 
+// The request number after q. Never 0 (the done words' initial value) or
+// kSvcStop, and never a value whose low 30 bits are 0: the compaction tiles
+// tag their look-back granules with seq & 0x3FFFFFFF (0 -> 1), so 2^30 would
+// share its tag with the request after it and a tile could take that request
+// predecessor's stale granule as current.
+uint32_t next_seq(uint32_t q) {
+    uint32_t s = q + 1;
+    while (s == 0 || s == jsp::kSvcStop || (s & 0x3FFFFFFFu) == 0) ++s;
+    return s;
+}
+
 // One placement through the service: J jobs of the engine's one class.
 int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
               int32_t* assign_out, uint32_t* placed) {
@@ -664,8 +737,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             std::memcpy(v.runs.as<uint32_t>(), run_class, (size_t)n_runs * 4);
             std::memcpy(v.runs.as<uint32_t>() + v.cap_runs, run_len, (size_t)n_runs * 4);
         }
-        seq = v.seq + 1;
-        if (seq == 0 || seq == jsp::kSvcStop) seq = 1;
+        seq = next_seq(v.seq);
         v.seq = seq;
         v.last = std::chrono::steady_clock::now();
         // second half first: the dispatcher reads both halves in one 16-byte load
@@ -804,10 +876,15 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
     auto* e = new (std::nothrow) jsp_engine();
     if (!e) return set_err(JSP_ENOMEM, "engine allocation failed");
     e->device = device_id;
+    e->n_cu = prop.multiProcessorCount;
     err = hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking);
     if (err != hipSuccess) {
         delete e;
         return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
+    }
+    if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming) != hipSuccess) {
+        delete e;
+        return set_err(JSP_EHIP, "hipEventCreate failed");
     }
     if (e->stats.reserve(16) != hipSuccess || hipMemset(e->stats.p, 0, 16) != hipSuccess) {
         delete e;
@@ -819,6 +896,10 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
     }
     std::memset(e->h_err.p, 0, 64);
     if (const char* v = std::getenv("JSP_SERVICE")) e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : JSP_SERVICE_AUTO;
+    // test hook: CUs the service may count on (stands in for a smaller GPU or a partition)
+    if (const char* v = std::getenv("JSP_SVC_CU_LIMIT")) e->n_cu = std::min<int>(e->n_cu, (int)std::strtol(v, nullptr, 10));
+    // test hook: the service's first request number (tests start it next to 2^30)
+    if (const char* v = std::getenv("JSP_SVC_SEQ0")) e->svc.seq = (uint32_t)std::strtoul(v, nullptr, 0);
     *out = e;
     return JSP_OK;
 }
@@ -873,7 +954,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
         return set_err(JSP_ERANGE, "topology has %u bitmap words over all levels; engine limit is %u (%u domains)",
                        off, jsp::kMaxTakenWords, jsp::kMaxTakenWords * 64);
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     jsp::TopoDev td{};
     td.K = K;
     for (uint32_t k = 0; k < K; ++k) {
@@ -952,7 +1033,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     }
     const uint32_t npad = ((N + 63) / 64) * 64 + 64;
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(e->labels.reserve((size_t)W * npad * 8));
     HIP_TRY(e->taints.reserve((size_t)npad * 4));
     HIP_TRY(e->freer.reserve((size_t)R * npad * 4));
@@ -1035,7 +1116,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
         }
     }
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->tmp_a, rows, n, s));
     if (labels) HIP_TRY(upload(e->tmp_b, labels, (size_t)e->W * n, s));
     if (taints) HIP_TRY(upload(e->tmp_c, taints, n, s));
@@ -1085,7 +1166,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
         woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
     }
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->cls, h.data(), h.size(), s));
     HIP_TRY(upload(e->word_off, woff.data(), woff.size(), s));
     HIP_TRY(e->feas.reserve((size_t)std::max<uint32_t>(woff[C], 1) * 8));
@@ -1107,8 +1188,11 @@ int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t l
     if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
     if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
     if (int rc = check_launch_error(e)) return rc;
-    if (int rc = enter_stream(e, pick(e, stream))) return rc;
-    return tally_impl(e, d_cap, d_occ, ld, pick(e, stream));
+    hipStream_t s = pick(e, stream);
+    if (int rc = enter_stream(e, s)) return rc;
+    const int rc = tally_impl(e, d_cap, d_occ, ld, s);
+    if (int lr = leave_stream(e, s)) return lr;
+    return rc;
 }
 
 int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
@@ -1122,8 +1206,11 @@ int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_oc
     if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
     if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
     if (int rc = check_launch_error(e)) return rc;
-    if (int rc = enter_stream(e, pick(e, stream))) return rc;
-    return assign_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
+    hipStream_t s = pick(e, stream);
+    if (int rc = enter_stream(e, s)) return rc;
+    const int rc = assign_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs, d_assign, s);
+    if (int lr = leave_stream(e, s)) return lr;
+    return rc;
 }
 
 int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
@@ -1136,8 +1223,11 @@ int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t*
     if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
     if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
     if (int rc = check_launch_error(e)) return rc;
-    if (int rc = enter_stream(e, pick(e, stream))) return rc;
-    return place_impl(e, d_run_class, d_run_len, n_runs, n_jobs, d_assign, pick(e, stream));
+    hipStream_t s = pick(e, stream);
+    if (int rc = enter_stream(e, s)) return rc;
+    const int rc = place_impl(e, d_run_class, d_run_len, n_runs, n_jobs, d_assign, s);
+    if (int lr = leave_stream(e, s)) return lr;
+    return rc;
 }
 
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
@@ -1157,7 +1247,16 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (!want_tally && svc_ok(e)) {
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
-        if (int rc = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed)) return rc;
+        if (svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed) != JSP_OK) {
+            // the service could not answer (not co-resident, left, or a request
+            // failed on the device): stop it, keep it off until the next upload,
+            // and answer this call on the launch path
+            (void)svc_stop(e);
+            e->svc.broken = true;
+            e->acc.svc_fallbacks += 1;
+            goto launch_path;
+        }
+        {
         const auto t2 = std::chrono::steady_clock::now();
         e->last_shape = e->svc.shape == 1 ? 4 : 3;
         if (stats) {
@@ -1172,10 +1271,12 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         e->acc.host_prep_us += us(t1 - t0).count();
         e->acc.host_wait_us += us(t2 - t1).count();
         return JSP_OK;
+        }
     }
+launch_path:
     hipStream_t s = e->stream;
     if (int rc = check_launch_error(e)) return rc;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     // runs in, assign[] and stats out through pinned mapped host memory: one
     // launch sequence, no DMA round trips. The single-launch shapes signal
     // completion through host words (wait_done); the others, and calls that
@@ -1251,7 +1352,7 @@ int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const 
     if (n == 0) return JSP_OK;
     if (!leader_rows || !levels || !domain_out) return set_err(JSP_EINVAL, "NULL buffer");
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->tmp_a, leader_rows, n, s));
     HIP_TRY(upload(e->tmp_b, levels, n, s));
     HIP_TRY(e->tmp_c.reserve((size_t)n * 4));
@@ -1276,7 +1377,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
         if (follower_off[i] > follower_off[i + 1]) return set_err(JSP_EINVAL, "follower_off not monotone at %u", i);
     if (M > 0 && !follower_domains) return set_err(JSP_EINVAL, "follower_domains is NULL");
     hipStream_t s = e->stream;
-    if (int rc = enter_stream(e, s)) return rc;
+    if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s));
     HIP_TRY(upload(e->tmp_b, levels, n_jobs, s));
     HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s));
@@ -1357,14 +1458,19 @@ int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (e->have_last && e->last_stream != e->stream) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    if (e->have_last && e->last_foreign) HIP_TRY(hipEventSynchronize(e->ev_last));
     return JSP_OK;
 }
 
 int jsp_engine_check(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
-    if (e->have_last) HIP_TRY(hipStreamSynchronize(e->last_stream));
+    // everything enqueued so far is ordered before the last call's work, so
+    // waiting for that (an engine-owned event, or the engine stream) suffices
+    if (e->have_last) {
+        if (e->last_foreign) HIP_TRY(hipEventSynchronize(e->ev_last));
+        else HIP_TRY(hipStreamSynchronize(e->stream));
+    }
     return check_launch_error(e);
 }
 

@@ -206,6 +206,9 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);
 hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
+// Workgroups of the resident service kernel (shape 2 compaction, 1 fused) of
+// this W/R that one CU holds at once with lds_bytes each (occupancy API).
+hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, int* blocks_per_cu);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
                        uint32_t topo_words, uint32_t fscr_words);
 // u64 words of the fused tail's upper-level feasibility scratch: one sum per

@@ -2519,6 +2519,17 @@ hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const Se
     JSP_DISPATCH_WR(launch_fused_service_wr, a, f, v, s)
 }
 
+template <int W, int R>
+static hipError_t service_occupancy_wr(const TallyArgs&, int shape, size_t lds_bytes, int* blocks) {
+    const void* fn = shape == 2 ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
+                                : reinterpret_cast<const void*>(&place_fused_service_kernel<W, R>);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fn, kTallyThreads, lds_bytes);
+}
+
+hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, int* blocks_per_cu) {
+    JSP_DISPATCH_WR(service_occupancy_wr, a, shape, lds_bytes, blocks_per_cu)
+}
+
 size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }
 
 

@@ -1,0 +1,48 @@
+# One parameterised GPU run (replaces the round-1/2 one-off scripts).
+#   bash scripts/gpu_run.sh TAG STEP [STEP ...]
+# Output goes to gpurun_out/TAG/. Steps, in the order given:
+#   tests     pytest -m gpu (one process, per-test timeout)
+#   smoke     __graft_entry__.smoke()
+#   bench     python bench.py (default flags) -> bench.json
+#   driver    python bench.py --gpus 1 --steps 20 --warmup 5 (the driver's flags) -> bench_driver.json
+#   ceiling   tools/bin/stream_ceiling (read / copy ceilings at the kernels' byte counts)
+#   probes    tools/svc_probe.py + tools/host_api_probe.py
+#   trace     rocprofv3 --kernel-trace --stats of the bench (no CPU legs)
+#   pmc       separate rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / SQ) on configs 2, 4, 5
+#   py:FILE   python FILE (a probe under tools/) -> FILE.txt
+# Every GPU step runs under its own time limit; the script stops at the first
+# failure, time-out or crash (nothing further touches the GPU).
+set -u
+TAG="$1"; shift
+cd "$GRAFT_REPO_ROOT"; R="$GRAFT_REPO_ROOT"; OUT="$R/gpurun_out/$TAG"; mkdir -p "$OUT"
+run() {  # run SECONDS LOG CMD...
+    local t="$1" log="$2"; shift 2
+    timeout -k 10 "$t" "$@" > "$log" 2>&1
+    local rc=$?
+    if [ $rc -ne 0 ]; then echo "FAILED ($rc): $*"; tail -40 "$log"; exit $rc; fi
+}
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case "$step" in
+    tests)   run 900 "$OUT/pytest_gpu.log" python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+             tail -2 "$OUT/pytest_gpu.log" ;;
+    smoke)   run 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"; cat "$OUT/smoke.log" ;;
+    bench)   run 500 "$OUT/bench.json" python bench.py; tail -c 600 "$OUT/bench.json" ;;
+    driver)  run 500 "$OUT/bench_driver.json" python bench.py --gpus 1 --steps 20 --warmup 5; tail -c 400 "$OUT/bench_driver.json" ;;
+    ceiling) run 120 "$OUT/stream_ceiling.json" tools/bin/stream_ceiling; cat "$OUT/stream_ceiling.json" ;;
+    probes)  run 200 "$OUT/svc_probe.txt" python3 tools/svc_probe.py 2000
+             run 240 "$OUT/host_api_phases.txt" python3 tools/host_api_probe.py ;;
+    trace)   ( cd /tmp && export TMPDIR=/tmp && run 500 "$OUT/bench_trace.log" rocprofv3 --kernel-trace --stats -d "$OUT/bench_trace" -o run --output-format csv -- python3 "$R/bench.py" --trials 100 --cold-trials 0 --cpu-seconds 0 ) || exit $?
+             python3 tools/summarize_prof.py "$OUT" > "$OUT/summary.txt" 2>&1 ;;
+    pmc)     ( cd /tmp && export TMPDIR=/tmp
+               for cfg in 2 4 5; do
+                 run 120 "$OUT/pmc_fetch$cfg.log" rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20
+                 run 120 "$OUT/pmc_write$cfg.log" rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20
+                 run 120 "$OUT/pmc_sq$cfg.log" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/pmc_sq$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20
+               done ) || exit $?
+             python3 tools/summarize_prof.py "$OUT" > "$OUT/summary.txt" 2>&1 ;;
+    py:*)    f="${step#py:}"; run 300 "$OUT/$(basename "$f").txt" python3 -u "$f"; tail -30 "$OUT/$(basename "$f").txt" ;;
+    *)       echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo all-done

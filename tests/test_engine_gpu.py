@@ -3,6 +3,8 @@ bit-exact on assign[], the per-(class, leaf) tallies and the occupancy
 counts, on BASELINE.json configs 1-5 and on ragged random snapshots; plus the
 invariants of SURVEY.md §8c and the edge cases of the reference's own tests
 (empty inputs, unplaceable jobs, maximum sizes)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -573,3 +575,51 @@ def test_tally_width_bound_is_erange(engine):
     engine.upload_classes([JobClass(pods=(1 << 21) - 1)])
     got = engine.place(np.zeros(1, dtype=np.uint32), want_tally=True)
     assert got.cap[0, 0] == ((1 << 21) - 1) * N and got.assign.tolist() == [0]
+
+
+def _loaded_hip_runtime():
+    """ctypes handle on the HIP runtime this process already uses (torch's
+    bundled libamdhip64, which libjsplace.so binds to): found in
+    /proc/self/maps, so no second runtime is loaded."""
+    import ctypes
+    for line in open("/proc/self/maps"):
+        path = line.split()[-1]
+        if "libamdhip64.so" in path and os.path.exists(path):
+            return ctypes.CDLL(path)
+    raise RuntimeError("libamdhip64 is not loaded")
+
+
+def test_caller_stream_destroyed_between_calls(engine):
+    """A caller's stream is used only inside the call it was given to: after
+    the caller synchronises and destroys it, later calls (host API, device
+    path on another stream, jsp_engine_check) never touch it (ADVICE r2:
+    enter_stream kept the handle and recorded events on it)."""
+    import ctypes
+
+    import torch
+    from jobset_amd.snapshot import job_runs
+    hip = _loaded_hip_runtime()
+    p = synth.config5()
+    engine.load(p)
+    a = O.place_c(p)[0]
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    for it in range(3):
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        out = torch.full((p.n_jobs,), -7, dtype=torch.int32, device="cuda")
+        engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s.value)
+        engine.check()  # waits on the engine's own event, not on the stream
+        assert hip.hipStreamSynchronize(s) == 0
+        assert hip.hipStreamDestroy(s) == 0
+        np.testing.assert_array_equal(out.cpu().numpy(), a)
+        # later calls: a patch (engine stream), the host API, the device path on torch's stream
+        engine.patch_rows(np.array([it], dtype=np.uint32), taints=p.nodes.taints[it:it + 1])
+        np.testing.assert_array_equal(engine.place(p.job_class).assign, a)
+        out2 = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+        engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out2.data_ptr(),
+                            torch.cuda.current_stream().cuda_stream)
+        engine.check()
+        np.testing.assert_array_equal(out2.cpu().numpy(), a)
+        engine.sync()

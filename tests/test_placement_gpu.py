@@ -350,6 +350,47 @@ def test_engine_bound_topology_boundary_cases(engine):
     assert e is None and m["spec"]["nodeSelector"] == {"rack": ""}
 
 
+def test_node_events_after_sync_take_node_get_path(engine):
+    """After a sync, a Node removed or relabelled in the cache must not be
+    answered from the (now stale) snapshot: the reference's live Node Get
+    gives "" + nil for a removed node and the new label value for a
+    relabelled one (pod_mutating_webhook.go:173-194, pod_controller.go:242-263).
+    Default, DefaultBatch and Reconcile stay identical to the Node-Get cache
+    until the next sync, which serves from the engine again."""
+    plain, bound = host.Cache(), host.Cache()
+    for c in (plain, bound):
+        rack_cluster(c)
+    bound.planner_new(engine, ["zone", "rack"], RES)
+    bound.planner_sync()
+    leaders = ["z0-r1-n2", "z1-r3-n0", "z0-r0-n0"]
+    all_pods = [webhook_pods("default", "ev", i, f"u{i}", "rack", leaders[i]) for i in range(3)]
+    for pods in all_pods:
+        for c in (plain, bound):
+            c.add_pod(pods[0])
+    # events after the sync: leader 0's node is deleted, leader 1's node moves rack
+    moved = node("z1-r3-n0", {"zone": "zone-1", "rack": "zone-1-rack-9", "kubernetes.io/hostname": "z1-r3-n0"})
+    for c in (plain, bound):
+        c.remove_node("z0-r1-n2")
+        c.add_node(moved)
+    followers = [p for pods in all_pods for p in pods[1:]]
+    want = [plain.Default(f) for f in followers]
+    assert [bound.Default(f) for f in followers] == want
+    assert bound.DefaultBatch(followers) == want
+    assert want[0][0]["spec"]["nodeSelector"] == {"rack": ""}
+    assert want[2][0]["spec"]["nodeSelector"] == {"rack": "zone-1-rack-9"}
+    for (p, _) in want:
+        for c in (plain, bound):
+            c.add_pod(p)
+    for pods in all_pods:
+        name = pods[0]["metadata"]["name"]
+        assert bound.Reconcile("default", name) == plain.Reconcile("default", name)
+    # the next sync brings the snapshot up to date: engine answers, same mutations
+    bound.planner_sync()
+    b0 = bound.stats()
+    assert bound.DefaultBatch(followers[4:]) == want[4:]
+    assert bound.stats()["engineCalls"] - b0["engineCalls"] == 1
+
+
 def test_label_nodes_is_deterministic(engine):
     """§8f row 4: the node-selector strategy's node patches from the engine's
     lowest-index assignment, replacing label_nodes.py's set-order mapping

@@ -275,3 +275,64 @@ def test_two_engines_with_services(svc_engine):
         e2.close()  # its service is running: destroy stops it
     for _ in range(10):
         np.testing.assert_array_equal(svc_engine.place(p2.job_class).assign, a2)
+
+
+def test_service_request_numbers_across_2_pow_30(monkeypatch):
+    """The compaction tiles tag their look-back granules with the request
+    number's low 30 bits: requests must never share a tag with the request
+    before them across 2^30. A service started at 2^30 - 3 answers
+    every request bit-exactly through the wrap."""
+    from jobset_amd.engine import Engine
+    monkeypatch.setenv("JSP_SVC_SEQ0", str((1 << 30) - 3))
+    e = Engine(0)
+    try:
+        p = synth.config2()
+        e.load(p)
+        a = O.place_c(p)[0]
+        call = e.host_placer(*job_runs(p.job_class))
+        for _ in range(12):
+            st = call()
+            assert st.fused == 3
+            np.testing.assert_array_equal(call.assign, a)
+        rng = np.random.default_rng(3)
+        for _ in range(4):  # the answers change between requests: stale granules would show
+            rows = np.sort(rng.choice(p.nodes.n_nodes, size=40, replace=False)).astype(np.uint32)
+            t = rng.integers(0, 2, size=40).astype(np.uint32)
+            e.patch_rows(rows, taints=t)
+            p.nodes.taints[rows] = t
+            got = e.place(p.job_class)
+            np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    finally:
+        e.close()
+
+
+def test_service_that_cannot_fit_falls_back(monkeypatch):
+    """Every workgroup of a service grid must be co-resident. On a GPU (or a
+    partition) with too few CUs for the grid -- JSP_SVC_CU_LIMIT stands in for
+    one -- the service is not started: the call is answered by the launch
+    path (same assign[]), counted once in jsp_timing.svc_fallbacks, and the
+    engine stays on the launch path until the next upload."""
+    from jobset_amd.engine import Engine
+    monkeypatch.setenv("JSP_SVC_CU_LIMIT", "2")  # read at engine creation
+    e = Engine(0)
+    try:
+        for cfg in (2, 5):
+            p = synth.CONFIGS[cfg]()
+            e.load(p)
+            a = O.place_c(p)[0]
+            e.timing(reset=True)
+            for _ in range(5):
+                got = e.place(p.job_class)
+                assert got.fused in (1, 2)  # launch shapes only
+                np.testing.assert_array_equal(got.assign, a)
+            assert e.timing(reset=True).svc_fallbacks == 1
+    finally:
+        e.close()
+    e = Engine(0)  # no limit: the same snapshot is served by the service
+    try:
+        p = synth.config2()
+        e.load(p)
+        got = e.place(p.job_class)
+        assert got.fused == 3 and e.timing(reset=True).svc_fallbacks == 0
+    finally:
+        e.close()
