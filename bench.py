@@ -52,11 +52,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level
 SHAPES = {0: "three launches (tally -> feas -> assign + expand)", 1: "fused single launch",
           2: "single-class compaction, one launch",
           3: "single-class compaction answered by the resident service (no launch per placement)",
-          4: "fused shape answered by the resident service (no launch per placement)"}
+          4: "fused shape answered by the resident service (no launch per placement)",
+          5: "split service: resident tiles tally and hand back per-domain feasibility, the host walks"}
 # the launch shape the device path (jsp_place_device) takes for a host-API shape
 DEVICE_SHAPE = {3: 2, 4: 1, 5: 1}
 KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel",
-          4: "place_fused_kernel"}
+          4: "place_fused_kernel", 5: "place_fused_kernel"}
 
 
 def tally_bytes(p) -> int:
@@ -486,6 +487,12 @@ def main() -> None:
             if cfg in (3, 5):
                 line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
                 line["host_api_cold_recovery"] = cold_recovery_latency(eng, pc, args.cold_trials // 2)
+                # A/B: the same placements with the walk on the GPU (the fused resident kernel)
+                eng.set_service(True, device_walk=True)
+                ab = host_api_latency(eng, pc, 200)
+                ab["shape"] = SHAPES[eng.place(pc.job_class).fused]
+                line["host_api_resident_device_walk"] = ab
+                eng.set_service(True)
             eng.service_stop()
             if world == 1 and args.cpu_seconds > 0:
                 from oracle import oracle as O

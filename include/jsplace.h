@@ -122,7 +122,8 @@ typedef struct jsp_stats {
     uint32_t runs;             /* replicated-job runs the assignment walked */
     uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction,
                                   3 one-class compaction answered by the resident service,
-                                  4 fused shape answered by the resident service */
+                                  4 fused shape answered by the resident service (walk on the GPU),
+                                  5 split service: resident tiles + the walk on the host */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
@@ -166,7 +167,11 @@ typedef struct jsp_timing {
  * torch.cuda.synchronize) waits for it to leave: call
  * jsp_engine_service_stop first. */
 #define JSP_SERVICE_OFF 0
-#define JSP_SERVICE_AUTO 1     /* default */
+#define JSP_SERVICE_AUTO 1     /* default: the multi-class / multi-level shapes are answered by the split
+                                  service -- resident tiles tally and hand back per-domain feasibility,
+                                  the host walks (stats.fused = 5) */
+#define JSP_SERVICE_DEVICE_WALK 2  /* as AUTO, but those shapes walk on the GPU too (the fused resident
+                                      kernel, stats.fused = 4); kept for A/B measurement */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);

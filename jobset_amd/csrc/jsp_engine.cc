@@ -15,6 +15,7 @@
 
 #include "../../include/jsplace.h"
 #include "jsp_internal.h"
+#include "jsp_walk.h"
 
 namespace {
 
@@ -104,6 +105,11 @@ struct jsp_engine {
     uint32_t t_off_h[JSP_MAX_LEVELS + 1] = {0, 0, 0, 0, 0};
     DevBuf t_off;
     jsp::TopoDev topo{};
+    // host copies of the hierarchy tables (the split service's host walk)
+    std::vector<uint32_t> h_fl[JSP_MAX_LEVELS], h_cs[JSP_MAX_LEVELS];
+    std::vector<int32_t> h_par[JSP_MAX_LEVELS];
+    std::vector<uint32_t> blk_l0, blk_l1;  // leaf range of each tally row block
+    jsp::HostWalk walk;
 
     // snapshot
     bool have_snap = false;
@@ -160,6 +166,9 @@ struct jsp_engine {
         HostBuf runs;    // fused shape: run_class[cap_runs] | run_len[cap_runs]
         DevBuf granules; // compaction granules | bell | counter | n_runs, one 128-B line each after the granules
         DevBuf tally;    // fused shape: the service's own cap[C][L] | occ[L] (device-path launches use e->cap)
+        HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
+        uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
+        uint32_t blocks = 0;           // row blocks the running service was started for
         uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
         int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
@@ -537,13 +546,45 @@ double svc_idle_ms() {
     return ms;
 }
 
+// Class groups of the split service's tiles: as the fused shape's (up to 4
+// groups of >= 2 classes, within 128 tiles); JSP_SPLIT_GROUPS overrides it
+// (A/B runs), capped by the co-resident tile limit.
+uint32_t split_groups(jsp_engine* e) {
+    uint32_t g = 1;
+    if (e->C > 2) {
+        const uint32_t by_c = std::min<uint32_t>(4, (e->C + 1) / 2);
+        const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
+        g = std::max<uint32_t>(1, std::min(by_c, by_t));
+    }
+    if (const char* v = std::getenv("JSP_SPLIT_GROUPS")) {
+        const long x = std::strtol(v, nullptr, 10);
+        if (x >= 1 && x <= (long)std::max<uint32_t>(e->C, 1)) g = (uint32_t)x;
+    }
+    while (g > 1 && e->n_blocks * g > kSvcMaxBlocks) --g;
+    return g;
+}
+
+// The split shape (tiles resident, the walk on the host): any snapshot whose
+// tiles fit the service, all classes in <= 16 per group.
+bool split_ok(jsp_engine* e) {
+    if (e->fused_mode != JSP_FUSED_AUTO || e->n_blocks == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total)
+        return false;
+    const uint32_t g = split_groups(e);
+    return e->n_blocks * g <= kSvcMaxBlocks && (e->C + g - 1) / g <= (uint32_t)jsp::kTallyClasses && e->C > 0;
+}
+
 // The shape the service would run for the engine's current state (2
-// compaction, 1 fused), 0 = none.
+// compaction, 3 split, 1 fused), 0 = none. The split shape answers
+// everything the fused one would (and more: no LDS limit on the walk);
+// JSP_SERVICE_DEVICE_WALK keeps the fused device walk (A/B), JSP_SPLIT_COMPACT=1
+// sends the one-class leaf shape through the split service too.
 int svc_shape(jsp_engine* e) {
-    if (e->svc_mode != JSP_SERVICE_AUTO || !e->have_topo || !e->have_snap || !e->have_cls ||
+    if (e->svc_mode == JSP_SERVICE_OFF || !e->have_topo || !e->have_snap || !e->have_cls ||
         e->n_blocks > kSvcMaxBlocks || e->svc.broken)
         return 0;
-    if (compact_ok(e)) return 2;
+    static const bool split_compact = [] { const char* v = std::getenv("JSP_SPLIT_COMPACT"); return v && v[0] == '1'; }();
+    if (compact_ok(e) && !(split_compact && split_ok(e))) return 2;
+    if (e->svc_mode == JSP_SERVICE_AUTO && split_ok(e)) return 3;
     if (fused_ok(e) && !std::getenv("JSP_SERVICE_NO_FUSED")) return 1;
     return 0;
 }
@@ -590,7 +631,17 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
         HIP_TRY(v.runs.reserve((size_t)cr * 8));
         v.cap_runs = cr;
     }
-    const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * nb + 3;
+    uint32_t n_tiles = nb;  // workgroups that answer (and write a done word), dispatcher excluded
+    if (shape == 3) {
+        v.groups = split_groups(e);
+        v.cpg = (e->C + v.groups - 1) / v.groups;
+        n_tiles = nb * v.groups;
+        const size_t sb = (size_t)n_tiles * (v.cpg + 1) * jsp::kSplitSlot * 8;
+        HIP_TRY(v.split.reserve(sb));
+        std::memset(v.split.p, 0, sb);
+        e->walk.set_tiles(e->blk_l0, e->blk_l1, v.groups, v.cpg);
+    }
+    const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3;
     HIP_TRY(v.words.reserve(nw * 4));
     std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
     HIP_TRY(v.box.reserve(64));
@@ -616,15 +667,16 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();
     a.done = w;
-    a.stats = w + nb;
-    a.err = w + nb + 2;
-    a.clk = e->timing && shape == 2 ? w + nb + 3 : nullptr;
+    a.stats = w + n_tiles;
+    a.err = w + n_tiles + 2;
+    a.clk = e->timing && shape == 2 ? w + n_tiles + 3 : nullptr;
     a.spin_limit = e->spin_limit;
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
     a.ready = ready;
     a.gen = v.gen;
     v.err_ack = 0;
-    v.nb = nb;
+    v.nb = n_tiles;
+    v.blocks = nb;
     v.clk = e->timing;
     v.shape = shape;
     // Every workgroup of the grid must be resident at once (tiles wait on each
@@ -636,9 +688,18 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     uint32_t grid = 0;
     jsp::FusedArgs f{};
     jsp::TallyArgs ta{};
+    jsp::SplitArgs sp{};
     if (shape == 2) {
         lds = jsp::compact_lds_bytes(e->blk_leaves);
         grid = nb + 1;
+    } else if (shape == 3) {
+        sp.groups = v.groups;
+        sp.cpg = v.cpg;
+        sp.C = e->C;
+        sp.out = v.split.as<uint64_t>();
+        sp.topo = e->topo;
+        lds = jsp::split_lds_bytes(v.cpg, e->blk_leaves);
+        grid = n_tiles + 1;
     } else {
         const size_t cl = (size_t)std::max<uint32_t>(e->C, 1) * std::max<uint32_t>(e->L_total, 1);
         HIP_TRY(v.tally.reserve((cl + std::max<uint32_t>(e->L_total, 1)) * 4));
@@ -660,6 +721,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
                                        "of LDS each", grid, e->n_cu, (long long)fit, lds);
     }
     if (shape == 2) HIP_TRY(jsp::launch_service(ta0, a, v.stream));
+    else if (shape == 3) HIP_TRY(jsp::launch_split_service(ta0, sp, a, v.stream));
     else HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
     v.running = true;
     e->acc.svc_starts += 1;
@@ -724,7 +786,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     auto& v = e->svc;
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
-    bool restart = !v.running || J > v.cap || v.clk != e->timing || v.nb != e->n_blocks || v.shape != shape ||
+    bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
                    (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
     uint32_t seq = 0;
@@ -753,6 +815,11 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         if (rc == kSvcGone) return set_err(JSP_EHIP, "placement service left before answering request %u", seq);
         if (rc) return rc;
         break;
+    }
+    if (v.shape == 3) {  // the tiles answered: the walk, into the caller's buffer
+        *placed = e->walk.place(v.split.as<uint64_t>(), run_class, run_len, n_runs, assign_out);
+        e->acc.svc_calls += 1;
+        return JSP_OK;
     }
     const uint32_t* w = v.words.as<uint32_t>();
     const uint32_t ew = __atomic_load_n(w + v.nb + 2, __ATOMIC_ACQUIRE);
@@ -895,7 +962,9 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         return set_err(JSP_ENOMEM, "error word");
     }
     std::memset(e->h_err.p, 0, 64);
-    if (const char* v = std::getenv("JSP_SERVICE")) e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : JSP_SERVICE_AUTO;
+    if (const char* v = std::getenv("JSP_SERVICE"))
+        e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : std::strcmp(v, "2") == 0 ? JSP_SERVICE_DEVICE_WALK
+                                                                                           : JSP_SERVICE_AUTO;
     // test hook: CUs the service may count on (stands in for a smaller GPU or a partition)
     if (const char* v = std::getenv("JSP_SVC_CU_LIMIT")) e->n_cu = std::min<int>(e->n_cu, (int)std::strtol(v, nullptr, 10));
     // test hook: the service's first request number (tests start it next to 2^30)
@@ -967,6 +1036,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
                 cs[d] = (uint32_t)(std::lower_bound(fl[k + 1].begin(), fl[k + 1].end(), fl[k][d]) - fl[k + 1].begin());
             HIP_TRY(upload(e->cs[k], cs.data(), cs.size(), s));
             td.cs[k] = e->cs[k].as<uint32_t>();
+            e->h_cs[k] = cs;
         }
         if (k > 0) {  // parent at level k-1 of each level-k domain (by its first leaf)
             std::vector<int32_t> par(std::max<uint32_t>(t->n_domains[k], 1));
@@ -974,11 +1044,14 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
                 par[d] = (int32_t)(std::upper_bound(fl[k - 1].begin(), fl[k - 1].end(), fl[k][d]) - fl[k - 1].begin()) - 1;
             HIP_TRY(upload(e->par[k], par.data(), par.size(), s));
             td.par[k] = e->par[k].as<int32_t>();
+            e->h_par[k] = par;
         }
     }
     HIP_TRY(upload(e->t_off, e->t_off_h, K + 1, s));
     HIP_TRY(hipStreamSynchronize(s));
     e->topo = td;
+    for (uint32_t k = 0; k < K; ++k) e->h_fl[k] = fl[k];
+    e->walk.set_topology(K, t->n_domains, e->h_fl, e->h_cs, e->h_par);
     e->K = K;
     for (uint32_t k = 0; k < JSP_MAX_LEVELS; ++k) e->D[k] = k < K ? t->n_domains[k] : 0;
     e->L_total = L;
@@ -1055,6 +1128,8 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     HIP_TRY(upload(e->leaf_start, ls, (size_t)NL + 1, s));
     std::vector<uint4> bt(blk.size() > 0 ? blk.size() - 1 : 0);
     for (size_t b = 0; b + 1 < blk.size(); ++b) bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
+    e->blk_l0.assign(blk.begin(), blk.end() - (blk.empty() ? 0 : 1));
+    e->blk_l1.assign(blk.begin() + (blk.empty() ? 0 : 1), blk.end());
     HIP_TRY(upload(e->blk, bt.data(), std::max<size_t>(bt.size(), 1), s));
     HIP_TRY(e->ticket.reserve(16));
     HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch tickets (tile draws, finished tiles)
@@ -1174,6 +1249,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
     HIP_TRY(e->occ.reserve((size_t)std::max<uint32_t>(e->L_total, 1) * 4));
     HIP_TRY(hipStreamSynchronize(s));
     e->cls_h.assign(h.begin(), h.begin() + C);
+    e->walk.set_classes(e->cls_h);
     e->C = C;
     e->feas_words = woff[C];
     e->have_cls = true;
@@ -1258,7 +1334,7 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         }
         {
         const auto t2 = std::chrono::steady_clock::now();
-        e->last_shape = e->svc.shape == 1 ? 4 : 3;
+        e->last_shape = e->svc.shape == 1 ? 4 : e->svc.shape == 3 ? 5 : 3;
         if (stats) {
             stats->jobs = J;
             stats->runs = n_runs;
@@ -1406,8 +1482,9 @@ int jsp_engine_set_fused(jsp_engine* e, int mode) {
 int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
-    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO) return set_err(JSP_EINVAL, "service mode %d", mode);
-    if (mode == JSP_SERVICE_OFF) {
+    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO && mode != JSP_SERVICE_DEVICE_WALK)
+        return set_err(JSP_EINVAL, "service mode %d", mode);
+    if (mode != e->svc_mode) {  // the running service's shape may change
         e->svc.resume = false;
         if (int rc = svc_stop(e)) return rc;
     }

@@ -167,6 +167,25 @@ struct ServiceArgs {
     unsigned long long* counter;        // device: finished tiles over all requests (fused shape)
 };
 
+// Split service (place_split_service_kernel): the fused shape's tiles stay
+// resident and hand the host, per request, only what the sequential greedy
+// needs -- per tile and class, the feasibility bits of its leaves (leaf-level
+// classes) or its partial capacity sums per upper-level domain (upper
+// classes), plus its leaves' occupancy bits -- through pinned host memory; the
+// host runs the O(J + C D / 64) walk.
+// Per tile, (cpg + 1) slots of 4 waves x kSplitWave u64: for a leaf-level
+// class word 0 of wave w's block is the ballot of leaves [64w, 64w+64) of
+// the tile; for an upper class word 0 is a record count n and words 1..n
+// records (domain << 32 | partial clamped capacity sum); slot cpg holds the
+// occupancy ballots (group-0 tiles only).
+constexpr uint32_t kSplitWave = 65;
+constexpr uint32_t kSplitSlot = 4 * kSplitWave;
+struct SplitArgs {
+    uint32_t groups, cpg, C;
+    uint64_t* out;  // host-mapped [n_tiles][(cpg + 1) * kSplitSlot]
+    TopoDev topo;
+};
+
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }
 constexpr uint32_t kFusedMaxWords = 6144;  // taken + feasibility words the fused tail keeps in LDS (48 KiB)
 constexpr uint32_t kFusedStage = 2048;     // ranks the fused tail stages per long-run step (8 KiB)
@@ -206,7 +225,9 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);
 hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
-// Workgroups of the resident service kernel (shape 2 compaction, 1 fused) of
+hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);
+size_t split_lds_bytes(uint32_t cpg, uint32_t la);
+// Workgroups of the resident service kernel (shape 2 compaction, 1 fused, 3 split) of
 // this W/R that one CU holds at once with lds_bytes each (occupancy API).
 hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, int* blocks_per_cu);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,

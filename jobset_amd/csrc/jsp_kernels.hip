@@ -2377,6 +2377,123 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
     }
 }
 
+// The split service (jsp_internal.h SplitArgs): the fused shape's tiles kept
+// resident, each answering a request with its feasibility ballots / partial
+// domain sums in pinned host memory and a done word; the host walks. One
+// workgroup per (row block, class group) tile + the dispatcher.
+// The tile's sums are in LDS after tally_block (cap_out == nullptr); for an
+// upper class the clamped per-leaf values min(cap, pods) are block-scanned
+// (exact: capsum >= pods iff the clamped sum is, and the clamped partial sums
+// of <= 256 leaves stay below 2^30) and every leaf that ends its level-k
+// domain inside the tile emits that domain's partial sum.
+__device__ __forceinline__ uint32_t leaf_ancestor(uint32_t leaf, uint32_t level, const TopoDev& topo) {
+    uint32_t d = leaf;
+    for (uint32_t k = topo.K - 1; k > level; --k) d = (uint32_t)topo.par[k][d];
+    return d;
+}
+
+__device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
+                                           uint32_t* lds, uint32_t* s_x) {
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int nc = (int)ag.nc;
+    JSP_LDS const DevClass* cls_l = lds_ptr(reinterpret_cast<const DevClass*>(lds));
+    JSP_LDS const uint32_t* s_acc = lds_ptr(lds + tally_acc_off(nc));
+    JSP_LDS uint32_t* s_pre = lds_ptr(s_x + 16);
+    const uint32_t la = ag.la;
+    const uint32_t l0 = bt.x, nl = bt.y - bt.x;
+    const bool in = (uint32_t)tid < nl;
+    const uint32_t K = sp.topo.K;
+    for (int c = 0; c < nc; ++c) {
+        const uint32_t level = to_sgpr(cls_l[c].level), pods = to_sgpr(cls_l[c].pods);
+        const uint32_t cap = in ? s_acc[c * la + tid] : 0u;
+        uint64_t* slot = out + (size_t)c * kSplitSlot + (size_t)wid * kSplitWave;
+        if (level + 1 == K) {
+            const uint64_t word = __ballot(in && cap >= pods);
+            if (lane == 0) __hip_atomic_store(slot, (unsigned long long)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            const uint32_t v = cap < pods ? cap : pods;
+            uint32_t total;
+            const uint32_t incl = block_excl_scan<kTallyThreads>(v, s_x + 4, &total) + v;
+            s_pre[tid] = incl;
+            __syncthreads();
+            bool last = false;
+            uint64_t rec = 0;
+            if (in) {
+                const uint32_t l = l0 + (uint32_t)tid;
+                const uint32_t d = leaf_ancestor(l, level, sp.topo);
+                const uint32_t beg = sp.topo.fl[level][d], end = sp.topo.fl[level][d + 1];
+                last = (uint32_t)tid + 1 == nl || l + 1 == end;
+                const uint32_t first = (beg > l0 ? beg : l0) - l0;
+                const uint32_t partial = incl - (first > 0 ? s_pre[first - 1] : 0u);
+                rec = ((uint64_t)d << 32) | partial;
+            }
+            const uint64_t m = __ballot(last);
+            if (last) __hip_atomic_store(slot + 1 + mbcnt64(m), (unsigned long long)rec, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0)
+                __hip_atomic_store(slot, (unsigned long long)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __syncthreads();  // s_pre and the scan scratch are rewritten by the next upper class
+        }
+    }
+    if (ag.do_occ) {
+        const uint32_t o = in ? s_acc[nc * la + tid] : 0u;
+        const uint64_t word = __ballot(in && o != 0u);
+        if (lane == 0)
+            __hip_atomic_store(out + (size_t)sp.cpg * kSplitSlot + (size_t)wid * kSplitWave, (unsigned long long)word,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(TallyArgs a, SplitArgs sp, ServiceArgs v) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const uint32_t tile = blockIdx.x;
+    const uint32_t n_tiles = a.n_blocks * sp.groups;
+    uint32_t* s_x = lds + tally_lds_words((int)sp.cpg, (int)sp.cpg + 1, (int)a.la);  // [0] seq [4..16) scan [16..) prefixes
+    if (tile == n_tiles) {
+        service_dispatch(v, s_x);
+        return;
+    }
+    const FusedTile ft = fused_tile(tile, sp.groups, sp.cpg, sp.C);
+    TallyArgs ag = a;
+    ag.c0 = ft.c0;
+    ag.nc = ft.nc;
+    ag.do_occ = ft.do_occ;
+    ag.cap_out = nullptr;  // the sums stay in LDS
+    const uint4 bt = a.blk[ft.blk];
+    uint64_t* out = sp.out + (size_t)tile * (sp.cpg + 1) * kSplitSlot;
+    uint32_t seq = v.seq0;
+    while (true) {
+        if (threadIdx.x == 0) {
+            uint32_t next = 0;  // 0: leave
+            const uint64_t t0 = wall_clock64();
+            while (true) {
+                const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t q = (uint32_t)m;
+                if (q == kSvcStop) break;
+                if (q != seq && q != 0) {
+                    next = q;
+                    break;
+                }
+                if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_x[0] = next;
+        }
+        __syncthreads();
+        const uint32_t next = s_x[0];
+        if (next == 0) return;
+        tally_block<W, R, false, true>(ag, ft.blk, lds);
+        split_emit(ag, sp, bt, out, lds, s_x);
+        signal_host(v.done + tile, next, false);
+        // drop this CU's L1 lines before the next request (patches come from
+        // other launches), off the request path
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        seq = next;
+        __syncthreads();  // s_x and the tally carve are rewritten by the next request
+    }
+}
+
 // ----------------------------------------------------------------- A5 / A9 batch kernels
 __device__ __forceinline__ uint32_t upper_bound_u32(const uint32_t* a, uint32_t n, uint32_t x) {
     uint32_t lo = 0, hi = n;
@@ -2519,10 +2636,27 @@ hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const Se
     JSP_DISPATCH_WR(launch_fused_service_wr, a, f, v, s)
 }
 
+size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
+    return sizeof(uint32_t) * ((size_t)tally_lds_words((int)cpg, (int)cpg + 1, (int)la) + 16 + kTallyThreads + 4);
+}
+
+template <int W, int R>
+static hipError_t launch_split_service_wr(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v,
+                                          hipStream_t s) {
+    hipLaunchKernelGGL((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups + 1), dim3(kTallyThreads),
+                       split_lds_bytes(sp.cpg, a.la), s, a, sp, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_split_service_wr, a, sp, v, s)
+}
+
 template <int W, int R>
 static hipError_t service_occupancy_wr(const TallyArgs&, int shape, size_t lds_bytes, int* blocks) {
-    const void* fn = shape == 2 ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
-                                : reinterpret_cast<const void*>(&place_fused_service_kernel<W, R>);
+    const void* fn = shape == 2   ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
+                     : shape == 3 ? reinterpret_cast<const void*>(&place_split_service_kernel<W, R>)
+                                  : reinterpret_cast<const void*>(&place_fused_service_kernel<W, R>);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fn, kTallyThreads, lds_bytes);
 }
 

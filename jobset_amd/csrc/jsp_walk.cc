@@ -1,0 +1,256 @@
+// jsp_walk.cc — host half of the split placement service (jsp_walk.h).
+//
+// Feasibility: a leaf-level class's domain (leaf) is feasible
+// when its capacity covers the job's pods and no foreign exclusive job covers
+// one of its rows: the tiles' ballots give the first, the group-0 tiles'
+// occupancy ballots the second. An upper-level class's domain is feasible
+// when the sum over its leaves of min(cap, pods) reaches pods (the tiles'
+// clamped partial sums per domain, added here) and none of its leaves is
+// occupied. The walk is the lowest-index rule of oracle/cpu_ref.c: jobs in
+// global order, each takes the lowest feasible domain at its class's level
+// not yet taken; taking a domain takes its ancestors and descendants.
+#include "jsp_walk.h"
+
+#include <algorithm>
+#include <cstring>
+
+namespace jsp {
+
+namespace {
+
+inline void or_bits(uint64_t* g, uint32_t pos, uint64_t x) {
+    const uint32_t w = pos >> 6, b = pos & 63u;
+    g[w] |= x << b;
+    if (b != 0) g[w + 1] |= x >> (64u - b);
+}
+
+inline void set_range(uint64_t* t, uint32_t lo, uint32_t hi) {
+    while (lo < hi) {
+        const uint32_t w = lo >> 6, b = lo & 63u;
+        const uint32_t n = (hi - lo) < (64u - b) ? (hi - lo) : (64u - b);
+        t[w] |= (n == 64u) ? ~0ull : (((1ull << n) - 1ull) << b);
+        lo += n;
+    }
+}
+
+// any bit of g in [lo, hi)
+inline bool any_bits(const uint64_t* g, uint32_t lo, uint32_t hi) {
+    while (lo < hi) {
+        const uint32_t w = lo >> 6, b = lo & 63u;
+        const uint32_t n = (hi - lo) < (64u - b) ? (hi - lo) : (64u - b);
+        const uint64_t m = (n == 64u) ? ~0ull : (((1ull << n) - 1ull) << b);
+        if (g[w] & m) return true;
+        lo += n;
+    }
+    return false;
+}
+
+}  // namespace
+
+void HostWalk::set_topology(uint32_t K, const uint32_t* D, const std::vector<uint32_t>* fl,
+                            const std::vector<uint32_t>* cs, const std::vector<int32_t>* par) {
+    K_ = K;
+    uint32_t off = 0;
+    toff_.assign(K + 1, 0);
+    for (uint32_t k = 0; k < kMaxLevels; ++k) {
+        D_[k] = k < K ? D[k] : 0;
+        fl_[k] = k < K ? fl[k] : std::vector<uint32_t>();
+        cs_[k] = k + 1 < K ? cs[k] : std::vector<uint32_t>();
+        par_[k] = k >= 1 && k < K ? par[k] : std::vector<int32_t>();
+        if (k < K) {
+            toff_[k] = off;
+            off += (D_[k] + 63) / 64;
+        }
+    }
+    toff_[K] = off;
+    L_ = D_[K - 1];
+    taken_.assign(off + 1, 0);
+    occ_lvl_.assign(off + 1, 0);
+    occ_.assign((L_ + 63) / 64 + 1, 0);
+}
+
+void HostWalk::set_classes(const std::vector<DevClass>& cls) {
+    C_ = (uint32_t)cls.size();
+    level_.resize(C_);
+    pods_.resize(C_);
+    woff_.assign(C_ + 1, 0);
+    uoff_.assign(C_ + 1, 0);
+    any_upper_ = false;
+    for (uint32_t c = 0; c < C_; ++c) {
+        level_[c] = cls[c].level;
+        pods_[c] = cls[c].pods;
+        const uint32_t D = D_[level_[c]];
+        woff_[c + 1] = woff_[c] + (D + 63) / 64;
+        const bool upper = level_[c] + 1 < K_;
+        uoff_[c + 1] = uoff_[c] + (upper ? D : 0u);
+        any_upper_ |= upper;
+    }
+    feas_.assign(woff_[C_] + 1, 0);
+    sums_.assign(uoff_[C_] + 1, 0);
+    cursor_.assign(C_ + 1, 0);
+}
+
+void HostWalk::set_tiles(const std::vector<uint32_t>& blk_l0, const std::vector<uint32_t>& blk_l1, uint32_t groups,
+                         uint32_t cpg) {
+    l0_ = blk_l0;
+    l1_ = blk_l1;
+    groups_ = groups;
+    cpg_ = cpg;
+}
+
+void HostWalk::build_feasibility(const uint64_t* slots) {
+    const size_t tile_words = (size_t)(cpg_ + 1) * kSplitSlot;
+    const uint32_t nb = (uint32_t)l0_.size();
+    // occupied leaves, from the group-0 tiles
+    std::fill(occ_.begin(), occ_.end(), 0ull);
+    for (uint32_t b = 0; b < nb; ++b) {
+        const uint64_t* s = slots + (size_t)(b * groups_) * tile_words + (size_t)cpg_ * kSplitSlot;
+        const uint32_t nl = l1_[b] - l0_[b];
+        for (uint32_t w = 0; 64 * w < nl; ++w) {
+            const uint64_t x = s[w * kSplitWave];
+            if (x) or_bits(occ_.data(), l0_[b] + 64 * w, x);
+        }
+    }
+    // occupied domains above the leaves (only levels some class places at)
+    if (any_upper_) {
+        std::fill(occ_lvl_.begin(), occ_lvl_.end(), 0ull);
+        for (uint32_t k = 0; k + 1 < K_; ++k) {
+            bool used = false;
+            for (uint32_t c = 0; c < C_ && !used; ++c) used = level_[c] == k;
+            if (!used) continue;
+            uint64_t* o = occ_lvl_.data() + toff_[k];
+            const uint32_t* fl = fl_[k].data();
+            for (uint32_t d = 0; d < D_[k]; ++d)
+                if (any_bits(occ_.data(), fl[d], fl[d + 1])) o[d >> 6] |= 1ull << (d & 63);
+        }
+    }
+    std::fill(feas_.begin(), feas_.end(), 0ull);
+    for (uint32_t c = 0; c < C_; ++c) {
+        const uint32_t g = c / cpg_, j = c % cpg_, k = level_[c], pods = pods_[c];
+        uint64_t* F = feas_.data() + woff_[c];
+        if (k + 1 == K_) {
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words + (size_t)j * kSplitSlot;
+                const uint32_t nl = l1_[b] - l0_[b];
+                for (uint32_t w = 0; 64 * w < nl; ++w) {
+                    const uint64_t x = s[w * kSplitWave];
+                    if (x) or_bits(F, l0_[b] + 64 * w, x);
+                }
+            }
+            const uint32_t nw = woff_[c + 1] - woff_[c];
+            for (uint32_t w = 0; w < nw; ++w) F[w] &= ~occ_[w];
+        } else {
+            uint64_t* S = sums_.data() + uoff_[c];
+            std::fill(S, S + D_[k], 0ull);
+            for (uint32_t b = 0; b < nb; ++b) {
+                const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words + (size_t)j * kSplitSlot;
+                const uint32_t nl = l1_[b] - l0_[b];
+                for (uint32_t w = 0; 64 * w < nl; ++w) {
+                    const uint64_t* q = s + w * kSplitWave;
+                    const uint32_t n = (uint32_t)std::min<uint64_t>(q[0], 64);
+                    for (uint32_t i = 0; i < n; ++i) {
+                        const uint64_t r = q[1 + i];
+                        const uint32_t d = (uint32_t)(r >> 32);
+                        if (d < D_[k]) S[d] += (uint32_t)r;
+                    }
+                }
+            }
+            const uint64_t* O = occ_lvl_.data() + toff_[k];
+            for (uint32_t d = 0; d < D_[k]; ++d)
+                if (S[d] >= pods && !((O[d >> 6] >> (d & 63)) & 1ull)) F[d >> 6] |= 1ull << (d & 63);
+        }
+    }
+}
+
+void HostWalk::take(uint32_t d, uint32_t k) {
+    taken_[toff_[k] + (d >> 6)] |= 1ull << (d & 63);
+    if (K_ == 1) return;
+    if (fl_[k][d] == fl_[k][d + 1]) return;  // an empty domain intersects nothing (never feasible)
+    uint32_t dd = d;
+    for (int kk = (int)k - 1; kk >= 0; --kk) {
+        dd = (uint32_t)par_[kk + 1][dd];
+        taken_[toff_[kk] + (dd >> 6)] |= 1ull << (dd & 63);
+    }
+    uint32_t lo = d, hi = d + 1;
+    for (uint32_t kk = k + 1; kk < K_; ++kk) {
+        lo = cs_[kk - 1][lo];
+        hi = cs_[kk - 1][hi];
+        set_range(taken_.data() + toff_[kk], lo, hi);
+    }
+}
+
+uint32_t HostWalk::place(const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                         int32_t* assign) {
+    build_feasibility(slots);
+    std::fill(taken_.begin(), taken_.end(), 0ull);
+    std::fill(cursor_.begin(), cursor_.end(), 0u);
+    uint32_t placed = 0;
+    size_t j = 0;
+    for (uint32_t r = 0; r < n_runs; ++r) {
+        const uint32_t c = run_class[r], k = level_[c], D = D_[k], nw = (D + 63) / 64;
+        const uint64_t* F = feas_.data() + woff_[c];
+        const uint64_t* T = taken_.data() + toff_[k];
+        for (uint32_t i = 0; i < run_len[r]; ++i, ++j) {
+            const uint32_t cur = cursor_[c];
+            if (cur >= D) {
+                assign[j] = -1;
+                continue;
+            }
+            uint32_t w = cur >> 6;
+            uint64_t bits = F[w] & ~T[w] & (~0ull << (cur & 63));
+            while (bits == 0 && ++w < nw) bits = F[w] & ~T[w];
+            if (bits == 0) {
+                cursor_[c] = D;
+                assign[j] = -1;
+                continue;
+            }
+            const uint32_t d = w * 64 + (uint32_t)__builtin_ctzll(bits);
+            assign[j] = (int32_t)d;
+            cursor_[c] = d + 1;
+            ++placed;
+            take(d, k);
+        }
+    }
+    return placed;
+}
+
+}  // namespace jsp
+
+// Internal entry for the CPU tests of the host walk (tests/test_host_walk.py):
+// not part of include/jsplace.h. The hierarchy tables are derived from
+// first_leaf as jsp_topology_upload derives them.
+extern "C" int jspi_walk_test(uint32_t K, const uint32_t* D, const uint32_t* const* first_leaf, uint32_t C,
+                              const uint32_t* cls_level, const uint32_t* cls_pods, uint32_t n_blocks,
+                              const uint32_t* blk_l0, const uint32_t* blk_l1, uint32_t groups, uint32_t cpg,
+                              const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len,
+                              uint32_t n_runs, int32_t* assign) {
+    using jsp::kMaxLevels;
+    if (K < 1 || K > kMaxLevels) return -1;
+    std::vector<uint32_t> fl[kMaxLevels], cs[kMaxLevels];
+    std::vector<int32_t> par[kMaxLevels];
+    for (uint32_t k = 0; k < K; ++k) fl[k].assign(first_leaf[k], first_leaf[k] + D[k] + 1);
+    for (uint32_t k = 0; k < K; ++k) {
+        if (k + 1 < K) {
+            cs[k].resize(D[k] + 1);
+            for (uint32_t d = 0; d <= D[k]; ++d)
+                cs[k][d] = (uint32_t)(std::lower_bound(fl[k + 1].begin(), fl[k + 1].end(), fl[k][d]) - fl[k + 1].begin());
+        }
+        if (k > 0) {
+            par[k].resize(std::max<uint32_t>(D[k], 1));
+            for (uint32_t d = 0; d < D[k]; ++d)
+                par[k][d] = (int32_t)(std::upper_bound(fl[k - 1].begin(), fl[k - 1].end(), fl[k][d]) - fl[k - 1].begin()) - 1;
+        }
+    }
+    std::vector<jsp::DevClass> cls(C);
+    for (uint32_t c = 0; c < C; ++c) {
+        std::memset(&cls[c], 0, sizeof cls[c]);
+        cls[c].level = cls_level[c];
+        cls[c].pods = cls_pods[c];
+    }
+    jsp::HostWalk w;
+    w.set_topology(K, D, fl, cs, par);
+    w.set_classes(cls);
+    w.set_tiles(std::vector<uint32_t>(blk_l0, blk_l0 + n_blocks), std::vector<uint32_t>(blk_l1, blk_l1 + n_blocks),
+                groups, cpg);
+    return (int)w.place(slots, run_class, run_len, n_runs, assign);
+}

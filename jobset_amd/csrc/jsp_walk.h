@@ -1,0 +1,59 @@
+// jsp_walk.h — host half of the split placement service: the lowest-index
+// 1:1 greedy over the feasibility the
+// resident tiles hand back. The tiles do the streaming part (predicate +
+// capacity tally over every node row, per-leaf feasibility, partial sums per
+// upper-level domain); what is left is sequential across jobs and small
+// (O(J + C D / 64) word operations), so it runs on the host, next to the
+// caller, instead of on one GPU wave.
+#pragma once
+#include <stdint.h>
+
+#include <vector>
+
+#include "jsp_internal.h"
+
+namespace jsp {
+
+class HostWalk {
+public:
+    // topology: first_leaf per level (identity at the leaves), child_start
+    // per level k < K-1, parent per level k >= 1 (the engine's upload tables)
+    void set_topology(uint32_t K, const uint32_t* D, const std::vector<uint32_t>* fl,
+                      const std::vector<uint32_t>* cs, const std::vector<int32_t>* par);
+    // classes: level and pods of each (the engine's class upload)
+    void set_classes(const std::vector<DevClass>& cls);
+    // tiles of the split service: row block leaf ranges (blk table, first and
+    // end leaf per block), class groups and classes per group
+    void set_tiles(const std::vector<uint32_t>& blk_l0, const std::vector<uint32_t>& blk_l1, uint32_t groups,
+                   uint32_t cpg);
+
+    // One request: feasibility from the tiles' slots (jsp_internal.h
+    // SplitArgs), then the walk over runs in global order. Returns the
+    // number of placed jobs; assign[j] = domain at the job's class level or -1.
+    uint32_t place(const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                   int32_t* assign);
+
+    // The feasibility bitmaps of the last request (tests / diagnostics):
+    // words [woff[c], woff[c+1]) of class c.
+    const std::vector<uint64_t>& feas() const { return feas_; }
+
+private:
+    void build_feasibility(const uint64_t* slots);
+    void take(uint32_t d, uint32_t k);
+
+    uint32_t K_ = 0, L_ = 0, C_ = 0, groups_ = 1, cpg_ = 1;
+    uint32_t D_[kMaxLevels] = {0, 0, 0, 0};
+    std::vector<uint32_t> fl_[kMaxLevels], cs_[kMaxLevels];
+    std::vector<int32_t> par_[kMaxLevels];
+    std::vector<uint32_t> level_, pods_, woff_, toff_, uoff_;
+    std::vector<uint32_t> l0_, l1_;          // per row block
+    std::vector<uint64_t> occ_;              // occupied leaves (bitmap)
+    std::vector<uint64_t> occ_lvl_;          // occupied domains per level above the leaves (toff_ layout)
+    std::vector<uint64_t> feas_;             // feasibility words of every class (woff_ layout)
+    std::vector<uint64_t> sums_;             // clamped capacity sums of every upper class's domains (uoff_ layout)
+    std::vector<uint64_t> taken_;            // taken domains per level (toff_ layout)
+    std::vector<uint32_t> cursor_;           // per class: first domain not yet passed
+    bool any_upper_ = false;
+};
+
+}  // namespace jsp

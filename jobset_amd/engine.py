@@ -33,7 +33,7 @@ class PlaceResult:
     placed: int
     runs: int
     wall_us: float
-    fused: int = 0               # launch shape: 0 three launches, 1 fused tail, 2 one-class compaction, 3/4 the resident service (compaction / fused)
+    fused: int = 0               # launch shape: 0 three launches, 1 fused tail, 2 one-class compaction, 3/4 the resident service (compaction / fused), 5 the split service (host walk)
 
 
 class Engine:
@@ -206,10 +206,14 @@ class Engine:
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
-    def set_service(self, enable: bool) -> None:
-        """Resident placement service for host-API compaction placements
-        (jsp_engine_set_service; on by default)."""
-        check(self._lib.jsp_engine_set_service(self._h, native.JSP_SERVICE_AUTO if enable else native.JSP_SERVICE_OFF))
+    def set_service(self, enable: bool, device_walk: bool = False) -> None:
+        """Resident placement service for host-API placements
+        (jsp_engine_set_service; on by default). device_walk: the
+        multi-class shapes walk on the GPU (fused resident kernel) instead of
+        the split service's host walk (A/B)."""
+        mode = native.JSP_SERVICE_OFF if not enable else (
+            native.JSP_SERVICE_DEVICE_WALK if device_walk else native.JSP_SERVICE_AUTO)
+        check(self._lib.jsp_engine_set_service(self._h, mode))
 
     def service_stop(self) -> None:
         """Stop the resident service now (before a device-wide synchronize)."""

@@ -194,27 +194,41 @@ def test_service_after_device_path_and_patch(svc_engine):
 
 
 # ---------------------------------------------------------------- fused shape (cfg3, cfg5)
+# Two resident forms: the split service (default: tiles hand back per-domain
+# feasibility, the host walks; stats.fused 5) and the fused service (the walk
+# on the GPU by the tile that finished last; stats.fused 4).
+WALKS = [pytest.param(False, id="host-walk"), pytest.param(True, id="device-walk")]
+
+
+def walk_shape(device_walk):
+    return 4 if device_walk else 5
+
+
+@pytest.mark.parametrize("device_walk", WALKS)
 @pytest.mark.parametrize("cfg", [3, 5])
-def test_fused_service_configs(svc_engine, cfg):
-    """The fused shape resident: several classes / levels, runs through pinned
-    memory, the tail on the tile that finished last; 100 requests each."""
+def test_fused_service_configs(svc_engine, cfg, device_walk):
+    """The multi-class shape resident: several classes / levels, 100 requests
+    each, in both forms."""
+    svc_engine.set_service(True, device_walk=device_walk)
     p = synth.CONFIGS[cfg]()
     svc_engine.load(p)
     a = O.place_c(p)[0]
     call = svc_engine.host_placer(*job_runs(p.job_class))
     for _ in range(100):
         st = call()
-        assert st.fused == 4
+        assert st.fused == walk_shape(device_walk)
         np.testing.assert_array_equal(call.assign, a)
         assert st.placed == int((a >= 0).sum())
     rc, rl = job_runs(p.job_class)
     assert st.runs == rc.shape[0]
 
 
+@pytest.mark.parametrize("device_walk", WALKS)
 @pytest.mark.parametrize("seed", range(40))
-def test_fused_service_random_parity(svc_engine, seed):
-    """Ragged random snapshots in their own shape (the fused service when the
+def test_fused_service_random_parity(svc_engine, seed, device_walk):
+    """Ragged random snapshots in their own shape (a resident service when the
     snapshot is small enough), the job order changing between requests."""
+    svc_engine.set_service(True, device_walk=device_walk)
     p = synth.random_problem(seed)
     svc_engine.load(p)
     a = O.place_c(p)[0]
@@ -229,10 +243,12 @@ def test_fused_service_random_parity(svc_engine, seed):
     np.testing.assert_array_equal(ref.assign, a)
 
 
-def test_fused_service_patch_and_device_path(svc_engine):
+@pytest.mark.parametrize("device_walk", WALKS)
+def test_fused_service_patch_and_device_path(svc_engine, device_walk):
     """cfg5 resident while device-path launches (their own tally buffers) and
     patches interleave with its requests."""
     import torch
+    svc_engine.set_service(True, device_walk=device_walk)
     p = synth.config5()
     svc_engine.load(p)
     rc, rl = job_runs(p.job_class)
@@ -243,7 +259,7 @@ def test_fused_service_patch_and_device_path(svc_engine):
     rng = np.random.default_rng(5)
     for step in range(20):
         got = svc_engine.place(p.job_class)
-        assert got.fused == 4
+        assert got.fused == walk_shape(device_walk)
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
         svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
                                 side.cuda_stream)
@@ -268,7 +284,7 @@ def test_two_engines_with_services(svc_engine):
         for _ in range(50):
             g2 = svc_engine.place(p2.job_class)
             g5 = e2.place(q5.job_class)
-            assert g2.fused == 3 and g5.fused == 4
+            assert g2.fused == 3 and g5.fused == 5
             np.testing.assert_array_equal(g2.assign, a2)
             np.testing.assert_array_equal(g5.assign, a5)
     finally:
@@ -328,6 +344,7 @@ def test_service_that_cannot_fit_falls_back(monkeypatch):
             assert e.timing(reset=True).svc_fallbacks == 1
     finally:
         e.close()
+    monkeypatch.delenv("JSP_SVC_CU_LIMIT")
     e = Engine(0)  # no limit: the same snapshot is served by the service
     try:
         p = synth.config2()
