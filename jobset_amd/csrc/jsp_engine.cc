@@ -116,6 +116,8 @@ struct jsp_engine {
     uint32_t N = 0, npad = 0, W = 0, R = 0, leaf_begin = 0, n_leaves = 0, max_leaf_rows = 0;
     uint32_t blk_leaves = 4;  // most leaves any tally workgroup owns, rounded up to 4 (LDS tally stride)
     DevBuf labels, taints, freer, excl, leaf_start, blk;
+    DevBuf wtiles;              // wave tiles of the three-launch tally (tally_wave_kernel)
+    uint32_t n_wtiles = 0;
     uint32_t n_blocks = 0;
     uint32_t fast_res = 0;  // bit r: every free[r] < 2^31 (upload: computed; patches only clear bits)
     uint32_t epoch = 0;  // compaction launches so far (granule tags)
@@ -153,6 +155,8 @@ struct jsp_engine {
     bool last_foreign = false;          // the last call enqueued on a caller's stream
     hipEvent_t ev_switch = nullptr;     // recorded on the engine stream
     hipEvent_t ev_last = nullptr;       // recorded on the last caller stream, at the end of its call
+    HostBuf mark;                       // stream-marker word (JSP_STREAM_MARK=value): written by the caller's
+    uint64_t mark_seq = 0;              //   stream at the end of a device call, waited on by the next stream
 
     // resident placement service: the compaction shape kept on the GPU
     // between host-API placements (place_service_kernel), fed by a host-mapped
@@ -224,10 +228,28 @@ constexpr uint32_t kFusedMaxBlocks = 256;
 // stream): the engine stream's work through an event recorded on it now, a
 // caller stream's through ev_last, recorded at the end of the call that used
 // it (that stream itself is never touched again: it may be gone).
+// How the end of a device call on a caller's stream is marked (A/B,
+// JSP_STREAM_MARK): 0 an engine-owned event (default), 1 a stream write of a
+// host-mapped sequence word that later streams wait on, 2 nothing (unsafe:
+// measurement only).
+int stream_mark_mode() {
+    static const int m = [] {
+        const char* v = std::getenv("JSP_STREAM_MARK");
+        if (!v) return 0;
+        if (std::strcmp(v, "value") == 0) return 1;
+        if (std::strcmp(v, "none") == 0) return 2;
+        return 0;
+    }();
+    return m;
+}
+
 int wait_prior(jsp_engine* e, hipStream_t s) {
     if (!e->have_last) return JSP_OK;
     if (e->last_foreign) {
-        HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
+        const int mm = stream_mark_mode();
+        if (mm == 0) HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
+        else if (mm == 1)
+            HIP_TRY(hipStreamWaitValue64(s, e->mark.p, e->mark_seq, hipStreamWaitValueGte, ~0ull));
     } else {
         if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(e->ev_switch, e->stream));
@@ -250,7 +272,28 @@ int leave_stream(jsp_engine* e, hipStream_t s) {
     e->last_stream = s;
     e->have_last = true;
     e->last_foreign = s != e->stream;
-    if (e->last_foreign) HIP_TRY(hipEventRecord(e->ev_last, s));
+    if (e->last_foreign) {
+        const int mm = stream_mark_mode();
+        if (mm == 0) {
+            HIP_TRY(hipEventRecord(e->ev_last, s));
+        } else if (mm == 1) {
+            if (!e->mark.p) {
+                HIP_TRY(e->mark.reserve(64));
+                std::memset(e->mark.p, 0, 64);
+            }
+            HIP_TRY(hipStreamWriteValue64(s, e->mark.p, ++e->mark_seq, 0));
+        }
+    }
+    return JSP_OK;
+}
+
+// Host wait for the last caller-stream call's work.
+int wait_last_foreign(jsp_engine* e) {
+    const int mm = stream_mark_mode();
+    if (mm == 0) HIP_TRY(hipEventSynchronize(e->ev_last));
+    else if (mm == 1)
+        while (__atomic_load_n(e->mark.as<uint64_t>(), __ATOMIC_ACQUIRE) < e->mark_seq) __builtin_ia32_pause();
+    else HIP_TRY(hipDeviceSynchronize());
     return JSP_OK;
 }
 
@@ -374,16 +417,32 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
     return a;
 }
 
+// Workgroups of the wave-tile tally: JSP_TALLY_WPS waves per SIMD (default 2)
+// over the CUs, never more than the tiles need.
+uint32_t tally_wave_grid(jsp_engine* e) {
+    static const uint32_t wps = [] {
+        const char* v = std::getenv("JSP_TALLY_WPS");
+        const long x = v ? std::strtol(v, nullptr, 10) : 2;
+        return (uint32_t)(x >= 1 && x <= 16 ? x : 2);
+    }();
+    const uint32_t waves = std::min<uint32_t>(e->n_wtiles, (uint32_t)std::max(e->n_cu, 1) * 4u * wps);
+    return std::max<uint32_t>(1, (waves + jsp::kTallyWaves - 1) / jsp::kTallyWaves);
+}
+
+// The tally alone (three-launch shape, jsp_tally_device): the wave-tile
+// kernel; JSP_TALLY_BLOCK=1 runs the workgroup-block kernel instead (A/B).
 int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s) {
     jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
     if (e->n_blocks == 0) return JSP_OK;
+    static const bool block = [] { const char* v = std::getenv("JSP_TALLY_BLOCK"); return v && v[0] == '1'; }();
     EvPair* p = ev_begin(e, 0, s);
     uint32_t c0 = 0;
     do {
         a.c0 = c0;
         a.nc = std::min<uint32_t>(e->C - c0, jsp::kTallyClasses);
         a.do_occ = (c0 == 0);
-        HIP_TRY(jsp::launch_tally(a, s));
+        if (block || e->n_wtiles == 0) HIP_TRY(jsp::launch_tally(a, s));
+        else HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, tally_wave_grid(e), s));
         c0 += a.nc;
     } while (c0 < e->C);
     ev_end(p, s);
@@ -1131,6 +1190,26 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     e->blk_l0.assign(blk.begin(), blk.end() - (blk.empty() ? 0 : 1));
     e->blk_l1.assign(blk.begin() + (blk.empty() ? 0 : 1), blk.end());
     HIP_TRY(upload(e->blk, bt.data(), std::max<size_t>(bt.size(), 1), s));
+    {
+        // wave tiles: up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4
+        // rows (one wave chunk at any row alignment), or one larger leaf alone
+        std::vector<uint4> wt;
+        const uint32_t max_rows = (uint32_t)jsp::kWaveTileRows - 4;
+        for (uint32_t l = 0; l < NL;) {
+            const uint32_t r0 = ls[l];
+            if (ls[l + 1] - r0 > max_rows) {
+                wt.push_back(make_uint4(l, l + 1, r0, ls[l + 1]));
+                ++l;
+                continue;
+            }
+            uint32_t end = l;
+            while (end < NL && end - l < (uint32_t)jsp::kWaveTileLeaves && ls[end + 1] - r0 <= max_rows) ++end;
+            wt.push_back(make_uint4(l, end, r0, ls[end]));
+            l = end;
+        }
+        HIP_TRY(upload(e->wtiles, wt.data(), std::max<size_t>(wt.size(), 1), s));
+        e->n_wtiles = (uint32_t)wt.size();
+    }
     HIP_TRY(e->ticket.reserve(16));
     HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch tickets (tile draws, finished tiles)
     HIP_TRY(e->granules.reserve(8 * blk.size()));
@@ -1535,7 +1614,9 @@ int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
     std::lock_guard<std::mutex> g(e->mu);
     HIP_TRY(hipStreamSynchronize(e->stream));
-    if (e->have_last && e->last_foreign) HIP_TRY(hipEventSynchronize(e->ev_last));
+    if (e->have_last && e->last_foreign) {
+        if (int rc = wait_last_foreign(e)) return rc;
+    }
     return JSP_OK;
 }
 
@@ -1545,8 +1626,11 @@ int jsp_engine_check(jsp_engine* e) {
     // everything enqueued so far is ordered before the last call's work, so
     // waiting for that (an engine-owned event, or the engine stream) suffices
     if (e->have_last) {
-        if (e->last_foreign) HIP_TRY(hipEventSynchronize(e->ev_last));
-        else HIP_TRY(hipStreamSynchronize(e->stream));
+        if (e->last_foreign) {
+            if (int rc = wait_last_foreign(e)) return rc;
+        } else {
+            HIP_TRY(hipStreamSynchronize(e->stream));
+        }
     }
     return check_launch_error(e);
 }

@@ -11,6 +11,8 @@ constexpr int kTallyWaves = kTallyThreads / 64;
 constexpr int kRowsPerThread = 4;                  // 16-B column loads
 constexpr int kChunkRows = kTallyThreads * kRowsPerThread;
 constexpr int kMaxBlkLeaves = 256;                 // leaves one tally workgroup may own
+constexpr int kWaveTileRows = 256;                 // one wave's chunk: 64 lanes x 4 rows
+constexpr int kWaveTileLeaves = 64;                // leaves of a multi-leaf wave tile (one per lane)
 constexpr int kTallyClasses = 16;                  // classes per tally pass
 constexpr int kAssignThreads = 1024;               // 16 waves, one workgroup
 constexpr int kAssignWaves = kAssignThreads / 64;
@@ -220,6 +222,11 @@ struct AssignPlan {
 AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_words);
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
+// Wave-tile tally (tally_wave_kernel): tiles {first leaf, end leaf, first row,
+// end row} of up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4 rows,
+// or one leaf of any size; `grid` workgroups of 4 waves take them in turn.
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid, hipStream_t s);
+size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);

@@ -492,6 +492,160 @@ __global__ __launch_bounds__(kTallyThreads) void tally_kernel(TallyArgs a) {
     JSP_STAMP(blockIdx.x, 5);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a 16-B LDS store in any address space
+
+// ---- wave-tile tally (the three-launch shape's tally: large snapshots)
+// Every wave works alone -- no workgroup barrier after the class records are
+// staged -- on a stream of wave tiles (jsp_internal.h kWaveTile*): a tile is
+// either up to 64 whole leaves in <= 252 rows (one 256-row chunk: lane i
+// holds rows base + 4i .. + 3), or one leaf of any size, walked chunk by
+// chunk. A wave takes tiles gw, gw + waves, ... and issues the next chunk's
+// row loads before it evaluates the current one, so its loads stay in flight
+// under its own row pass and the other waves' (several waves per SIMD). Per
+// chunk and value: the 4-row partial sums, a DPP wave scan, the row prefixes
+// into the wave's own LDS slice; lane li then forms leaf li's sum as
+// prefix(last row) - prefix(row before its first) and stores it (a tile's
+// leaves are consecutive: one coalesced store per value). A multi-chunk leaf
+// adds each chunk's total (lane 63's prefix) in an SGPR-held running sum.
+template <int W, int R>
+__global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, const uint4* __restrict__ tiles,
+                                                                   uint32_t n_tiles) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    const int nc = (int)a.nc;
+    const int nv = nc + a.do_occ;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
+    if (tid < nc * kClsVec) reinterpret_cast<uint4*>(lds)[tid] = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
+    __syncthreads();
+    const DevClass* s_cls = reinterpret_cast<const DevClass*>(lds);  // read once per class and chunk, into SGPRs
+    JSP_LDS uint32_t* s_pre = lds_ptr(lds + tally_acc_off(nc) + wid * nv * kWaveTileRows);
+    const uint32_t waves = gridDim.x * kTallyWaves;
+    uint32_t t = blockIdx.x * kTallyWaves + wid;
+    if (t >= n_tiles) return;
+    uint4 bt = tiles[t];
+    uint32_t base = bt.z & ~3u;
+    RowRegs<W, R> cur;
+    {
+        const uint32_t row = base + 4u * lane;
+        load_rows<W, R>(a, row, row < bt.w && row + 3 >= bt.z, cur);
+    }
+    uint32_t ls_lo = 0, ls_hi = 0;  // lane li: leaf l0 + li's rows
+    {
+        const uint32_t nl = bt.y - bt.x;
+        if ((uint32_t)lane < nl) {
+            ls_lo = a.leaf_start[bt.x + lane];
+            ls_hi = a.leaf_start[bt.x + lane + 1];
+        }
+    }
+    while (true) {
+        // the next chunk of this wave's stream: the tile's next 256 rows, or
+        // the first chunk of its next tile
+        uint32_t nt = t, nbase = base + kWaveTileRows;
+        uint4 nbt = bt;
+        if (nbase >= bt.w) {
+            nt = t + waves;
+            if (nt < n_tiles) {
+                nbt = tiles[nt];
+                nbase = nbt.z & ~3u;
+            }
+        }
+        const bool more = nt < n_tiles;
+        RowRegs<W, R> nxt;
+        if (more) {
+            const uint32_t row = nbase + 4u * lane;
+            load_rows<W, R>(a, row, row < nbt.w && row + 3 >= nbt.z, nxt);
+        }
+        const uint32_t row = base + 4u * lane;
+        bool valid[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) valid[i] = row + i >= bt.z && row + i < bt.w;
+        const uint32_t l0 = bt.x, nl = bt.y - bt.x;
+        const bool single = nl == 1 && bt.w - bt.z > kWaveTileRows - 4;  // one leaf over several chunks
+        const bool first_chunk = base == (bt.z & ~3u), last_chunk = base + kWaveTileRows >= bt.w;
+        for (int c = 0; c < nv; ++c) {
+            uint32_t v[4];
+            if (c < nc) {
+                const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
+                uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    if (k.res[r] == 0) continue;
+                    if (k.shift[r] == kDivIdentity) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], cur.fr[r][i]);
+                    } else if ((a.fast_res >> r) & 1u) {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(cur.fr[r][i], k.magic31[r]) >> k.shift31[r]);
+                    } else {
+#pragma unroll
+                        for (int i = 0; i < 4; ++i) {
+                            const uint32_t n = cur.fr[r][i], h = __umulhi(n, k.magic[r]);
+                            cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
+                        }
+                    }
+                }
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    bool ok = valid[i] & ((cur.tn[i] & k.tol_inv) == 0);
+#pragma unroll
+                    for (int w = 0; w < W; ++w) ok = ok & ((cur.lab[w][i] & k.mask[w]) == k.req[w]);
+                    v[i] = ok ? cap[i] : 0u;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v[i] = (valid[i] && cur.ex[i] != -1) ? 1u : 0u;
+            }
+            const uint32_t p0 = v[0], p1 = p0 + v[1], p2 = p1 + v[2], p3 = p2 + v[3];
+            const uint32_t incl = wave_incl_scan(p3, lane);
+            uint32_t* out = c < nc ? a.cap_out + (size_t)(a.c0 + c) * a.ld : a.occ_out;
+            if (single) {
+                // one leaf: this chunk's total, carried in s_pre's tail word of the value
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                JSP_LDS uint32_t* accw = lds_ptr(lds + tally_acc_off(nc) + kTallyWaves * nv * kWaveTileRows) +
+                                         wid * kMaxClasses + c;
+                const uint32_t acc = (first_chunk ? 0u : *accw) + tot;
+                if (last_chunk) {
+                    if (lane == 0) out[a.leaf_base + l0] = acc;
+                } else if (lane == 0) {
+                    *accw = acc;
+                }
+                continue;
+            }
+            const uint32_t wex = incl - p3;
+            reinterpret_cast<JSP_LDS u32x4*>(s_pre + c * kWaveTileRows)[lane] = u32x4{wex + p0, wex + p1, wex + p2, incl};
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if ((uint32_t)lane < nl) {
+                uint32_t sum = 0;
+                const uint32_t lo = ls_lo, hi = ls_hi;
+                if (lo < hi) {
+                    const uint32_t hp = s_pre[c * kWaveTileRows + (hi - 1 - base)];
+                    const uint32_t bp = lo > base ? s_pre[c * kWaveTileRows + (lo - 1 - base)] : 0u;
+                    sum = hp - bp;
+                }
+                out[a.leaf_base + l0 + lane] = sum;
+            }
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        if (!more) break;
+        if (nt != t) {
+            t = nt;
+            bt = nbt;
+            const uint32_t nnl = bt.y - bt.x;
+            ls_lo = ls_hi = 0;
+            if ((uint32_t)lane < nnl) {
+                ls_lo = a.leaf_start[bt.x + lane];
+                ls_hi = a.leaf_start[bt.x + lane + 1];
+            }
+        }
+        base = nbase;
+        cur = nxt;
+    }
+}
+
 // ----------------------------------------------------------------- feasibility
 // Bit d of class c's word w: capsum(c, d) >= pods[c] && occsum(d) == 0 over the
 // leaves of domain d = 64w + lane at level lvl. One wave computes one word.
@@ -2568,6 +2722,14 @@ static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
 }
 
 template <int W, int R>
+static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid,
+                                       hipStream_t s) {
+    hipLaunchKernelGGL((tally_wave_kernel<W, R>), dim3(grid), dim3(kTallyThreads),
+                       tally_wave_lds_bytes(a.nc, a.nc + a.do_occ), s, a, tiles, n_tiles);
+    return hipGetLastError();
+}
+
+template <int W, int R>
 static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
     hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks * f.groups + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
                        s, a, f);
@@ -2604,6 +2766,15 @@ static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hi
 #define JSP_DISPATCH_WR(FN, ...) JSP_DISPATCH_WR_OR(hipErrorInvalidValue, FN, __VA_ARGS__)
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s) { JSP_DISPATCH_WR(launch_tally_wr, a, s) }
+
+size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv) {
+    return sizeof(uint32_t) * ((size_t)tally_acc_off((int)nc) + (size_t)kTallyWaves * nv * kWaveTileRows +
+                               (size_t)kTallyWaves * kMaxClasses);
+}
+
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_tally_wave_wr, a, tiles, n_tiles, grid, s)
+}
 
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
     JSP_DISPATCH_WR(launch_fused_wr, a, f, s)

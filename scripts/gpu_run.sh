@@ -9,7 +9,8 @@
 #   probes    tools/svc_probe.py + tools/host_api_probe.py
 #   trace     rocprofv3 --kernel-trace --stats of the bench (no CPU legs)
 #   pmc       separate rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / SQ) on configs 2, 4, 5
-#   py:FILE   python FILE (a probe under tools/) -> FILE.txt
+#   py:FILE[:ARG]  python FILE ARG (a probe under tools/) -> FILE_ARG.txt
+#   pytest:SEL     pytest SEL -m gpu (one file or node id)
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure, time-out or crash (nothing further touches the GPU).
 set -u
@@ -41,7 +42,11 @@ for step in "$@"; do
                  run 120 "$OUT/pmc_sq$cfg.log" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/pmc_sq$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20
                done ) || exit $?
              python3 tools/summarize_prof.py "$OUT" > "$OUT/summary.txt" 2>&1 ;;
-    py:*)    f="${step#py:}"; run 300 "$OUT/$(basename "$f").txt" python3 -u "$f"; tail -30 "$OUT/$(basename "$f").txt" ;;
+    py:*)    spec="${step#py:}"; f="${spec%%:*}"; arg=""; [ "$spec" != "$f" ] && arg="${spec#*:}"
+             log="$OUT/$(basename "$f" .py)${arg:+_$arg}.txt"
+             run 600 "$log" python3 -u "$f" $arg; tail -30 "$log" ;;
+    pytest:*) sel="${step#pytest:}"; run 900 "$OUT/pytest_$(echo "$sel" | tr '/:' '__').log" python -u -m pytest $sel -m gpu -x -q --timeout 120 --timeout-method thread
+             tail -3 "$OUT/pytest_$(echo "$sel" | tr '/:' '__').log" ;;
     *)       echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""A/B probes on cuda:0 (diagnostic only, not the bench). Each variant runs in
+its own child process because the engine reads its tuning variables once.
+
+  python tools/ab_probe.py tally     cfg4 tally: block kernel vs wave-tile kernel
+                                     (waves per SIMD 1/2/3/4), warm (200 back-to-back
+                                     launches, HIP events) and cold (512 MiB scrub
+                                     before each of 20 launches), bit-exact vs oracle
+  python tools/ab_probe.py mark      device path (jsp_place_device) per-call host and
+                                     GPU time with each caller-stream marker
+  python tools/ab_probe.py one KEY   one variant (the child side)
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave1": {"JSP_TALLY_WPS": "1"}, "wave2": {"JSP_TALLY_WPS": "2"},
+         "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"}}
+MARK = {"event": {}, "value": {"JSP_STREAM_MARK": "value"}, "none": {"JSP_STREAM_MARK": "none"}}
+
+
+def child_tally():
+    import numpy as np
+    import torch
+
+    import bench
+    from jobset_amd import synth
+    from jobset_amd.engine import Engine
+    from oracle import oracle as O
+    p = synth.config4()
+    eng = Engine(0)
+    eng.load(p)
+    stream = torch.cuda.current_stream().cuda_stream
+    C, L = len(p.classes), p.topology.n_leaves
+    cap = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
+    fn = lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), L, stream)  # noqa: E731
+    fn()
+    eng.check()
+    _, ocap, oocc = O.place_c(p)
+    got = cap.cpu().numpy().astype(np.uint32)
+    exact = bool(np.array_equal(got[:C], ocap) and np.array_equal(got[C], oocc))
+    for _ in range(10):
+        fn()
+    warm = bench.event_loop_us(fn, 200, stream)
+    scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")
+    cold = bench.cold_us(fn, 20, stream, scrub)
+    eng.check()
+    tb = bench.tally_bytes(p)
+    return {"exact": exact, "warm_us": round(warm, 2), "cold_us": round(cold, 2),
+            "warm_frac": round(tb / warm / 1e3 / 8000, 4), "cold_frac": round(tb / cold / 1e3 / 8000, 4)}
+
+
+def child_mark():
+    import numpy as np
+    import torch
+
+    import bench
+    from jobset_amd import synth
+    from jobset_amd.engine import Engine
+    from jobset_amd.snapshot import job_runs
+    out = {}
+    eng = Engine(0)
+    stream = torch.cuda.current_stream().cuda_stream
+    for cfg in (1, 2):
+        p = synth.CONFIGS[cfg]()
+        eng.load(p)
+        rc, rl = job_runs(p.job_class)
+        rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+        rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+        o = torch.empty(max(p.n_jobs, 1), dtype=torch.int32, device="cuda")
+        fn = lambda: eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs,  # noqa: E731
+                                      o.data_ptr(), stream)
+        for _ in range(50):
+            fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(1000):
+            fn()
+        host = (time.perf_counter() - t0) * 1e6 / 1000
+        torch.cuda.synchronize()
+        gpu = bench.event_loop_us(fn, 1000, stream)
+        eng.check()
+        out[f"cfg{cfg}"] = {"host_us_per_call": round(host, 2), "gpu_us_per_call": round(gpu, 2)}
+    return out
+
+
+def main():
+    mode = sys.argv[1]
+    if mode == "one":
+        key = sys.argv[2]
+        res = child_tally() if key in TALLY else child_mark()
+        print(json.dumps({key: res}), flush=True)
+        return
+    variants = TALLY if mode == "tally" else MARK
+    for key, env in variants.items():
+        e = dict(os.environ)
+        e.update(env)
+        r = subprocess.run([sys.executable, os.path.abspath(__file__), "one", key], env=e, capture_output=True,
+                           text=True, timeout=240)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        print(line[-1] if line else json.dumps({key: {"rc": r.returncode, "err": r.stderr[-400:]}}), flush=True)
+        if r.returncode != 0:
+            sys.exit(r.returncode)
+
+
+if __name__ == "__main__":
+    main()
