@@ -73,3 +73,6 @@ clean:
 tools/bin/stream_ceiling: tools/stream_ceiling.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
+tools/bin/layout_probe: tools/layout_probe.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<

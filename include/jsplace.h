@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 3
+#define JSP_ABI_VERSION 4
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -148,6 +148,7 @@ typedef struct jsp_timing {
     uint64_t svc_fallbacks;    /* jsp_place calls the service could not answer (its grid does not fit the
                                   CUs, it left, or a request failed on the device): answered by the launch
                                   path instead; the service stays off until the next upload */
+    double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */

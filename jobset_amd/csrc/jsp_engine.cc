@@ -177,6 +177,8 @@ struct jsp_engine {
         int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
+        bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
+        std::chrono::steady_clock::time_point t_launch{};
         bool broken = false;  // a start or a request failed on this geometry: the launch path answers until
                               // the next upload (every upload clears it)
         std::chrono::steady_clock::time_point last{};
@@ -241,6 +243,16 @@ int stream_mark_mode() {
         return 0;
     }();
     return m;
+}
+
+// Flags of ev_last (JSP_EVENT_FLAGS: "sys" = a system-scope release on record,
+// the HIP default; "dev" = device-scope release; "nofence" = none). Ordering a
+// later stream after the device call needs only device scope.
+unsigned ev_last_flags() {
+    const char* v = std::getenv("JSP_EVENT_FLAGS");
+    if (v && std::strcmp(v, "sys") == 0) return hipEventDisableTiming;
+    if (v && std::strcmp(v, "nofence") == 0) return hipEventDisableTiming | hipEventDisableSystemFence;
+    return hipEventDisableTiming | hipEventReleaseToDevice;
 }
 
 int wait_prior(jsp_engine* e, hipStream_t s) {
@@ -595,6 +607,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
 // service is seen by a stream query and the request re-posted once).
 constexpr uint32_t kSvcMaxBlocks = 255;  // one tile per workgroup + the dispatcher, all co-resident (<= one per CU)
 constexpr int kSvcGone = 1;
+constexpr int kSvcUseLaunch = 2;  // svc_place: the service is (re)starting; answer this call on the launch path
 
 double svc_idle_ms() {
     static const double ms = [] {
@@ -667,15 +680,16 @@ int svc_suspend(jsp_engine* e) {
     return svc_stop(e);
 }
 
-int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs);
+int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready);
+int svc_wait_ready(jsp_engine* e);
 void svc_resume(jsp_engine* e) {
     if (e->svc.resume && svc_ok(e)) {
         e->svc.resume = false;
-        (void)svc_start(e, 0, 0);  // a failure here resurfaces at the next jsp_place
+        (void)svc_start(e, 0, 0, false);  // a failure here resurfaces at the next jsp_place
     }
 }
 
-int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
+int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     auto& v = e->svc;
     if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
     const uint32_t nb = e->n_blocks;
@@ -783,11 +797,21 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
     else if (shape == 3) HIP_TRY(jsp::launch_split_service(ta0, sp, a, v.stream));
     else HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
     v.running = true;
+    v.pending_ready = true;
+    v.t_launch = std::chrono::steady_clock::now();
+    v.last = v.t_launch;
     e->acc.svc_starts += 1;
-    // return once the dispatcher polls: a request posted now is answered
-    // without waiting for the launch (bounded: a dispatcher that cannot get a
-    // CU within 2 s means the grid is not co-resident)
-    const auto t_start = std::chrono::steady_clock::now();
+    return wait_ready ? svc_wait_ready(e) : JSP_OK;
+}
+
+// Return once the dispatcher polls: a request posted then is answered without
+// waiting for the launch (bounded: a dispatcher that cannot get a CU within
+// 2 s means the grid is not co-resident).
+int svc_wait_ready(jsp_engine* e) {
+    auto& v = e->svc;
+    if (!v.pending_ready) return JSP_OK;
+    const uint32_t* ready = v.box.as<uint32_t>() + 8;
+    const auto t_start = v.t_launch;
     for (uint64_t spins = 1; __atomic_load_n(ready, __ATOMIC_ACQUIRE) != v.gen; ++spins) {
         if ((spins & 255) == 0) {
             const hipError_t q = hipStreamQuery(v.stream);
@@ -802,6 +826,8 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs) {
             }
         }
     }
+    v.pending_ready = false;
+    e->acc.svc_ready_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_start).count();
     v.last = std::chrono::steady_clock::now();
     return JSP_OK;
 }
@@ -848,11 +874,25 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
                    (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
+    // A cold start -- the first request after an idle exit (recoveries are
+    // hours apart), an upload or a geometry change -- launches the service
+    // without waiting for its dispatcher and answers this call on the launch
+    // path meanwhile (kSvcUseLaunch); the next call finds it polling.
+    // JSP_COLD_LAUNCH=0: wait for the new service and post to it (A/B).
+    static const bool cold_launch = [] { const char* v = std::getenv("JSP_COLD_LAUNCH"); return !(v && v[0] == '0'); }();
+    if (restart && cold_launch) {
+        if (int rc = svc_stop(e)) return rc;
+        if (int rc = svc_start(e, J, n_runs, false)) return rc;
+        return kSvcUseLaunch;
+    }
+    if (!restart) {
+        if (int rc = svc_wait_ready(e)) return rc;
+    }
     uint32_t seq = 0;
     for (int attempt = 0;; ++attempt) {
         if (restart) {
             if (int rc = svc_stop(e)) return rc;
-            if (int rc = svc_start(e, J, n_runs)) return rc;
+            if (int rc = svc_start(e, J, n_runs, true)) return rc;
         }
         if (shape == 1 && n_runs > 0) {  // the tail reads the runs from pinned memory
             std::memcpy(v.runs.as<uint32_t>(), run_class, (size_t)n_runs * 4);
@@ -1008,7 +1048,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         delete e;
         return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
     }
-    if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e->ev_last, ev_last_flags()) != hipSuccess) {
         delete e;
         return set_err(JSP_EHIP, "hipEventCreate failed");
     }
@@ -1402,7 +1442,9 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (!want_tally && svc_ok(e)) {
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
-        if (svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed) != JSP_OK) {
+        const int src = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed);
+        if (src == kSvcUseLaunch) goto launch_path;
+        if (src != JSP_OK) {
             // the service could not answer (not co-resident, left, or a request
             // failed on the device): stop it, keep it off until the next upload,
             // and answer this call on the launch path

@@ -24,6 +24,18 @@ def svc_engine(engine):
     engine.service_stop()
 
 
+def warm(engine, job_class):
+    """The first host-API call after the service (re)starts -- an upload, an
+    idle exit, a geometry change -- is answered on the launch path while the
+    new service comes up (DESIGN.md §4.3 cold start); place until a resident
+    shape answers (at most a few calls). Returns that answer."""
+    for _ in range(4):
+        got = engine.place(job_class)
+        if got.fused in (3, 4, 5):
+            return got
+    return got
+
+
 def one_leaf_class(p):
     """The problem reduced to its first class moved to the leaf level (the
     compaction shape the service answers)."""
@@ -40,6 +52,7 @@ def test_service_configs_repeated(svc_engine):
         p = synth.CONFIGS[cfg]()
         svc_engine.load(p)
         a = O.place_c(p)[0]
+        warm(svc_engine, p.job_class)
         call = svc_engine.host_placer(*job_runs(p.job_class))
         for _ in range(200):
             st = call()
@@ -47,7 +60,7 @@ def test_service_configs_repeated(svc_engine):
             np.testing.assert_array_equal(call.assign, a)
             assert st.placed == int((a >= 0).sum())
     t = svc_engine.timing(reset=True)
-    assert t.svc_calls == 400
+    assert 400 <= t.svc_calls <= 402
     assert 2 <= t.svc_starts <= 4  # one per upload (+ a rare idle restart)
 
 
@@ -58,6 +71,7 @@ def test_service_random_parity(svc_engine, seed):
     p = one_leaf_class(synth.random_problem(seed))
     svc_engine.load(p)
     a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(warm(svc_engine, p.job_class).assign, a)
     for _ in range(3):
         got = svc_engine.place(p.job_class)
         assert got.fused == 3
@@ -71,15 +85,18 @@ def test_service_random_parity(svc_engine, seed):
 
 def test_service_job_counts_and_growth(svc_engine):
     """J = 0, 1, more jobs than feasible racks, and a J beyond the service's
-    output capacity (restart with a larger pinned buffer)."""
+    output capacity (restart with a larger pinned buffer: that call is
+    answered on the launch path, the next by the new service)."""
     p = synth.config2()
     svc_engine.load(p)
+    warm(svc_engine, p.job_class)
     for J in (0, 1, 990, 1500, 5000, 7000, 3, 0):
         p.job_class = np.zeros(J, dtype=np.uint32)
         a = O.place_c(p)[0]
-        got = svc_engine.place(p.job_class)
-        assert got.assign.shape == (J,)
-        np.testing.assert_array_equal(got.assign, a)
+        for _ in range(2):
+            got = svc_engine.place(p.job_class)
+            assert got.assign.shape == (J,)
+            np.testing.assert_array_equal(got.assign, a)
         assert got.fused == 3
 
 
@@ -88,7 +105,7 @@ def test_service_patch_and_reupload(svc_engine):
     is synchronous) and re-uploads (restart on new buffers) are both seen."""
     p = synth.config2()
     svc_engine.load(p)
-    np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, O.place_c(p)[0])
+    np.testing.assert_array_equal(warm(svc_engine, p.job_class).assign, O.place_c(p)[0])
     svc_engine.timing(reset=True)
     rng = np.random.default_rng(7)
     for step in range(10):
@@ -103,7 +120,7 @@ def test_service_patch_and_reupload(svc_engine):
     for t in range(5):  # recovery trials: a new post-delete snapshot each
         q = synth.config2(trial=t)
         svc_engine.load(q)
-        got = svc_engine.place(q.job_class)
+        got = svc_engine.place(q.job_class)  # the service restarted at the upload's end
         assert got.fused == 3
         np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
     assert svc_engine.timing(reset=True).svc_starts == 5
@@ -134,7 +151,7 @@ def test_service_idle_exit_and_stop(svc_engine):
 def test_service_off_equals_on(svc_engine):
     p = synth.config2(trial=3)
     svc_engine.load(p)
-    on = svc_engine.place(p.job_class)
+    on = warm(svc_engine, p.job_class)
     svc_engine.set_service(False)
     off = svc_engine.place(p.job_class)
     svc_engine.set_service(True)
@@ -150,6 +167,7 @@ def test_service_timing_stamps(svc_engine):
     svc_engine.load(p)
     svc_engine.set_timing(True)
     try:
+        warm(svc_engine, p.job_class)  # timing on restarts the service (stamps on)
         call = svc_engine.host_placer(*job_runs(p.job_class))
         svc_engine.timing(reset=True)
         walls = []
@@ -213,6 +231,7 @@ def test_fused_service_configs(svc_engine, cfg, device_walk):
     p = synth.CONFIGS[cfg]()
     svc_engine.load(p)
     a = O.place_c(p)[0]
+    warm(svc_engine, p.job_class)
     call = svc_engine.host_placer(*job_runs(p.job_class))
     for _ in range(100):
         st = call()
@@ -257,6 +276,7 @@ def test_fused_service_patch_and_device_path(svc_engine, device_walk):
     out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
     side = torch.cuda.Stream()
     rng = np.random.default_rng(5)
+    warm(svc_engine, p.job_class)
     for step in range(20):
         got = svc_engine.place(p.job_class)
         assert got.fused == walk_shape(device_walk)
@@ -281,6 +301,8 @@ def test_two_engines_with_services(svc_engine):
     e2 = Engine(0)
     try:
         e2.load(q5)
+        warm(svc_engine, p2.job_class)
+        warm(e2, q5.job_class)
         for _ in range(50):
             g2 = svc_engine.place(p2.job_class)
             g5 = e2.place(q5.job_class)
@@ -305,6 +327,7 @@ def test_service_request_numbers_across_2_pow_30(monkeypatch):
         p = synth.config2()
         e.load(p)
         a = O.place_c(p)[0]
+        warm(e, p.job_class)
         call = e.host_placer(*job_runs(p.job_class))
         for _ in range(12):
             st = call()
@@ -349,7 +372,7 @@ def test_service_that_cannot_fit_falls_back(monkeypatch):
     try:
         p = synth.config2()
         e.load(p)
-        got = e.place(p.job_class)
+        got = warm(e, p.job_class)
         assert got.fused == 3 and e.timing(reset=True).svc_fallbacks == 0
     finally:
         e.close()

@@ -21,7 +21,9 @@ sys.path.insert(0, ROOT)
 
 TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave1": {"JSP_TALLY_WPS": "1"}, "wave2": {"JSP_TALLY_WPS": "2"},
          "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"}}
-MARK = {"event": {}, "value": {"JSP_STREAM_MARK": "value"}, "none": {"JSP_STREAM_MARK": "none"}}
+MARK = {"event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
+        "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
+        "none": {"JSP_STREAM_MARK": "none"}}
 
 
 def child_tally():
