@@ -4,12 +4,12 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CXX ?= g++
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
-HDR = include/jsplace.h include/jsk_host.h jobset_amd/csrc/jsp_internal.h jobset_amd/csrc/jsp_walk.h
+HDR = include/jsplace.h include/jsk_host.h jobset_amd/csrc/jsp_internal.h jobset_amd/csrc/jsp_walk.h jobset_amd/csrc/jsp_multi.h
 HOST_SRC = $(wildcard jobset_amd/csrc/host/*.cc)
 HOST_HDR = $(wildcard jobset_amd/csrc/host/*.h)
 HOST_OBJ = $(patsubst jobset_amd/csrc/host/%.cc,build/host_%.o,$(HOST_SRC))
 LIB = jobset_amd/libjsplace.so
-OBJ = build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o $(HOST_OBJ)
+OBJ = build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ)
 
 all: $(LIB) oracle
 
@@ -25,12 +25,16 @@ build/jsp_walk.o: jobset_amd/csrc/jsp_walk.cc jobset_amd/csrc/jsp_walk.h $(HDR)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
 
+build/jsp_multi.o: jobset_amd/csrc/jsp_multi.cc jobset_amd/csrc/jsp_multi.h $(HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -x hip -c -o $@ $<
+
 build/host_%.o: jobset_amd/csrc/host/%.cc $(HOST_HDR) $(HDR)
 	@mkdir -p build
 	$(CXX) $(CXXFLAGS) -c -o $@ $<
 
 $(LIB): $(OBJ)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(OBJ) -ldl
 
 oracle:
 	$(MAKE) -s -C oracle
@@ -46,7 +50,7 @@ tools/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip jobset_amd/csrc/jsp_en
 	@mkdir -p build/diag tools/diag
 	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -c -o build/diag/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -x hip -c -o build/diag/e.o jobset_amd/csrc/jsp_engine.cc
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag/k.o build/diag/e.o build/jsp_walk.o $(HOST_OBJ)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag/k.o build/diag/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ)
 
 # ASan + UBSan build of the host mirror (webhook / reconciler / planner / JSON)
 # linked with the product engine objects, and of the C oracles; tests/
@@ -60,7 +64,7 @@ sanitize: build/asan/libjsplace.so
 build/asan/host_%.o: jobset_amd/csrc/host/%.cc $(HOST_HDR) $(HDR)
 	@mkdir -p build/asan
 	$(CXX) $(SANFLAGS) -c -o $@ $<
-build/asan/libjsplace.so: build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o $(ASAN_OBJ)
+build/asan/libjsplace.so: build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(ASAN_OBJ)
 	$(CXX) -shared -fsanitize=address,undefined -o $@ $^ -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64
 
 clean:

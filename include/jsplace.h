@@ -11,10 +11,11 @@
  * Which reference interface each entry point replaces (file:line under the
  * reference tree, danielvegamyhre/jobset @ 2024-10-08):
  *
- *  jsp_engine_create / jsp_engine_destroy
+ *  jsp_engine_create / jsp_engine_create_multi / jsp_engine_destroy
  *      Constructed beside NewPodReconciler / NewPodWebhook in main.go:168,186
  *      and injected into them (there is no engine in the reference: the domain
- *      is chosen by kube-scheduler).
+ *      is chosen by kube-scheduler); the device-set form is
+ *      the manager process's handle over several GPUs.
  *  jsp_topology_upload / jsp_snapshot_upload / jsp_snapshot_patch
  *      Replace the per-pod cached Node Get of topologyFromPod
  *      (pkg/webhooks/pod_mutating_webhook.go:173-194) and leaderPodTopology
@@ -123,7 +124,8 @@ typedef struct jsp_stats {
     uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction,
                                   3 one-class compaction answered by the resident service,
                                   4 fused shape answered by the resident service (walk on the GPU),
-                                  5 split service: resident tiles + the walk on the host */
+                                  5 split service: resident tiles + the walk on the host,
+                                  6 device set: shard tallies combined (RCCL / on-device add), then assign */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
@@ -179,6 +181,24 @@ int jsp_abi_version(void);
 const char* jsp_last_error(void);
 int jsp_device_count(int* out);
 int jsp_engine_create(int device_id, jsp_engine** out);
+/* A device-set engine: one handle over n_devices shard engines (device_ids
+ * may repeat: several shards on one GPU). The snapshot given to
+ * jsp_snapshot_upload (whole: leaves 0..L) is split by whole level-0 domains
+ * into row-balanced shards; jsp_place tallies every shard on its device,
+ * SUM-combines the per-(class, leaf) tallies -- one RCCL all-reduce over the
+ * distinct devices (ncclCommInitAll in this process; librccl.so.1 is loaded
+ * at run time), an on-device add between shards that share a device -- and
+ * runs feasibility + assignment on device_ids[0]. Results are bit-identical
+ * to a single-device engine (integer sums). Uploads, patches, jsp_place /
+ * jsp_place_jobs, jsp_resolve_leader_domains, jsp_audit_placements and the
+ * settings work as on a single engine; the *_device entry points return
+ * JSP_ESTATE (the device buffers span devices). stats.fused = 6.
+ * Replaces, for the Go manager's one process (main.go:161-190), the
+ * per-rank torch.distributed step of jobset_amd/distributed.py. */
+int jsp_engine_create_multi(const int* device_ids, int n_devices, jsp_engine** out);
+/* shards of a device-set engine and its distinct devices (1 and 1 for a
+ * single-device engine) */
+int jsp_engine_shards(jsp_engine* e, int* shards, int* devices);
 void jsp_engine_destroy(jsp_engine* e);
 
 /* ---- snapshot ---- */

@@ -15,6 +15,7 @@
 
 #include "../../include/jsplace.h"
 #include "jsp_internal.h"
+#include "jsp_multi.h"
 #include "jsp_walk.h"
 
 namespace {
@@ -90,8 +91,19 @@ struct EvPair {
 
 }  // namespace
 
+int jsp_internal_set_err(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
 struct jsp_engine {
     int device = 0;
+    jspm::Multi* multi = nullptr;  // a device-set engine (jsp_engine_create_multi): every call goes there
     int n_cu = 0;  // compute units (multiProcessorCount)
     hipStream_t stream = nullptr;
     std::mutex mu;
@@ -192,6 +204,7 @@ struct jsp_engine {
     jsp_timing acc{};
 
     ~jsp_engine() {
+        if (multi) jspm::destroy(multi);
         (void)hipSetDevice(device);
         for (auto& p : ev) {
             if (p.a) (void)hipEventDestroy(p.a);
@@ -1072,8 +1085,35 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
     return JSP_OK;
 }
 
+int jsp_engine_create_multi(const int* device_ids, int n_devices, jsp_engine** out) {
+    if (!out) return set_err(JSP_EINVAL, "out is NULL");
+    *out = nullptr;
+    jspm::Multi* m = nullptr;
+    if (int rc = jspm::create(device_ids, n_devices, &m)) return rc;
+    auto* e = new (std::nothrow) jsp_engine();
+    if (!e) {
+        jspm::destroy(m);
+        return set_err(JSP_ENOMEM, "engine allocation failed");
+    }
+    e->device = jspm::device_of(m);
+    e->multi = m;
+    *out = e;
+    return JSP_OK;
+}
+
+int jsp_engine_shards(jsp_engine* e, int* shards, int* devices) {
+    if (!e) return set_err(JSP_EINVAL, "engine is NULL");
+    if (shards) *shards = e->multi ? jspm::shard_count(e->multi) : 1;
+    if (devices) *devices = e->multi ? jspm::n_devices(e->multi) : 1;
+    return JSP_OK;
+}
+
 void jsp_engine_destroy(jsp_engine* e) {
     if (!e) return;
+    if (e->multi) {
+        delete e;  // the destructor tears the device set down
+        return;
+    }
     {
         std::lock_guard<std::mutex> g(e->mu);
         (void)hipSetDevice(e->device);
@@ -1085,6 +1125,7 @@ void jsp_engine_destroy(jsp_engine* e) {
 
 int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::topology_upload(e->multi, t);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!t) return set_err(JSP_EINVAL, "topology is NULL");
@@ -1162,6 +1203,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
 
 int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::snapshot_upload(e->multi, nd);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
@@ -1294,6 +1336,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
                        const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner);
     std::lock_guard<std::mutex> g(e->mu);
     if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
     if (n == 0) return JSP_OK;
@@ -1328,6 +1371,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
 
 int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::classes_upload(e->multi, classes, C);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
@@ -1378,6 +1422,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
 
 int jsp_tally_device(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, void* stream) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: use jsp_place (the shards tally and combine inside it)");
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
@@ -1394,6 +1439,7 @@ int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_oc
                       const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t n_jobs,
                       int32_t* d_assign, void* stream) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: use jsp_place");
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
@@ -1411,6 +1457,7 @@ int jsp_assign_device(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_oc
 int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
                      uint32_t n_jobs, int32_t* d_assign, void* stream) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: use jsp_place");
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
     if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
@@ -1428,6 +1475,7 @@ int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t*
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::place(e->multi, run_class, run_len, n_runs, assign_out, tally_out, occ_out, stats);
     auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
@@ -1544,6 +1592,7 @@ int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs, in
 int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels, uint32_t n,
                                int32_t* domain_out) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::resolve(e->multi, leader_rows, levels, n, domain_out);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, false)) return rc;
     if (n == 0) return JSP_OK;
@@ -1564,6 +1613,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
                          const uint32_t* follower_off, const int32_t* follower_domains, uint32_t n_jobs,
                          uint32_t* bad_out) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::audit(e->multi, leader_rows, levels, follower_off, follower_domains, n_jobs, bad_out);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, false)) return rc;
     if (n_jobs == 0) return JSP_OK;
@@ -1591,6 +1641,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
 
 int jsp_engine_set_fused(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::forward(e->multi, 0, mode);
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_FUSED_OFF && mode != JSP_FUSED_AUTO) return set_err(JSP_EINVAL, "fused mode %d", mode);
     if (mode != e->fused_mode) {
@@ -1602,6 +1653,7 @@ int jsp_engine_set_fused(jsp_engine* e, int mode) {
 
 int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::forward(e->multi, 1, mode);
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO && mode != JSP_SERVICE_DEVICE_WALK)
         return set_err(JSP_EINVAL, "service mode %d", mode);
@@ -1615,6 +1667,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
 
 int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) { if (n_tiles) *n_tiles = 0; return JSP_OK; }
     std::lock_guard<std::mutex> g(e->mu);
     if (!n_tiles) return set_err(JSP_EINVAL, "n_tiles is NULL");
     *n_tiles = 0;
@@ -1629,6 +1682,7 @@ int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_
 
 int jsp_engine_service_stop(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return JSP_OK;
     std::lock_guard<std::mutex> g(e->mu);
     e->svc.resume = false;
     return svc_stop(e);
@@ -1636,6 +1690,7 @@ int jsp_engine_service_stop(jsp_engine* e) {
 
 int jsp_engine_set_timing(jsp_engine* e, int enable) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::forward(e->multi, 2, enable);
     std::lock_guard<std::mutex> g(e->mu);
     e->timing = enable != 0;
     return JSP_OK;
@@ -1643,6 +1698,7 @@ int jsp_engine_set_timing(jsp_engine* e, int enable) {
 
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::get_timing(e->multi, out, reset);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = resolve_timing(e)) return rc;
     if (out) *out = e->acc;
@@ -1650,10 +1706,14 @@ int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
     return JSP_OK;
 }
 
-void* jsp_engine_stream(jsp_engine* e) { return e ? static_cast<void*>(e->stream) : nullptr; }
+void* jsp_engine_stream(jsp_engine* e) {
+    if (e && e->multi) return jspm::stream(e->multi);
+    return e ? static_cast<void*>(e->stream) : nullptr;
+}
 
 int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::sync(e->multi);
     std::lock_guard<std::mutex> g(e->mu);
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->have_last && e->last_foreign) {
@@ -1664,6 +1724,7 @@ int jsp_engine_sync(jsp_engine* e) {
 
 int jsp_engine_check(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
+    if (e->multi) return jspm::check(e->multi);
     std::lock_guard<std::mutex> g(e->mu);
     // everything enqueued so far is ordered before the last call's work, so
     // waiting for that (an engine-owned event, or the engine stream) suffices

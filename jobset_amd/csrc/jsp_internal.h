@@ -258,6 +258,9 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
                         const int32_t* fdom, uint32_t n_jobs, uint32_t n_rows, const uint32_t* leaf_start,
                         uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo, uint32_t* bad, hipStream_t s);
 
+// dst += src (n words, 16-B aligned buffers): shards of a device set on one device
+hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s);
+
 hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
                         const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
                         uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s);

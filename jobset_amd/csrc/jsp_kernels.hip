@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "jsp_internal.h"
@@ -2713,6 +2714,22 @@ __global__ void patch_kernel(const uint32_t* __restrict__ rows, uint32_t n, uint
     if (dexcl) excl[row] = dexcl[i];
 }
 
+// ----------------------------------------------------------------- shard tally sum
+// dst += src over n words (the device-set engine's shards on one device: the
+// on-device stand-in for the RCCL all-reduce between devices).
+__global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst, const uint32_t* __restrict__ src,
+                                                      size_t n) {
+    const size_t n4 = n / 4;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+        uint4 a = reinterpret_cast<const uint4*>(dst)[i];
+        const uint4 b = reinterpret_cast<const uint4*>(src)[i];
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+        reinterpret_cast<uint4*>(dst)[i] = a;
+    }
+    for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] += src[i];
+}
+
 // ----------------------------------------------------------------- launchers
 template <int W, int R>
 static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
@@ -2928,6 +2945,13 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
     if (n_jobs == 0) return hipSuccess;
     hipLaunchKernelGGL(audit_kernel, dim3((n_jobs + 3) / 4), dim3(256), 0, s, leader_rows, levels, foff, fdom,
                        n_jobs, n_rows, leaf_start, n_leaves, leaf_base, topo, bad);
+    return hipGetLastError();
+}
+
+hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const size_t blocks = std::min<size_t>(1024, (n / 4 + 255) / 256 + 1);
+    hipLaunchKernelGGL(add_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 

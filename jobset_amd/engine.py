@@ -37,12 +37,19 @@ class PlaceResult:
 
 
 class Engine:
-    """One engine per GPU (device id = local rank)."""
+    """One engine per GPU (device id = local rank), or -- with `devices`, a
+    list of device ids (repeats allowed) -- one device-set engine over several
+    shards (jsp_engine_create_multi)."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, devices: Optional[Sequence[int]] = None):
         self._lib = native.lib()
         h = ctypes.c_void_p()
-        check(self._lib.jsp_engine_create(device, ctypes.byref(h)))
+        if devices is not None:
+            ids = (ctypes.c_int * len(devices))(*devices)
+            check(self._lib.jsp_engine_create_multi(ids, len(devices), ctypes.byref(h)))
+            device = int(devices[0]) if len(devices) else 0
+        else:
+            check(self._lib.jsp_engine_create(device, ctypes.byref(h)))
         self._h = h
         self.device = device
         self._keep: List[object] = []
@@ -186,6 +193,12 @@ class Engine:
         call.stats = st
         call.keep = (rc, rl, assign)
         return call
+
+    def shards(self) -> Tuple[int, int]:
+        """(shards, distinct devices) of this engine (1, 1 unless a device set)."""
+        a, b = ctypes.c_int(0), ctypes.c_int(0)
+        check(self._lib.jsp_engine_shards(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
 
     def check(self) -> None:
         """jsp_engine_check: wait for the engine's launches, raise if one failed."""

@@ -62,6 +62,8 @@ SIGNATURES = [
     ("jsp_last_error", ctypes.c_char_p, []),
     ("jsp_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("jsp_engine_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(vp)]),
+    ("jsp_engine_create_multi", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(vp)]),
+    ("jsp_engine_shards", ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int)]),
     ("jsp_engine_destroy", None, [vp]),
     ("jsp_topology_upload", ctypes.c_int, [vp, ctypes.POINTER(JspTopology)]),
     ("jsp_snapshot_upload", ctypes.c_int, [vp, ctypes.POINTER(JspNodes)]),

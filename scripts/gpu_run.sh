@@ -6,6 +6,7 @@
 #   bench     python bench.py (default flags) -> bench.json
 #   driver    python bench.py --gpus 1 --steps 20 --warmup 5 (the driver's flags) -> bench_driver.json
 #   ceiling   tools/bin/stream_ceiling (read / copy ceilings at the kernels' byte counts)
+#   bin:NAME  tools/bin/NAME (a compiled probe) -> NAME.json
 #   probes    tools/svc_probe.py + tools/host_api_probe.py
 #   trace     rocprofv3 --kernel-trace --stats of the bench (no CPU legs)
 #   pmc       separate rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / SQ) on configs 2, 4, 5
@@ -31,6 +32,7 @@ for step in "$@"; do
     bench)   run 500 "$OUT/bench.json" python bench.py; tail -c 600 "$OUT/bench.json" ;;
     driver)  run 500 "$OUT/bench_driver.json" python bench.py --gpus 1 --steps 20 --warmup 5; tail -c 400 "$OUT/bench_driver.json" ;;
     ceiling) run 120 "$OUT/stream_ceiling.json" tools/bin/stream_ceiling; cat "$OUT/stream_ceiling.json" ;;
+    bin:*)   b="${step#bin:}"; run 120 "$OUT/$b.json" "tools/bin/$b"; cat "$OUT/$b.json" ;;
     probes)  run 200 "$OUT/svc_probe.txt" python3 tools/svc_probe.py 2000
              run 240 "$OUT/host_api_phases.txt" python3 tools/host_api_probe.py ;;
     trace)   ( cd /tmp && export TMPDIR=/tmp && run 500 "$OUT/bench_trace.log" rocprofv3 --kernel-trace --stats -d "$OUT/bench_trace" -o run --output-format csv -- python3 "$R/bench.py" --trials 100 --cold-trials 0 --cpu-seconds 0 ) || exit $?

@@ -56,3 +56,15 @@ def test_null_engine_is_einval():
     lib = native.lib()
     assert lib.jsp_engine_sync(None) == native.JSP_EINVAL
     assert b"NULL" in lib.jsp_last_error()
+
+
+def test_device_set_without_gpu_fails_loudly():
+    if native.device_count() > 0:
+        pytest.skip("a GPU is present")
+    from jobset_amd.engine import Engine
+    with pytest.raises(native.JspError) as ei:
+        Engine(devices=[0, 0])
+    assert ei.value.code == native.JSP_EHIP
+    with pytest.raises(native.JspError) as ei:
+        Engine(devices=[])
+    assert ei.value.code == native.JSP_EINVAL

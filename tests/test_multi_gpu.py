@@ -1,0 +1,113 @@
+"""The device-set engine behind the C ABI (jsp_engine_create_multi,
+SURVEY.md §8b/§8e): one handle, the node rows sharded by whole level-0
+domains, per-shard tallies SUM-combined, the assignment on the first device.
+On this one-GPU pool the shard ids repeat ({0, 0, 0}), so the shards are
+combined by the on-device add instead of the RCCL all-reduce (which only a
+set of distinct devices takes); the sharding, the per-shard tallies, the
+combine and the replicated walk are the same code. Everything is bit-exact
+against the unsharded oracle (integer sums)."""
+import numpy as np
+import pytest
+
+from jobset_amd import synth
+from jobset_amd.engine import Engine
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def multi():
+    e = Engine(devices=[0, 0, 0])
+    yield e
+    e.close()
+
+
+def test_device_set_shape(multi):
+    assert multi.shards() == (3, 1)
+
+
+@pytest.mark.parametrize("cfg", [2, 3, 4, 5])
+def test_device_set_configs(multi, cfg):
+    p = synth.CONFIGS[cfg]()
+    multi.load(p)
+    a, cap, occ = O.place_c(p)
+    for _ in range(2):  # repeated placements: the shard tallies rewrite their columns only
+        got = multi.place(p.job_class, want_tally=True)
+        assert got.fused == 6
+        np.testing.assert_array_equal(got.assign, a)
+        np.testing.assert_array_equal(got.cap, cap)
+        np.testing.assert_array_equal(got.occ, occ)
+        assert got.placed == int((a >= 0).sum())
+    got = multi.place(p.job_class)  # without tallies
+    np.testing.assert_array_equal(got.assign, a)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_device_set_random(multi, seed):
+    """Ragged random snapshots (1-3 levels, empty leaves, occupancy, up to 16
+    classes): some shards may be empty."""
+    p = synth.random_problem(seed, max_nodes=20_000, max_leaves=400)
+    multi.load(p)
+    got = multi.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+    np.testing.assert_array_equal(got.occ, occ)
+
+
+def test_device_set_patch(multi):
+    """Row patches are routed to the shard that holds each row."""
+    p = synth.config5()
+    multi.load(p)
+    rng = np.random.default_rng(9)
+    for _ in range(5):
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=300, replace=False)).astype(np.uint32)
+        taints = (rng.integers(0, 2, size=300) << rng.integers(0, 4, size=300)).astype(np.uint32)
+        free = rng.integers(0, 200_000, size=(p.nodes.free.shape[0], 300)).astype(np.uint32)
+        multi.patch_rows(rows, taints=taints, free=free)
+        p.nodes.taints[rows] = taints
+        p.nodes.free[:, rows] = free
+        np.testing.assert_array_equal(multi.place(p.job_class).assign, O.place_c(p)[0])
+
+
+def test_device_set_resolve_and_audit(multi):
+    """A5 / A9 batches on global rows: each row's shard answers."""
+    p = synth.config5()
+    multi.load(p)
+    single = Engine(0)
+    try:
+        single.load(p)
+        rows = np.array([0, 17, 16383, -1, 2048, 5000, 9000, 12345, 99999], dtype=np.int32)
+        levels = np.array([1, 0, 1, 1, 0, 1, 0, 1, 1], dtype=np.uint32)
+        got = multi.resolve_leader_domains(rows, levels)
+        np.testing.assert_array_equal(got, single.resolve_leader_domains(rows, levels))
+        off = np.array([0, 2, 2, 4, 5, 5, 7, 8, 9, 9], dtype=np.uint32)
+        fd = np.array([got[0], got[0] + 1, 3, got[2], 4, got[5], got[5], got[6], 7], dtype=np.int32)
+        np.testing.assert_array_equal(multi.audit_placements(rows, levels, off, fd),
+                                      single.audit_placements(rows, levels, off, fd))
+    finally:
+        single.close()
+
+
+def test_device_set_device_path_is_refused(multi):
+    from jobset_amd.native import JSP_ESTATE, JspError
+    p = synth.config2()
+    multi.load(p)
+    with pytest.raises(JspError) as ei:
+        multi.tally_device(0, 0, p.topology.n_leaves, None)
+    assert ei.value.code == JSP_ESTATE
+
+
+@pytest.mark.parametrize("ids", [[0], [0, 0], [0, 0, 0, 0, 0]])
+def test_device_set_sizes(ids):
+    """1, 2 and 5 shards give the same placement (cfg4: 1M nodes)."""
+    p = synth.config4()
+    a = O.place_c(p)[0]
+    e = Engine(devices=ids)
+    try:
+        e.load(p)
+        np.testing.assert_array_equal(e.place(p.job_class).assign, a)
+        assert e.shards() == (len(ids), 1)
+    finally:
+        e.close()

