@@ -1229,7 +1229,11 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     // 1024-row chunks each (a workgroup with several prefetches its next
     // chunk's rows while it evaluates one)
     const uint32_t chunks = block_chunks(N);
-    const uint32_t target_rows = chunks * (uint32_t)jsp::kChunkRows - 4;  // fits even when unaligned
+    uint32_t target_rows = chunks * (uint32_t)jsp::kChunkRows - 4;  // fits even when unaligned
+    if (const char* v = std::getenv("JSP_BLOCK_ROWS")) {  // smaller row blocks (A/B of the tile count)
+        const long x = std::strtol(v, nullptr, 10);
+        if (x >= 60 && x < (long)target_rows) target_rows = (uint32_t)x;
+    }
     std::vector<uint32_t> blk{0};
     {
         uint32_t rows = 0, leaves = 0;

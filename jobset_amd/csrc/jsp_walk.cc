@@ -189,27 +189,34 @@ uint32_t HostWalk::place(const uint64_t* slots, const uint32_t* run_class, const
     for (uint32_t r = 0; r < n_runs; ++r) {
         const uint32_t c = run_class[r], k = level_[c], D = D_[k], nw = (D + 63) / 64;
         const uint64_t* F = feas_.data() + woff_[c];
-        const uint64_t* T = taken_.data() + toff_[k];
-        for (uint32_t i = 0; i < run_len[r]; ++i, ++j) {
-            const uint32_t cur = cursor_[c];
-            if (cur >= D) {
-                assign[j] = -1;
-                continue;
-            }
+        uint64_t* T = taken_.data() + toff_[k];
+        const uint32_t n = run_len[r];
+        uint32_t cur = cursor_[c], i = 0;
+        if (cur < D) {
+            // The run's jobs take the free feasible bits in order. Taking a
+            // domain marks other levels only (ancestors above, descendants
+            // below), so at this level the only bits that change are the ones
+            // the run itself takes: the current word's free bits are kept
+            // across jobs and re-read only when a new word starts.
             uint32_t w = cur >> 6;
             uint64_t bits = F[w] & ~T[w] & (~0ull << (cur & 63));
-            while (bits == 0 && ++w < nw) bits = F[w] & ~T[w];
-            if (bits == 0) {
-                cursor_[c] = D;
-                assign[j] = -1;
-                continue;
+            const bool marks = K_ > 1;
+            for (; i < n; ++i) {
+                while (bits == 0 && ++w < nw) bits = F[w] & ~T[w];
+                if (bits == 0) break;
+                const uint32_t b = (uint32_t)__builtin_ctzll(bits);
+                const uint32_t d = w * 64 + b;
+                bits &= bits - 1;
+                assign[j + i] = (int32_t)d;
+                T[w] |= 1ull << b;
+                if (marks) take(d, k);
+                cur = d + 1;
             }
-            const uint32_t d = w * 64 + (uint32_t)__builtin_ctzll(bits);
-            assign[j] = (int32_t)d;
-            cursor_[c] = d + 1;
-            ++placed;
-            take(d, k);
+            placed += i;
+            cursor_[c] = i < n ? D : cur;
         }
+        for (; i < n; ++i) assign[j + i] = -1;
+        j += n;
     }
     return placed;
 }

@@ -21,6 +21,10 @@ sys.path.insert(0, ROOT)
 
 TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave1": {"JSP_TALLY_WPS": "1"}, "wave2": {"JSP_TALLY_WPS": "2"},
          "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"}}
+SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
+       "svc_rows508": {"JSP_BLOCK_ROWS": "508"}, "svc_rows252": {"JSP_BLOCK_ROWS": "252"},
+       "svc_split_rows252": {"JSP_SPLIT_COMPACT": "1", "JSP_BLOCK_ROWS": "252"},
+       "svc_cold_sync": {"JSP_COLD_LAUNCH": "0"}}
 MARK = {"event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
@@ -91,14 +95,57 @@ def child_mark():
     return out
 
 
+def child_svc():
+    """Host-API jsp_place p50/p99 (resident service) on cfg1/2/3/5, 1000 calls
+    each, plus 40 cold calls (the service idle-exited, a row patched)."""
+    import numpy as np
+
+    from jobset_amd import synth
+    from jobset_amd.engine import Engine
+    from jobset_amd.snapshot import job_runs
+    from oracle import oracle as O
+    out = {}
+    eng = Engine(0)
+    for cfg in (1, 2, 3, 5):
+        p = synth.CONFIGS[cfg]()
+        eng.load(p)
+        a = O.place_c(p)[0]
+        call = eng.host_placer(*job_runs(p.job_class))
+        for _ in range(20):
+            call()
+        assert np.array_equal(call.assign, a)
+        lat = []
+        for _ in range(1000):
+            t0 = time.perf_counter()
+            st = call()
+            lat.append((time.perf_counter() - t0) * 1e6)
+        shape = int(st.fused)
+        assert np.array_equal(call.assign, a)
+        cold = []
+        row = np.zeros(1, dtype=np.uint32)
+        for t in range(40):
+            time.sleep(0.06)
+            row[0] = (t * 7919) % p.nodes.n_nodes
+            eng.patch_rows(row, taints=p.nodes.taints[row])
+            t0 = time.perf_counter()
+            call()
+            cold.append((time.perf_counter() - t0) * 1e6)
+        assert np.array_equal(call.assign, a)
+        lat.sort()
+        cold.sort()
+        out[f"cfg{cfg}"] = {"shape": shape, "p50": round(lat[500], 2), "p99": round(lat[990], 2),
+                            "cold_p50": round(cold[20], 1), "cold_max": round(cold[-1], 1)}
+    return out
+
+
 def main():
     mode = sys.argv[1]
     if mode == "one":
         key = sys.argv[2]
-        res = child_tally() if key in TALLY else child_mark()
+        res = child_tally() if key in TALLY else child_svc() if key in SVC else child_mark()
         print(json.dumps({key: res}), flush=True)
         return
-    variants = TALLY if mode == "tally" else MARK
+    variants = TALLY if mode == "tally" else SVC if mode == "svc" else MARK
     for key, env in variants.items():
         e = dict(os.environ)
         e.update(env)
