@@ -466,8 +466,11 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
         a.c0 = c0;
         a.nc = std::min<uint32_t>(e->C - c0, jsp::kTallyClasses);
         a.do_occ = (c0 == 0);
-        if (block || e->n_wtiles == 0) HIP_TRY(jsp::launch_tally(a, s));
-        else HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, tally_wave_grid(e), s));
+        // the wave-tile kernel takes 1-4 classes with the occupancy count in one pass
+        const bool wave = !block && e->n_wtiles > 0 && a.do_occ && a.nc >= 1 && a.nc <= 4 &&
+                          (uint64_t)(e->C + 1) * ld * 4 < (1ull << 31);
+        if (!wave) HIP_TRY(jsp::launch_tally(a, s));
+        else HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, tally_wave_grid(e), s));
         c0 += a.nc;
     } while (c0 < e->C);
     ev_end(p, s);
@@ -1279,15 +1282,15 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     {
         // wave tiles: up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4
         // rows (one wave chunk at any row alignment), or one larger leaf alone
+        // (none when a leaf is larger than a tile or a column reaches 2^31 bytes:
+        // the workgroup tally then runs)
         std::vector<uint4> wt;
         const uint32_t max_rows = (uint32_t)jsp::kWaveTileRows - 4;
-        for (uint32_t l = 0; l < NL;) {
+        bool ok = (uint64_t)W * npad * 8 < (1ull << 31) && (uint64_t)R * npad * 4 < (1ull << 31) &&
+                  (uint64_t)jsp::kMaxClasses * std::max<uint32_t>(e->L_total, 1) * 4 < (1ull << 31);
+        for (uint32_t l = 0; l < NL && ok; ++l) ok = ls[l + 1] - ls[l] <= max_rows;
+        for (uint32_t l = 0; ok && l < NL;) {
             const uint32_t r0 = ls[l];
-            if (ls[l + 1] - r0 > max_rows) {
-                wt.push_back(make_uint4(l, l + 1, r0, ls[l + 1]));
-                ++l;
-                continue;
-            }
             uint32_t end = l;
             while (end < NL && end - l < (uint32_t)jsp::kWaveTileLeaves && ls[end + 1] - r0 <= max_rows) ++end;
             wt.push_back(make_uint4(l, end, r0, ls[end]));

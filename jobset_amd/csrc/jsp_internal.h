@@ -223,9 +223,12 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 // Wave-tile tally (tally_wave_kernel): tiles {first leaf, end leaf, first row,
-// end row} of up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4 rows,
-// or one leaf of any size; `grid` workgroups of 4 waves take them in turn.
-hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid, hipStream_t s);
+// end row} of up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4 rows
+// (snapshots with a larger leaf use the workgroup tally), 1-4 classes and the
+// occupancy count in one pass; `grid` workgroups of 4 waves take them in turn. Every column's bytes must stay below 2^31
+// (buffer offsets; the host checks).
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
+                             hipStream_t s);
 size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);

@@ -497,153 +497,202 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a 16-B LDS store
 
 // ---- wave-tile tally (the three-launch shape's tally: large snapshots)
 // Every wave works alone -- no workgroup barrier after the class records are
-// staged -- on a stream of wave tiles (jsp_internal.h kWaveTile*): a tile is
-// either up to 64 whole leaves in <= 252 rows (one 256-row chunk: lane i
-// holds rows base + 4i .. + 3), or one leaf of any size, walked chunk by
-// chunk. A wave takes tiles gw, gw + waves, ... and issues the next chunk's
-// row loads before it evaluates the current one, so its loads stay in flight
-// under its own row pass and the other waves' (several waves per SIMD). Per
-// chunk and value: the 4-row partial sums, a DPP wave scan, the row prefixes
-// into the wave's own LDS slice; lane li then forms leaf li's sum as
-// prefix(last row) - prefix(row before its first) and stores it (a tile's
-// leaves are consecutive: one coalesced store per value). A multi-chunk leaf
-// adds each chunk's total (lane 63's prefix) in an SGPR-held running sum.
+// staged -- on a stream of wave tiles (jsp_internal.h kWaveTile*): up to 64
+// whole leaves in <= 252 rows, one 256-row chunk (lane i holds rows base + 4i
+// .. + 3). A wave takes tiles gw, gw + waves, ... with two register sets in
+// turn: while it evaluates one tile, the next tile's rows (and leaf starts)
+// are already in flight in the other set. Loads and stores go through buffer
+// resources, so a load of a tile past the end (or a store of a lane without a
+// leaf) is issued all the same and reads zeros (or is dropped): every
+// iteration issues the same memory instructions, the compiler's vmcnt waits
+// count exactly the older set (no vmcnt(0) per tile), and no register set is
+// copied while its loads are in flight. Per tile and value: the 4-row partial
+// sums, a DPP wave scan, the row prefixes into the wave's own LDS slice; lane
+// li then forms leaf li's sum as prefix(last row) - prefix(row before its
+// first) and stores it (a tile's leaves are consecutive: one coalesced store
+// per value). Snapshots with a leaf over 252 rows use the workgroup tally.
+struct WaveRsrc {
+    __amdgpu_buffer_rsrc_t lab, tn, fr, ex, ls;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 rload16(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 template <int W, int R>
+struct WaveSet {
+    RowRegs<W, R> x;
+    uint32_t ls_lo, ls_hi;  // lane li: rows of leaf first + li
+};
+
+// Issue one tile's loads into `v` (base row `base`; a tile past the end reads
+// zeros: off is pushed beyond every resource's range).
+template <int W, int R>
+__device__ __forceinline__ void wave_issue(const TallyArgs& a, const WaveRsrc& rs, uint32_t base, uint32_t leaf0,
+                                           bool live, int lane, WaveSet<W, R>& v) {
+    const uint32_t row = base + 4u * (uint32_t)lane;
+    const uint32_t bad = live ? 0u : 0x80000000u;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const uint32_t off = ((uint32_t)w * a.npad + row) * 8u | bad;
+        const uint4 u = rload16(rs.lab, off), q = rload16(rs.lab, off + 16u);
+        v.x.lab[w][0] = ((uint64_t)u.y << 32) | u.x; v.x.lab[w][1] = ((uint64_t)u.w << 32) | u.z;
+        v.x.lab[w][2] = ((uint64_t)q.y << 32) | q.x; v.x.lab[w][3] = ((uint64_t)q.w << 32) | q.z;
+    }
+    const uint4 t4 = rload16(rs.tn, (row * 4u) | bad);
+    v.x.tn[0] = t4.x; v.x.tn[1] = t4.y; v.x.tn[2] = t4.z; v.x.tn[3] = t4.w;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint4 f4 = rload16(rs.fr, (((uint32_t)r * a.npad + row) * 4u) | bad);
+        v.x.fr[r][0] = f4.x; v.x.fr[r][1] = f4.y; v.x.fr[r][2] = f4.z; v.x.fr[r][3] = f4.w;
+    }
+    const uint4 e4 = rload16(rs.ex, (row * 4u) | bad);
+    v.x.ex[0] = (int32_t)e4.x; v.x.ex[1] = (int32_t)e4.y; v.x.ex[2] = (int32_t)e4.z; v.x.ex[3] = (int32_t)e4.w;
+    // leaf starts: lane li's leaf [ls[leaf0 + li], ls[leaf0 + li + 1]) (beyond the table: zeros)
+    const uint32_t lo = ((leaf0 + (uint32_t)lane) * 4u) | bad;
+    v.ls_lo = __builtin_amdgcn_raw_buffer_load_b32(rs.ls, lo, 0, 0);
+    v.ls_hi = __builtin_amdgcn_raw_buffer_load_b32(rs.ls, lo + 4u, 0, 0);
+}
+
+// Evaluate one tile from `v` and store its leaves' sums: NV values, the
+// first NV - 1 classes and the occupancy count (compile-time, so every store
+// of the unrolled loop is counted by the compiler's waits).
+template <int W, int R, int NV>
+__device__ __forceinline__ void wave_eval(const TallyArgs& a, const DevClass* s_cls, JSP_LDS uint32_t* s_pre, uint4 bt,
+                                          int lane, const WaveSet<W, R>& v, uint32_t (&sums)[NV]) {
+    constexpr int nc = NV - 1;
+    const uint32_t base = bt.z & ~3u;
+    const uint32_t row = base + 4u * (uint32_t)lane;
+    bool valid[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) valid[i] = row + i >= bt.z && row + i < bt.w;
+    const uint32_t l0 = bt.x, nl = bt.y - bt.x;
+    const bool has_leaf = (uint32_t)lane < nl;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        uint32_t val[4];
+        if (c < nc) {
+            const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
+            uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                if (k.res[r] == 0) continue;
+                if (k.shift[r] == kDivIdentity) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], v.x.fr[r][i]);
+                } else if ((a.fast_res >> r) & 1u) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(v.x.fr[r][i], k.magic31[r]) >> k.shift31[r]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint32_t n = v.x.fr[r][i], h = __umulhi(n, k.magic[r]);
+                        cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                bool ok = valid[i] & ((v.x.tn[i] & k.tol_inv) == 0);
+#pragma unroll
+                for (int w = 0; w < W; ++w) ok = ok & ((v.x.lab[w][i] & k.mask[w]) == k.req[w]);
+                val[i] = ok ? cap[i] : 0u;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) val[i] = (valid[i] && v.x.ex[i] != -1) ? 1u : 0u;
+        }
+        const uint32_t p0 = val[0], p1 = p0 + val[1], p2 = p1 + val[2], p3 = p2 + val[3];
+        const uint32_t incl = wave_incl_scan(p3, lane);
+        const uint32_t wex = incl - p3;
+        reinterpret_cast<JSP_LDS u32x4*>(s_pre + c * kWaveTileRows)[lane] = u32x4{wex + p0, wex + p1, wex + p2, incl};
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        uint32_t sum = 0;
+        const uint32_t lo = v.ls_lo, hi = v.ls_hi;
+        if (has_leaf && lo < hi) {
+            const uint32_t hp = s_pre[c * kWaveTileRows + (hi - 1 - base)];
+            const uint32_t bp = lo > base ? s_pre[c * kWaveTileRows + (lo - 1 - base)] : 0u;
+            sum = hp - bp;
+        }
+        sums[c] = sum;
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+// Store a tile's leaf sums: value c's column is cap[c0 + c][leaf] (occ[leaf]
+// for the last); a lane without a leaf stores out of range (dropped). Issued
+// after the next tile's loads, so no load waits on these stores' registers.
+template <int NV>
+__device__ __forceinline__ void wave_store(const TallyArgs& a, __amdgpu_buffer_rsrc_t cap_rsrc,
+                                           __amdgpu_buffer_rsrc_t occ_rsrc, uint4 bt, int lane,
+                                           const uint32_t (&sums)[NV]) {
+    const bool has_leaf = (uint32_t)lane < bt.y - bt.x;
+    const uint32_t leaf = a.leaf_base + bt.x + (uint32_t)lane;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        const uint32_t col = c < NV - 1 ? (a.c0 + (uint32_t)c) * a.ld : 0u;
+        const uint32_t off = has_leaf ? (col + leaf) * 4u : 0x80000000u;
+        __builtin_amdgcn_raw_buffer_store_b32(sums[c], c < NV - 1 ? cap_rsrc : occ_rsrc, off, 0, 0);
+    }
+}
+
+template <int W, int R, int NV>
 __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, const uint4* __restrict__ tiles,
-                                                                   uint32_t n_tiles) {
+                                                                   uint32_t n_tiles, uint32_t n_leaves) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const int nc = (int)a.nc;
-    const int nv = nc + a.do_occ;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    constexpr int nc = NV - 1;  // this launch: NV - 1 classes and the occupancy count
+    constexpr int nv = NV;
+    const int tid = threadIdx.x, lane = tid & 63;
+    // wave-uniform in SGPRs: the tile descriptors are then scalar loads (lgkmcnt),
+    // which never make a wave wait for its in-flight row loads (vmcnt)
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
     if (tid < nc * kClsVec) reinterpret_cast<uint4*>(lds)[tid] = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
     __syncthreads();
-    const DevClass* s_cls = reinterpret_cast<const DevClass*>(lds);  // read once per class and chunk, into SGPRs
+    const DevClass* s_cls = reinterpret_cast<const DevClass*>(lds);  // read once per class and tile, into SGPRs
     JSP_LDS uint32_t* s_pre = lds_ptr(lds + tally_acc_off(nc) + wid * nv * kWaveTileRows);
     const uint32_t waves = gridDim.x * kTallyWaves;
-    uint32_t t = blockIdx.x * kTallyWaves + wid;
-    if (t >= n_tiles) return;
-    uint4 bt = tiles[t];
-    uint32_t base = bt.z & ~3u;
-    RowRegs<W, R> cur;
-    {
-        const uint32_t row = base + 4u * lane;
-        load_rows<W, R>(a, row, row < bt.w && row + 3 >= bt.z, cur);
-    }
-    uint32_t ls_lo = 0, ls_hi = 0;  // lane li: leaf l0 + li's rows
-    {
-        const uint32_t nl = bt.y - bt.x;
-        if ((uint32_t)lane < nl) {
-            ls_lo = a.leaf_start[bt.x + lane];
-            ls_hi = a.leaf_start[bt.x + lane + 1];
-        }
-    }
+    uint32_t tA = blockIdx.x * kTallyWaves + wid;
+    if (tA >= n_tiles) return;
+    const WaveRsrc rs{make_rsrc(a.labels, (uint32_t)W * a.npad * 8u), make_rsrc(a.taints, a.npad * 4u),
+                      make_rsrc(a.freer, (uint32_t)R * a.npad * 4u), make_rsrc(a.excl, a.npad * 4u),
+                      make_rsrc(a.leaf_start, (n_leaves + 1u) * 4u)};
+    const __amdgpu_buffer_rsrc_t cap_r = make_rsrc(a.cap_out, (a.c0 + (uint32_t)nc) * a.ld * 4u);
+    const __amdgpu_buffer_rsrc_t occ_r = make_rsrc(a.occ_out, a.do_occ ? a.ld * 4u : 0u);
+    const uint32_t last = n_tiles - 1;
+    WaveSet<W, R> A, B;
+    uint4 btA = tiles[tA];
+    wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, true, lane, A);
+    // keep set A's loads ahead of set B's: the loop header's waits merge this
+    // order with the loop's, and an interleaved prologue would make them wait
+    // for nearly every load in flight
+    __builtin_amdgcn_sched_barrier(0);
+    uint32_t tB = tA + waves;
+    uint4 btB = tiles[tB < last ? tB : last];
+    wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, tB < n_tiles, lane, B);
+    uint32_t sums[NV];
     while (true) {
-        // the next chunk of this wave's stream: the tile's next 256 rows, or
-        // the first chunk of its next tile
-        uint32_t nt = t, nbase = base + kWaveTileRows;
-        uint4 nbt = bt;
-        if (nbase >= bt.w) {
-            nt = t + waves;
-            if (nt < n_tiles) {
-                nbt = tiles[nt];
-                nbase = nbt.z & ~3u;
-            }
-        }
-        const bool more = nt < n_tiles;
-        RowRegs<W, R> nxt;
-        if (more) {
-            const uint32_t row = nbase + 4u * lane;
-            load_rows<W, R>(a, row, row < nbt.w && row + 3 >= nbt.z, nxt);
-        }
-        const uint32_t row = base + 4u * lane;
-        bool valid[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) valid[i] = row + i >= bt.z && row + i < bt.w;
-        const uint32_t l0 = bt.x, nl = bt.y - bt.x;
-        const bool single = nl == 1 && bt.w - bt.z > kWaveTileRows - 4;  // one leaf over several chunks
-        const bool first_chunk = base == (bt.z & ~3u), last_chunk = base + kWaveTileRows >= bt.w;
-        for (int c = 0; c < nv; ++c) {
-            uint32_t v[4];
-            if (c < nc) {
-                const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
-                uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (k.res[r] == 0) continue;
-                    if (k.shift[r] == kDivIdentity) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], cur.fr[r][i]);
-                    } else if ((a.fast_res >> r) & 1u) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(cur.fr[r][i], k.magic31[r]) >> k.shift31[r]);
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const uint32_t n = cur.fr[r][i], h = __umulhi(n, k.magic[r]);
-                            cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    bool ok = valid[i] & ((cur.tn[i] & k.tol_inv) == 0);
-#pragma unroll
-                    for (int w = 0; w < W; ++w) ok = ok & ((cur.lab[w][i] & k.mask[w]) == k.req[w]);
-                    v[i] = ok ? cap[i] : 0u;
-                }
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v[i] = (valid[i] && cur.ex[i] != -1) ? 1u : 0u;
-            }
-            const uint32_t p0 = v[0], p1 = p0 + v[1], p2 = p1 + v[2], p3 = p2 + v[3];
-            const uint32_t incl = wave_incl_scan(p3, lane);
-            uint32_t* out = c < nc ? a.cap_out + (size_t)(a.c0 + c) * a.ld : a.occ_out;
-            if (single) {
-                // one leaf: this chunk's total, carried in s_pre's tail word of the value
-                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-                JSP_LDS uint32_t* accw = lds_ptr(lds + tally_acc_off(nc) + kTallyWaves * nv * kWaveTileRows) +
-                                         wid * kMaxClasses + c;
-                const uint32_t acc = (first_chunk ? 0u : *accw) + tot;
-                if (last_chunk) {
-                    if (lane == 0) out[a.leaf_base + l0] = acc;
-                } else if (lane == 0) {
-                    *accw = acc;
-                }
-                continue;
-            }
-            const uint32_t wex = incl - p3;
-            reinterpret_cast<JSP_LDS u32x4*>(s_pre + c * kWaveTileRows)[lane] = u32x4{wex + p0, wex + p1, wex + p2, incl};
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if ((uint32_t)lane < nl) {
-                uint32_t sum = 0;
-                const uint32_t lo = ls_lo, hi = ls_hi;
-                if (lo < hi) {
-                    const uint32_t hp = s_pre[c * kWaveTileRows + (hi - 1 - base)];
-                    const uint32_t bp = lo > base ? s_pre[c * kWaveTileRows + (lo - 1 - base)] : 0u;
-                    sum = hp - bp;
-                }
-                out[a.leaf_base + l0 + lane] = sum;
-            }
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-        if (!more) break;
-        if (nt != t) {
-            t = nt;
-            bt = nbt;
-            const uint32_t nnl = bt.y - bt.x;
-            ls_lo = ls_hi = 0;
-            if ((uint32_t)lane < nnl) {
-                ls_lo = a.leaf_start[bt.x + lane];
-                ls_hi = a.leaf_start[bt.x + lane + 1];
-            }
-        }
-        base = nbase;
-        cur = nxt;
+        wave_eval<W, R, NV>(a, s_cls, s_pre, btA, lane, A, sums);
+        const uint4 done_a = btA;
+        tA = tB + waves;
+        btA = tiles[tA < last ? tA : last];
+        wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, tA < n_tiles, lane, A);
+        wave_store<NV>(a, cap_r, occ_r, done_a, lane, sums);
+        if (tB >= n_tiles) break;
+        wave_eval<W, R, NV>(a, s_cls, s_pre, btB, lane, B, sums);
+        const uint4 done_b = btB;
+        tB = tA + waves;
+        btB = tiles[tB < last ? tB : last];
+        wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, tB < n_tiles, lane, B);
+        wave_store<NV>(a, cap_r, occ_r, done_b, lane, sums);
+        if (tA >= n_tiles) break;
     }
 }
 
@@ -2739,10 +2788,16 @@ static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
 }
 
 template <int W, int R>
-static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid,
-                                       hipStream_t s) {
-    hipLaunchKernelGGL((tally_wave_kernel<W, R>), dim3(grid), dim3(kTallyThreads),
-                       tally_wave_lds_bytes(a.nc, a.nc + a.do_occ), s, a, tiles, n_tiles);
+static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves,
+                                       uint32_t grid, hipStream_t s) {
+    const size_t lds = tally_wave_lds_bytes(a.nc, a.nc + 1);
+    switch (a.nc) {
+        case 1: hipLaunchKernelGGL((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 2: hipLaunchKernelGGL((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 3: hipLaunchKernelGGL((tally_wave_kernel<W, R, 4>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 4: hipLaunchKernelGGL((tally_wave_kernel<W, R, 5>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 
@@ -2789,8 +2844,9 @@ size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv) {
                                (size_t)kTallyWaves * kMaxClasses);
 }
 
-hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t grid, hipStream_t s) {
-    JSP_DISPATCH_WR(launch_tally_wave_wr, a, tiles, n_tiles, grid, s)
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
+                             hipStream_t s) {
+    JSP_DISPATCH_WR(launch_tally_wave_wr, a, tiles, n_tiles, n_leaves, grid, s)
 }
 
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
