@@ -80,3 +80,6 @@ tools/bin/stream_ceiling: tools/stream_ceiling.hip
 tools/bin/layout_probe: tools/layout_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
+tools/bin/mailbox_probe: tools/mailbox_probe.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $< -lhsa-runtime64

@@ -443,14 +443,17 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
 }
 
 // Workgroups of the wave-tile tally: JSP_TALLY_WPS waves per SIMD (default 2)
-// over the CUs, never more than the tiles need.
+// over the CUs, never more than the tiles need and never fewer than 64 tiles
+// per wave allow.
 uint32_t tally_wave_grid(jsp_engine* e) {
     static const uint32_t wps = [] {
         const char* v = std::getenv("JSP_TALLY_WPS");
         const long x = v ? std::strtol(v, nullptr, 10) : 2;
         return (uint32_t)(x >= 1 && x <= 16 ? x : 2);
     }();
-    const uint32_t waves = std::min<uint32_t>(e->n_wtiles, (uint32_t)std::max(e->n_cu, 1) * 4u * wps);
+    // at least n_wtiles / 64 waves: a wave holds at most 64 tile descriptors
+    const uint32_t waves = std::max<uint32_t>(std::min<uint32_t>(e->n_wtiles, (uint32_t)std::max(e->n_cu, 1) * 4u * wps),
+                                              (e->n_wtiles + 63) / 64);
     return std::max<uint32_t>(1, (waves + jsp::kTallyWaves - 1) / jsp::kTallyWaves);
 }
 
@@ -1278,7 +1281,8 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     for (size_t b = 0; b + 1 < blk.size(); ++b) bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
     e->blk_l0.assign(blk.begin(), blk.end() - (blk.empty() ? 0 : 1));
     e->blk_l1.assign(blk.begin() + (blk.empty() ? 0 : 1), blk.end());
-    HIP_TRY(upload(e->blk, bt.data(), std::max<size_t>(bt.size(), 1), s));
+    if (bt.empty()) bt.push_back(make_uint4(0, 0, 0, 0));  // no rows: never read
+    HIP_TRY(upload(e->blk, bt.data(), bt.size(), s));
     {
         // wave tiles: up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4
         // rows (one wave chunk at any row alignment), or one larger leaf alone
@@ -1296,8 +1300,9 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
             wt.push_back(make_uint4(l, end, r0, ls[end]));
             l = end;
         }
-        HIP_TRY(upload(e->wtiles, wt.data(), std::max<size_t>(wt.size(), 1), s));
         e->n_wtiles = (uint32_t)wt.size();
+        if (wt.empty()) wt.push_back(make_uint4(0, 0, 0, 0));  // never read (n_wtiles == 0)
+        HIP_TRY(upload(e->wtiles, wt.data(), wt.size(), s));
     }
     HIP_TRY(e->ticket.reserve(16));
     HIP_TRY(hipMemsetAsync(e->ticket.p, 0, 16, s));  // single-launch tickets (tile draws, finished tiles)

@@ -650,49 +650,58 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     constexpr int nc = NV - 1;  // this launch: NV - 1 classes and the occupancy count
     constexpr int nv = NV;
     const int tid = threadIdx.x, lane = tid & 63;
-    // wave-uniform in SGPRs: the tile descriptors are then scalar loads (lgkmcnt),
-    // which never make a wave wait for its in-flight row loads (vmcnt)
+    // wave-uniform in SGPRs, so every tile index and descriptor below is scalar
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t waves = gridDim.x * kTallyWaves;
+    const uint32_t t0 = blockIdx.x * kTallyWaves + wid;
+    // the wave's tiles are t0, t0 + waves, ...: lane k holds the k-th one's
+    // descriptor (<= 64, checked by the host), loaded once beside the class
+    // staging, so no tile waits on a descriptor load
+    uint4 dl = make_uint4(0, 0, 0, 0);
+    if (t0 + (uint32_t)lane * waves < n_tiles) dl = tiles[t0 + (uint32_t)lane * waves];
     constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
     if (tid < nc * kClsVec) reinterpret_cast<uint4*>(lds)[tid] = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
     __syncthreads();
+    if (t0 >= n_tiles) return;
+    const uint32_t nt = (n_tiles - t0 + waves - 1) / waves;  // this wave's tiles
     const DevClass* s_cls = reinterpret_cast<const DevClass*>(lds);  // read once per class and tile, into SGPRs
     JSP_LDS uint32_t* s_pre = lds_ptr(lds + tally_acc_off(nc) + wid * nv * kWaveTileRows);
-    const uint32_t waves = gridDim.x * kTallyWaves;
-    uint32_t tA = blockIdx.x * kTallyWaves + wid;
-    if (tA >= n_tiles) return;
+    auto desc = [&](uint32_t k) {
+        const int l = (int)(k < nt ? k : nt - 1);
+        return make_uint4(__builtin_amdgcn_readlane(dl.x, l), __builtin_amdgcn_readlane(dl.y, l),
+                          __builtin_amdgcn_readlane(dl.z, l), __builtin_amdgcn_readlane(dl.w, l));
+    };
     const WaveRsrc rs{make_rsrc(a.labels, (uint32_t)W * a.npad * 8u), make_rsrc(a.taints, a.npad * 4u),
                       make_rsrc(a.freer, (uint32_t)R * a.npad * 4u), make_rsrc(a.excl, a.npad * 4u),
                       make_rsrc(a.leaf_start, (n_leaves + 1u) * 4u)};
     const __amdgpu_buffer_rsrc_t cap_r = make_rsrc(a.cap_out, (a.c0 + (uint32_t)nc) * a.ld * 4u);
     const __amdgpu_buffer_rsrc_t occ_r = make_rsrc(a.occ_out, a.do_occ ? a.ld * 4u : 0u);
-    const uint32_t last = n_tiles - 1;
     WaveSet<W, R> A, B;
-    uint4 btA = tiles[tA];
+    uint32_t kA = 0, kB = 1;
+    uint4 btA = desc(kA);
     wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, true, lane, A);
     // keep set A's loads ahead of set B's: the loop header's waits merge this
     // order with the loop's, and an interleaved prologue would make them wait
     // for nearly every load in flight
     __builtin_amdgcn_sched_barrier(0);
-    uint32_t tB = tA + waves;
-    uint4 btB = tiles[tB < last ? tB : last];
-    wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, tB < n_tiles, lane, B);
+    uint4 btB = desc(kB);
+    wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, kB < nt, lane, B);
     uint32_t sums[NV];
     while (true) {
         wave_eval<W, R, NV>(a, s_cls, s_pre, btA, lane, A, sums);
         const uint4 done_a = btA;
-        tA = tB + waves;
-        btA = tiles[tA < last ? tA : last];
-        wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, tA < n_tiles, lane, A);
+        kA = kB + 1;
+        btA = desc(kA);
+        wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, kA < nt, lane, A);
         wave_store<NV>(a, cap_r, occ_r, done_a, lane, sums);
-        if (tB >= n_tiles) break;
+        if (kB >= nt) break;
         wave_eval<W, R, NV>(a, s_cls, s_pre, btB, lane, B, sums);
         const uint4 done_b = btB;
-        tB = tA + waves;
-        btB = tiles[tB < last ? tB : last];
-        wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, tB < n_tiles, lane, B);
+        kB = kA + 1;
+        btB = desc(kB);
+        wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, kB < nt, lane, B);
         wave_store<NV>(a, cap_r, occ_r, done_b, lane, sums);
-        if (tA >= n_tiles) break;
+        if (kA >= nt) break;
     }
 }
 
@@ -2791,6 +2800,8 @@ template <int W, int R>
 static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves,
                                        uint32_t grid, hipStream_t s) {
     const size_t lds = tally_wave_lds_bytes(a.nc, a.nc + 1);
+    // a wave holds at most 64 tile descriptors, one per lane
+    if ((uint64_t)grid * kTallyWaves * 64u < n_tiles) return hipErrorInvalidValue;
     switch (a.nc) {
         case 1: hipLaunchKernelGGL((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
         case 2: hipLaunchKernelGGL((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
