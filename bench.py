@@ -171,17 +171,23 @@ def event_loop_us(fn, k: int, stream) -> float:
     return a.elapsed_time(b) * 1e3 / k
 
 
-def cold_us(fn, k: int, stream, scrub) -> float:
+def cold_us(fn, k: int, stream, scrub, dirty: bool = False) -> float:
     """Median µs of one call of `fn` with cold caches: before each call a
-    512 MiB buffer is read and written on the same stream, which evicts the
-    256 MiB Infinity Cache and every XCD's L2; HIP events bracket the call."""
+    512 MiB buffer is read on the same stream (a sum: no lines dirtied, as the
+    read-only scrub of tools/stream_ceiling.hip), which evicts the 256 MiB
+    Infinity Cache and every XCD's L2; HIP events bracket the call. dirty=True
+    reads and writes it instead (add_): the call's misses then also pay the
+    write-back of the scrub's dirty lines."""
     import torch
     s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.default_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
     with torch.cuda.stream(s):
         for _ in range(k):
-            scrub.add_(1)
+            if dirty:
+                scrub.add_(1)
+            else:
+                scrub.sum()
             a.record(s)
             fn()
             b.record(s)
@@ -549,15 +555,18 @@ def main() -> None:
                                  tally_loop, stream)
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
-        tally_cold = cold_us(lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream),
-                             20, stream, scrub)
+        tally_fn = lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream)  # noqa: E731
+        tally_cold = cold_us(tally_fn, 20, stream, scrub)
+        tally_cold_dirty = cold_us(tally_fn, 20, stream, scrub, dirty=True)
         copy_ceiling = None
         if world == 1:  # achievable streaming rate: a cold copy of the same byte count
             src = torch.empty(tb4 // 2 // 16 * 4, dtype=torch.int32, device="cuda").fill_(1)
             dst = torch.empty_like(src)
             cu = cold_us(lambda: dst.copy_(src), 20, stream, scrub)
+            cud = cold_us(lambda: dst.copy_(src), 20, stream, scrub, dirty=True)
             copy_ceiling = {"bytes": 2 * src.numel() * 4, "cold_us": round(cu, 2),
-                            "cold_gbs": round(2 * src.numel() * 4 / (cu * 1e-6) / 1e9, 1)}
+                            "cold_gbs": round(2 * src.numel() * 4 / (cu * 1e-6) / 1e9, 1),
+                            "cold_dirty_us": round(cud, 2)}
             del src, dst
         del scrub
         sp.engine.check()
@@ -588,6 +597,9 @@ def main() -> None:
                 "tally_cold_us": round(tally_cold, 2),
                 "tally_cold_gbs": round(tb4 / (tally_cold * 1e-6) / 1e9, 1),
                 "tally_cold_frac": round(tb4 / (tally_cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                "tally_cold_dirty_us": round(tally_cold_dirty, 2),
+                "cold_note": "cold: a 512 MiB read-only scrub before each launch (as tools/stream_ceiling.hip); "
+                             "cold_dirty: the scrub also writes it, so the launch's misses pay its write-backs",
                 "copy_ceiling_same_bytes": copy_ceiling,
                 "tally_traffic": pmc_traffic("tally_kernel", 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),

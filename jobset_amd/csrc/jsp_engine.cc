@@ -253,10 +253,15 @@ int stream_mark_mode() {
         if (!v) return 0;
         if (std::strcmp(v, "value") == 0) return 1;
         if (std::strcmp(v, "none") == 0) return 2;
+        if (std::strcmp(v, "record") == 0) return 3;
         return 0;
     }();
     return m;
 }
+// Mode 0 (default): ev_last rides on the call's kernel launches as their stop
+// event (jsp::set_launch_stop), so it completes with the last kernel and no
+// marker packet follows it; a call that launched nothing records it. Mode 3:
+// an hipEventRecord after every call (the round-2 fix; A/B).
 
 // Flags of ev_last (JSP_EVENT_FLAGS: "sys" = a system-scope release on record,
 // the HIP default; "dev" = device-scope release; "nofence" = none). Ordering a
@@ -272,7 +277,7 @@ int wait_prior(jsp_engine* e, hipStream_t s) {
     if (!e->have_last) return JSP_OK;
     if (e->last_foreign) {
         const int mm = stream_mark_mode();
-        if (mm == 0) HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
+        if (mm == 0 || mm == 3) HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
         else if (mm == 1)
             HIP_TRY(hipStreamWaitValue64(s, e->mark.p, e->mark_seq, hipStreamWaitValueGte, ~0ull));
     } else {
@@ -287,19 +292,23 @@ int wait_prior(jsp_engine* e, hipStream_t s) {
 // another stream (uploads and jsp_place use the engine stream, the device
 // entry points the caller's). Calls on one stream cost nothing here.
 int enter_stream(jsp_engine* e, hipStream_t s) {
-    if (e->have_last && e->last_stream != s) return wait_prior(e, s);
+    if (e->have_last && e->last_stream != s)
+        if (int rc = wait_prior(e, s)) return rc;
+    if (s != e->stream && stream_mark_mode() == 0) jsp::set_launch_stop(e->ev_last);
     return JSP_OK;
 }
 
 // After a call enqueued its work on s: a caller's stream gets ev_last
 // recorded on it while the handle is known to be valid.
 int leave_stream(jsp_engine* e, hipStream_t s) {
+    const bool launched = jsp::launch_stop_used();
+    jsp::set_launch_stop(nullptr);
     e->last_stream = s;
     e->have_last = true;
     e->last_foreign = s != e->stream;
     if (e->last_foreign) {
         const int mm = stream_mark_mode();
-        if (mm == 0) {
+        if ((mm == 0 && !launched) || mm == 3) {
             HIP_TRY(hipEventRecord(e->ev_last, s));
         } else if (mm == 1) {
             if (!e->mark.p) {
@@ -315,7 +324,7 @@ int leave_stream(jsp_engine* e, hipStream_t s) {
 // Host wait for the last caller-stream call's work.
 int wait_last_foreign(jsp_engine* e) {
     const int mm = stream_mark_mode();
-    if (mm == 0) HIP_TRY(hipEventSynchronize(e->ev_last));
+    if (mm == 0 || mm == 3) HIP_TRY(hipEventSynchronize(e->ev_last));
     else if (mm == 1)
         while (__atomic_load_n(e->mark.as<uint64_t>(), __ATOMIC_ACQUIRE) < e->mark_seq) __builtin_ia32_pause();
     else HIP_TRY(hipDeviceSynchronize());
@@ -473,7 +482,11 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
         const bool wave = !block && e->n_wtiles > 0 && a.do_occ && a.nc >= 1 && a.nc <= 4 &&
                           (uint64_t)(e->C + 1) * ld * 4 < (1ull << 31);
         if (!wave) HIP_TRY(jsp::launch_tally(a, s));
-        else HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, tally_wave_grid(e), s));
+        else {
+            jsp::WaveClasses kc{};
+            for (uint32_t c = 0; c < a.nc; ++c) kc.c[c] = e->cls_h[c0 + c];
+            HIP_TRY(jsp::launch_tally_wave(a, kc, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, tally_wave_grid(e), s));
+        }
         c0 += a.nc;
     } while (c0 < e->C);
     ev_end(p, s);

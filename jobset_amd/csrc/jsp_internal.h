@@ -221,13 +221,25 @@ struct AssignPlan {
 };
 AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_words);
 
+// While set (non-null), every launch records `ev` at its kernel's completion
+// (the device-path calls' end-of-call marker); launch_stop_used() says whether
+// a launch did since the last set.
+void set_launch_stop(hipEvent_t ev);
+bool launch_stop_used();
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 // Wave-tile tally (tally_wave_kernel): tiles {first leaf, end leaf, first row,
 // end row} of up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4 rows
 // (snapshots with a larger leaf use the workgroup tally), 1-4 classes and the
 // occupancy count in one pass; `grid` workgroups of 4 waves take them in turn. Every column's bytes must stay below 2^31
 // (buffer offsets; the host checks).
-hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
+// The wave-tile tally's classes, passed by value: kernel arguments are read by
+// scalar loads, so a class's fields reach SGPRs without LDS staging, a
+// workgroup barrier or readfirstlane (c[0..nc) = classes c0 .. c0 + nc - 1).
+struct WaveClasses {
+    DevClass c[4];
+};
+hipError_t launch_tally_wave(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
+                             uint32_t n_leaves, uint32_t grid,
                              hipStream_t s);
 size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);

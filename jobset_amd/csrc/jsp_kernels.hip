@@ -20,6 +20,7 @@
 // Plus gather kernels for the webhook / reconciler batch paths (A5, A9) and the
 // snapshot patch.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 
 #include <algorithm>
@@ -47,7 +48,15 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
     do {                                                                                  \
         if (threadIdx.x == 0 && (row) < 4096) jsp_dbg[(row) * 8 + (i)] = (unsigned long long)(v); \
     } while (0)
+// per-wave real-time stamp (lane 0 of each wave)
+#define JSP_WSTAMP(w, i)                                                                  \
+    do {                                                                                  \
+        if ((threadIdx.x & 63) == 0 && (w) < 4096) jsp_dbg[(w) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
 #else
+#define JSP_WSTAMP(w, i) \
+    do {                 \
+    } while (0)
 #define JSP_DBGV(row, i, v) \
     do {                    \
     } while (0)
@@ -560,22 +569,48 @@ __device__ __forceinline__ void wave_issue(const TallyArgs& a, const WaveRsrc& r
 // Evaluate one tile from `v` and store its leaves' sums: NV values, the
 // first NV - 1 classes and the occupancy count (compile-time, so every store
 // of the unrolled loop is counted by the compiler's waits).
+// The fields of one class straight from the kernel arguments (scalar loads).
+template <int W, int R>
+__device__ __forceinline__ ClassRegs<W, R> class_args(const DevClass& d) {
+    ClassRegs<W, R> k;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        k.req[w] = d.req[w];
+        k.mask[w] = d.mask[w];
+    }
+    k.tol_inv = d.tol_inv;
+    k.pods = d.pods;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        k.res[r] = d.res[r];
+        k.magic[r] = d.magic[r];
+        k.shift[r] = d.shift[r];
+        k.magic31[r] = d.magic31[r];
+        k.shift31[r] = d.shift31[r];
+    }
+    return k;
+}
+
+// Evaluate one tile from `v` and keep its leaves' sums: NV values, the first
+// NV - 1 classes and the occupancy count (compile-time, so every store of the
+// unrolled loop is counted by the compiler's waits). Rows outside the tile's
+// leaves are evaluated like any other and not masked: a leaf's sum is
+// prefix(its last row) - prefix(the row before its first), and a row before
+// the tile's first leaf is in both prefixes, a row after its last leaf in
+// neither (the u32 differences are exact: a tile's prefix stays below
+// 256 x 2^22 -- pods <= 2^22, checked at class upload).
 template <int W, int R, int NV>
-__device__ __forceinline__ void wave_eval(const TallyArgs& a, const DevClass* s_cls, JSP_LDS uint32_t* s_pre, uint4 bt,
+__device__ __forceinline__ void wave_eval(const TallyArgs& a, const WaveClasses& kc, JSP_LDS uint32_t* s_pre, uint4 bt,
                                           int lane, const WaveSet<W, R>& v, uint32_t (&sums)[NV]) {
     constexpr int nc = NV - 1;
     const uint32_t base = bt.z & ~3u;
-    const uint32_t row = base + 4u * (uint32_t)lane;
-    bool valid[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) valid[i] = row + i >= bt.z && row + i < bt.w;
-    const uint32_t l0 = bt.x, nl = bt.y - bt.x;
+    const uint32_t nl = bt.y - bt.x;
     const bool has_leaf = (uint32_t)lane < nl;
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
         uint32_t val[4];
         if (c < nc) {
-            const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
+            const ClassRegs<W, R> k = class_args<W, R>(kc.c[c]);
             uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
@@ -596,14 +631,14 @@ __device__ __forceinline__ void wave_eval(const TallyArgs& a, const DevClass* s_
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                bool ok = valid[i] & ((v.x.tn[i] & k.tol_inv) == 0);
+                bool ok = (v.x.tn[i] & k.tol_inv) == 0;
 #pragma unroll
                 for (int w = 0; w < W; ++w) ok = ok & ((v.x.lab[w][i] & k.mask[w]) == k.req[w]);
                 val[i] = ok ? cap[i] : 0u;
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) val[i] = (valid[i] && v.x.ex[i] != -1) ? 1u : 0u;
+            for (int i = 0; i < 4; ++i) val[i] = v.x.ex[i] != -1 ? 1u : 0u;
         }
         const uint32_t p0 = val[0], p1 = p0 + val[1], p2 = p1 + val[2], p3 = p2 + val[3];
         const uint32_t incl = wave_incl_scan(p3, lane);
@@ -644,7 +679,8 @@ __device__ __forceinline__ void wave_store(const TallyArgs& a, __amdgpu_buffer_r
 }
 
 template <int W, int R, int NV>
-__global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, const uint4* __restrict__ tiles,
+__global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, WaveClasses kc,
+                                                                   const uint4* __restrict__ tiles,
                                                                    uint32_t n_tiles, uint32_t n_leaves) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr int nc = NV - 1;  // this launch: NV - 1 classes and the occupancy count
@@ -655,17 +691,16 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     const uint32_t waves = gridDim.x * kTallyWaves;
     const uint32_t t0 = blockIdx.x * kTallyWaves + wid;
     // the wave's tiles are t0, t0 + waves, ...: lane k holds the k-th one's
-    // descriptor (<= 64, checked by the host), loaded once beside the class
-    // staging, so no tile waits on a descriptor load
+    // descriptor (<= 64, checked by the host), loaded once, so no later tile
+    // waits on a descriptor load. No workgroup barrier: the classes come from
+    // the kernel arguments and each wave has its own LDS slice.
+    JSP_WSTAMP(t0, 0);
+    if (t0 >= n_tiles) return;
     uint4 dl = make_uint4(0, 0, 0, 0);
     if (t0 + (uint32_t)lane * waves < n_tiles) dl = tiles[t0 + (uint32_t)lane * waves];
-    constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
-    if (tid < nc * kClsVec) reinterpret_cast<uint4*>(lds)[tid] = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
-    __syncthreads();
-    if (t0 >= n_tiles) return;
+    JSP_WSTAMP(t0, 1);
     const uint32_t nt = (n_tiles - t0 + waves - 1) / waves;  // this wave's tiles
-    const DevClass* s_cls = reinterpret_cast<const DevClass*>(lds);  // read once per class and tile, into SGPRs
-    JSP_LDS uint32_t* s_pre = lds_ptr(lds + tally_acc_off(nc) + wid * nv * kWaveTileRows);
+    JSP_LDS uint32_t* s_pre = lds_ptr(lds + wid * nv * kWaveTileRows);
     auto desc = [&](uint32_t k) {
         const int l = (int)(k < nt ? k : nt - 1);
         return make_uint4(__builtin_amdgcn_readlane(dl.x, l), __builtin_amdgcn_readlane(dl.y, l),
@@ -687,15 +722,18 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     uint4 btB = desc(kB);
     wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, kB < nt, lane, B);
     uint32_t sums[NV];
+    bool first = true;
     while (true) {
-        wave_eval<W, R, NV>(a, s_cls, s_pre, btA, lane, A, sums);
+        wave_eval<W, R, NV>(a, kc, s_pre, btA, lane, A, sums);
+        if (first) JSP_WSTAMP(t0, 2);
+        first = false;
         const uint4 done_a = btA;
         kA = kB + 1;
         btA = desc(kA);
         wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, kA < nt, lane, A);
         wave_store<NV>(a, cap_r, occ_r, done_a, lane, sums);
         if (kB >= nt) break;
-        wave_eval<W, R, NV>(a, s_cls, s_pre, btB, lane, B, sums);
+        wave_eval<W, R, NV>(a, kc, s_pre, btB, lane, B, sums);
         const uint4 done_b = btB;
         kB = kA + 1;
         btB = desc(kB);
@@ -703,6 +741,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
         wave_store<NV>(a, cap_r, occ_r, done_b, lane, sums);
         if (kA >= nt) break;
     }
+    JSP_WSTAMP(t0, 3);
 }
 
 // ----------------------------------------------------------------- feasibility
@@ -2789,24 +2828,47 @@ __global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst
 }
 
 // ----------------------------------------------------------------- launchers
+// Every launch goes through jsp_launch. While a device-path call on a caller's
+// stream is being enqueued, the engine names an event (set_launch_stop): each
+// launch then carries it as its stop event (hipExtLaunchKernel), so the event
+// completes with the call's last kernel -- the kernel's own completion signal,
+// with no marker packet behind it on the caller's stream (an hipEventRecord
+// after each call cost 2-3 us of GPU time per call, profiles/r03).
+namespace {
+thread_local hipEvent_t t_stop = nullptr;
+thread_local bool t_stop_used = false;
+}  // namespace
+void set_launch_stop(hipEvent_t ev) {
+    t_stop = ev;
+    t_stop_used = false;
+}
+bool launch_stop_used() { return t_stop_used; }
+
+template <typename F, typename... Args>
+static inline void jsp_launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t s,
+                              Args... args) {
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, nullptr, t_stop, 0u, args...);
+    if (t_stop) t_stop_used = true;
+}
+
 template <int W, int R>
 static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
-    hipLaunchKernelGGL((tally_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
+    jsp_launch((tally_kernel<W, R>), dim3(a.n_blocks), dim3(kTallyThreads),
                        sizeof(uint32_t) * tally_lds_words(a), s, a);
     return hipGetLastError();
 }
 
 template <int W, int R>
-static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves,
-                                       uint32_t grid, hipStream_t s) {
+static hipError_t launch_tally_wave_wr(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
+                                       uint32_t n_leaves, uint32_t grid, hipStream_t s) {
     const size_t lds = tally_wave_lds_bytes(a.nc, a.nc + 1);
     // a wave holds at most 64 tile descriptors, one per lane
     if ((uint64_t)grid * kTallyWaves * 64u < n_tiles) return hipErrorInvalidValue;
     switch (a.nc) {
-        case 1: hipLaunchKernelGGL((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
-        case 2: hipLaunchKernelGGL((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
-        case 3: hipLaunchKernelGGL((tally_wave_kernel<W, R, 4>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
-        case 4: hipLaunchKernelGGL((tally_wave_kernel<W, R, 5>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 1: jsp_launch((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
+        case 2: jsp_launch((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
+        case 3: jsp_launch((tally_wave_kernel<W, R, 4>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
+        case 4: jsp_launch((tally_wave_kernel<W, R, 5>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2814,14 +2876,14 @@ static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, u
 
 template <int W, int R>
 static hipError_t launch_fused_wr(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL((place_fused_kernel<W, R>), dim3(a.n_blocks * f.groups + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
+    jsp_launch((place_fused_kernel<W, R>), dim3(a.n_blocks * f.groups + kSpareBlocks), dim3(kTallyThreads), f.lds_bytes,
                        s, a, f);
     return hipGetLastError();
 }
 
 template <int W, int R>
 static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hipStream_t s) {
-    hipLaunchKernelGGL((place_compact_kernel<W, R>), dim3(a.n_blocks + kSpareBlocks), dim3(kTallyThreads),
+    jsp_launch((place_compact_kernel<W, R>), dim3(a.n_blocks + kSpareBlocks), dim3(kTallyThreads),
                        compact_lds_bytes(a.la), s, a, f);
     return hipGetLastError();
 }
@@ -2850,14 +2912,13 @@ static hipError_t launch_compact_wr(const TallyArgs& a, const CompactArgs& f, hi
 
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s) { JSP_DISPATCH_WR(launch_tally_wr, a, s) }
 
-size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv) {
-    return sizeof(uint32_t) * ((size_t)tally_acc_off((int)nc) + (size_t)kTallyWaves * nv * kWaveTileRows +
-                               (size_t)kTallyWaves * kMaxClasses);
+size_t tally_wave_lds_bytes(uint32_t /*nc*/, uint32_t nv) {
+    return sizeof(uint32_t) * (size_t)kTallyWaves * nv * kWaveTileRows;
 }
 
-hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
-                             hipStream_t s) {
-    JSP_DISPATCH_WR(launch_tally_wave_wr, a, tiles, n_tiles, n_leaves, grid, s)
+hipError_t launch_tally_wave(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
+                             uint32_t n_leaves, uint32_t grid, hipStream_t s) {
+    JSP_DISPATCH_WR(launch_tally_wave_wr, a, kc, tiles, n_tiles, n_leaves, grid, s)
 }
 
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {
@@ -2870,7 +2931,7 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 
 template <int W, int R>
 static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
-    hipLaunchKernelGGL((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), compact_lds_bytes(a.la),
+    jsp_launch((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), compact_lds_bytes(a.la),
                        s, a, v);
     return hipGetLastError();
 }
@@ -2882,7 +2943,7 @@ hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t 
 template <int W, int R>
 static hipError_t launch_fused_service_wr(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v,
                                           hipStream_t s) {
-    hipLaunchKernelGGL((place_fused_service_kernel<W, R>), dim3(a.n_blocks * f.groups + 1), dim3(kTallyThreads), f.lds_bytes,
+    jsp_launch((place_fused_service_kernel<W, R>), dim3(a.n_blocks * f.groups + 1), dim3(kTallyThreads), f.lds_bytes,
                        s, a, f, v);
     return hipGetLastError();
 }
@@ -2898,7 +2959,7 @@ size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
 template <int W, int R>
 static hipError_t launch_split_service_wr(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v,
                                           hipStream_t s) {
-    hipLaunchKernelGGL((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups + 1), dim3(kTallyThreads),
+    jsp_launch((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups + 1), dim3(kTallyThreads),
                        split_lds_bytes(sp.cpg, a.la), s, a, sp, v);
     return hipGetLastError();
 }
@@ -2967,7 +3028,7 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
                        hipStream_t s) {
     if (total_words == 0) return hipSuccess;
     const uint32_t blocks = (total_words + 3) / 4;
-    hipLaunchKernelGGL(feas_kernel, dim3(blocks), dim3(256), 0, s, cap, occ, ld, cls, C, word_off, topo, feas);
+    jsp_launch(feas_kernel, dim3(blocks), dim3(256), 0, s, cap, occ, ld, cls, C, word_off, topo, feas);
     return hipGetLastError();
 }
 
@@ -2987,13 +3048,13 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
     const uint32_t topo_words = topo.K > 1 ? topo_table_words(topo.K, topo.D) : 0u;
     const AssignPlan p = plan_assign(t_words, feas_words, topo_words);
     if (p.lds_bytes == 0) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
+    jsp_launch(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
                        run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
                        topo_words, p.stage_cap, recs, rec_count, pipe_walk_enabled() ? 1u : 0u);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
     // records never outnumber the placed jobs (each taken domain is in one record)
     const uint32_t waves = J < 8192u ? J : 8192u;
-    hipLaunchKernelGGL(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, assign);
+    jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, assign);
     return hipGetLastError();
 }
 
@@ -3001,7 +3062,7 @@ hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t 
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, levels, n, n_rows, leaf_start,
+    jsp_launch(resolve_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, levels, n, n_rows, leaf_start,
                        n_leaves, leaf_base, topo, out);
     return hipGetLastError();
 }
@@ -3010,7 +3071,7 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
                         const int32_t* fdom, uint32_t n_jobs, uint32_t n_rows, const uint32_t* leaf_start,
                         uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo, uint32_t* bad, hipStream_t s) {
     if (n_jobs == 0) return hipSuccess;
-    hipLaunchKernelGGL(audit_kernel, dim3((n_jobs + 3) / 4), dim3(256), 0, s, leader_rows, levels, foff, fdom,
+    jsp_launch(audit_kernel, dim3((n_jobs + 3) / 4), dim3(256), 0, s, leader_rows, levels, foff, fdom,
                        n_jobs, n_rows, leaf_start, n_leaves, leaf_base, topo, bad);
     return hipGetLastError();
 }
@@ -3018,7 +3079,7 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
 hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const size_t blocks = std::min<size_t>(1024, (n / 4 + 255) / 256 + 1);
-    hipLaunchKernelGGL(add_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
+    jsp_launch(add_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 
@@ -3026,7 +3087,7 @@ hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_
                         const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
                         uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s) {
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, n, npad, W, R, dlab, dtaint,
+    jsp_launch(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, n, npad, W, R, dlab, dtaint,
                        dfree, dexcl, labels, taints, freer, excl);
     return hipGetLastError();
 }

@@ -12,6 +12,7 @@
 #   pmc       separate rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / SQ) on configs 2, 4, 5
 #   py:FILE[:ARG]  python FILE ARG (a probe under tools/) -> FILE_ARG.txt
 #   pytest:SEL     pytest SEL -m gpu (one file or node id)
+#   tracepy:NAME:FILE[:ARG]  rocprofv3 --kernel-trace --stats of python FILE ARG -> NAME/ (+ NAME_summary.txt)
 # Every GPU step runs under its own time limit; the script stops at the first
 # failure, time-out or crash (nothing further touches the GPU).
 set -u
@@ -44,9 +45,13 @@ for step in "$@"; do
                  run 120 "$OUT/pmc_sq$cfg.log" rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/pmc_sq$cfg" -o run --output-format csv -- python3 "$R/tools/run_cfg.py" --cfg $cfg --steps 20
                done ) || exit $?
              python3 tools/summarize_prof.py "$OUT" > "$OUT/summary.txt" 2>&1 ;;
-    py:*)    spec="${step#py:}"; f="${spec%%:*}"; arg=""; [ "$spec" != "$f" ] && arg="${spec#*:}"
-             log="$OUT/$(basename "$f" .py)${arg:+_$arg}.txt"
+    py:*)    spec="${step#py:}"; f="${spec%%:*}"; arg=""; [ "$spec" != "$f" ] && arg="${spec#*:}"; arg="${arg//:/ }"
+             log="$OUT/$(basename "$f" .py)${arg:+_${arg// /_}}.txt"
              run 600 "$log" python3 -u "$f" $arg; tail -30 "$log" ;;
+    tracepy:*) spec="${step#tracepy:}"; name="${spec%%:*}"; rest="${spec#*:}"; f="${rest%%:*}"; arg=""
+             [ "$rest" != "$f" ] && arg="${rest#*:}"; arg="${arg//:/ }"
+             ( cd /tmp && export TMPDIR=/tmp && run 300 "$OUT/$name.log" rocprofv3 --kernel-trace --stats -d "$OUT/$name" -o run --output-format csv -- python3 "$R/$f" $arg ) || exit $?
+             python3 tools/summarize_prof.py "$OUT/$name" > "$OUT/${name}_summary.txt" 2>&1; tail -25 "$OUT/${name}_summary.txt" ;;
     pytest:*) sel="${step#pytest:}"; run 900 "$OUT/pytest_$(echo "$sel" | tr '/:' '__').log" python -u -m pytest $sel -m gpu -x -q --timeout 120 --timeout-method thread
              tail -3 "$OUT/pytest_$(echo "$sel" | tr '/:' '__').log" ;;
     *)       echo "unknown step $step"; exit 2 ;;

@@ -20,12 +20,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave1": {"JSP_TALLY_WPS": "1"}, "wave2": {"JSP_TALLY_WPS": "2"},
-         "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"}}
+         "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"},
+         "wave6": {"JSP_TALLY_WPS": "6"}, "wave8": {"JSP_TALLY_WPS": "8"}}
 SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
        "svc_rows508": {"JSP_BLOCK_ROWS": "508"}, "svc_rows252": {"JSP_BLOCK_ROWS": "252"},
        "svc_split_rows252": {"JSP_SPLIT_COMPACT": "1", "JSP_BLOCK_ROWS": "252"},
        "svc_cold_sync": {"JSP_COLD_LAUNCH": "0"}}
-MARK = {"event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
+MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
 
@@ -55,9 +56,10 @@ def child_tally():
     warm = bench.event_loop_us(fn, 200, stream)
     scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")
     cold = bench.cold_us(fn, 20, stream, scrub)
+    cold_dirty = bench.cold_us(fn, 20, stream, scrub, dirty=True)
     eng.check()
     tb = bench.tally_bytes(p)
-    return {"exact": exact, "warm_us": round(warm, 2), "cold_us": round(cold, 2),
+    return {"exact": exact, "warm_us": round(warm, 2), "cold_us": round(cold, 2), "cold_dirty_us": round(cold_dirty, 2),
             "warm_frac": round(tb / warm / 1e3 / 8000, 4), "cold_frac": round(tb / cold / 1e3 / 8000, 4)}
 
 
@@ -142,6 +144,8 @@ def main():
     mode = sys.argv[1]
     if mode == "one":
         key = sys.argv[2]
+        for d in (TALLY, SVC, MARK):  # the variant's environment (also when run directly, e.g. under rocprofv3)
+            os.environ.update(d.get(key, {}))
         res = child_tally() if key in TALLY else child_svc() if key in SVC else child_mark()
         print(json.dumps({key: res}), flush=True)
         return

@@ -21,7 +21,8 @@ def main(root):
         print("##", os.path.relpath(f, root))
         for (k, g), v in sorted(by.items()):
             v.sort()
-            print(f"  {k:40s} grid={g:>8s} n={len(v):5d} median_ns={v[len(v)//2]:8d} min_ns={v[0]:8d}")
+            print(f"  {k:40s} grid={g:>8s} n={len(v):5d} median_ns={v[len(v)//2]:8d} min_ns={v[0]:8d} "
+                  f"p90_ns={v[min(len(v) - 1, len(v) * 9 // 10)]:8d} max_ns={v[-1]:8d}")
     for f in sorted(glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True)):
         agg = collections.defaultdict(lambda: collections.defaultdict(list))
         for r in csv.DictReader(open(f)):
