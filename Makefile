@@ -83,3 +83,13 @@ tools/bin/layout_probe: tools/layout_probe.hip
 tools/bin/mailbox_probe: tools/mailbox_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $< -lhsa-runtime64
+tools/bin/valu_rate: tools/valu_rate.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
+
+# A/B builds of the kernels with one build flag (tools/ab_probe.py loads them
+# through JSP_LIB_PATH): tools/ablib/<name>/libjsplace.so
+tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_$* tools/ablib/$*
+	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS_$*) -c -o build/ab_$*/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_$*/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

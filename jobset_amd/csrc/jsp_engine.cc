@@ -131,7 +131,6 @@ struct jsp_engine {
     DevBuf wtiles;              // wave tiles of the three-launch tally (tally_wave_kernel)
     uint32_t n_wtiles = 0;
     uint32_t n_blocks = 0;
-    uint32_t fast_res = 0;  // bit r: every free[r] < 2^31 (upload: computed; patches only clear bits)
     uint32_t epoch = 0;  // compaction launches so far (granule tags)
 
     // classes
@@ -447,18 +446,18 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
     a.c0 = 0;
     a.nc = std::min<uint32_t>(e->C, jsp::kTallyClasses);
     a.do_occ = 1;
-    a.fast_res = std::getenv("JSP_NO_FAST_DIV") ? 0u : e->fast_res;
     return a;
 }
 
-// Workgroups of the wave-tile tally: JSP_TALLY_WPS waves per SIMD (default 2)
+// Workgroups of the wave-tile tally: JSP_TALLY_WPS waves per SIMD (default 4:
+// best warm and cold of 1-8 on cfg4, tools/ab_probe.py tally, profiles/r03)
 // over the CUs, never more than the tiles need and never fewer than 64 tiles
 // per wave allow.
 uint32_t tally_wave_grid(jsp_engine* e) {
     static const uint32_t wps = [] {
         const char* v = std::getenv("JSP_TALLY_WPS");
-        const long x = v ? std::strtol(v, nullptr, 10) : 2;
-        return (uint32_t)(x >= 1 && x <= 16 ? x : 2);
+        const long x = v ? std::strtol(v, nullptr, 10) : 4;
+        return (uint32_t)(x >= 1 && x <= 16 ? x : 4);
     }();
     // at least n_wtiles / 64 waves: a wave holds at most 64 tile descriptors
     const uint32_t waves = std::max<uint32_t>(std::min<uint32_t>(e->n_wtiles, (uint32_t)std::max(e->n_cu, 1) * 4u * wps),
@@ -482,11 +481,7 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
         const bool wave = !block && e->n_wtiles > 0 && a.do_occ && a.nc >= 1 && a.nc <= 4 &&
                           (uint64_t)(e->C + 1) * ld * 4 < (1ull << 31);
         if (!wave) HIP_TRY(jsp::launch_tally(a, s));
-        else {
-            jsp::WaveClasses kc{};
-            for (uint32_t c = 0; c < a.nc; ++c) kc.c[c] = e->cls_h[c0 + c];
-            HIP_TRY(jsp::launch_tally_wave(a, kc, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, tally_wave_grid(e), s));
-        }
+        else HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, tally_wave_grid(e), s));
         c0 += a.nc;
     } while (c0 < e->C);
     ev_end(p, s);
@@ -907,14 +902,20 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
                    (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
     // A cold start -- the first request after an idle exit (recoveries are
-    // hours apart), an upload or a geometry change -- launches the service
-    // without waiting for its dispatcher and answers this call on the launch
-    // path meanwhile (kSvcUseLaunch); the next call finds it polling.
-    // JSP_COLD_LAUNCH=0: wait for the new service and post to it (A/B).
-    static const bool cold_launch = [] { const char* v = std::getenv("JSP_COLD_LAUNCH"); return !(v && v[0] == '0'); }();
+    // hours apart), an upload or a geometry change -- launches the service,
+    // waits for its dispatcher to poll and posts to it. Measured after 60 ms
+    // idle on MI355X (profiles/r03, tools/ab_probe.py svc): cfg2 p50 33 us,
+    // max 67 us this way, against 66 / 428 us when the launch path answers the
+    // cold call while the service comes up (JSP_COLD_LAUNCH=1, A/B) -- the
+    // polling dispatcher brings the GPU out of its idle state while the host
+    // waits, and a launch after idling pays that wake-up inside the kernel.
+    static const bool cold_launch = [] { const char* v = std::getenv("JSP_COLD_LAUNCH"); return v && v[0] == '1'; }();
+    // The new service is launched once this call's answer is back
+    // (jsp_place): launched before, its co-resident grid can hold the CUs the
+    // launch path's workgroups need until it idle-exits (a 50 ms stall seen
+    // as the cold-recovery maximum, profiles/r03).
     if (restart && cold_launch) {
         if (int rc = svc_stop(e)) return rc;
-        if (int rc = svc_start(e, J, n_runs, false)) return rc;
         return kSvcUseLaunch;
     }
     if (!restart) {
@@ -989,46 +990,13 @@ int check_runs(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len
     return JSP_OK;
 }
 
-// Branch-free invariant-divisor constants for floor(n / d) over uint32 n
-// (the form of libdivide's u32 "branchfree" divider; exactness is checked by
-// tests/test_engine_gpu.py::test_exact_division_boundaries).
-void divisor_magic(uint32_t d, uint32_t* magic, uint32_t* shift) {
-    *magic = 0;
-    *shift = jsp::kDivIdentity;
-    if (d <= 1) return;  // d == 0: resource not requested (never divided)
-    uint32_t L = 31 - (uint32_t)__builtin_clz(d);
-    if ((d & (d - 1)) == 0) {  // 2^L: t = n >> 1, then >> (L - 1)
-        *shift = L - 1;
-        return;
-    }
-    const uint64_t num = 1ull << (32 + L);
-    uint64_t m = num / d;
-    const uint64_t rem = num % d;
-    m = (m + m) & 0xFFFFFFFFull;
-    if (rem + rem >= d) m = (m + 1) & 0xFFFFFFFFull;
-    *magic = (uint32_t)((1 + m) & 0xFFFFFFFFull);
-    *shift = L;
-}
-
-// The 2-op form for dividends below 2^31: floor(n / d) = mulhi(n, m) >> s.
-// d = 2^L: m = 2^31, s = L - 1. Otherwise, with L = floor(log2 d) and
-// l = L + 1 = ceil(log2 d): m = ceil(2^(31+l) / d) < 2^32, s = L; the error
-// e = m d - 2^(31+l) < d adds less than n e / (d 2^(31+l)) < 2^-l <= 1/d to
-// n / d for n < 2^31, which never crosses an integer.
-void divisor_magic31(uint32_t d, uint32_t* magic, uint32_t* shift) {
-    *magic = 0;
-    *shift = 0;
-    if (d <= 1) return;  // identity / not requested: the kernel never takes this form
-    const uint32_t L = 31 - (uint32_t)__builtin_clz(d);
-    if ((d & (d - 1)) == 0) {
-        *magic = 1u << 31;
-        *shift = L - 1;
-        return;
-    }
-    const uint64_t num = 1ull << (32 + L);
-    *magic = (uint32_t)((num + d - 1) / d);
-    *shift = L;
-}
+// The f64 reciprocal r of d >= 2 with floor(double(n) * r) == floor(n / d)
+// for every u32 n (the device truncates fl(n * r) to u32). With r = (1/d)(1 + e):
+// fl(n * r) >= n/d needs e above the two roundings (2^-52); below q + 1 it
+// needs (n/d)(1 + e + 2^-52) < q + 1, i.e. e < 1/(n + d) - 2^-52, which holds
+// for e < 2^-34 as n + d < 2^33. r = fl(fl(1/d) (1 + 2^-45)) has e within
+// 2^-45 +- 2^-52. tests/test_engine_gpu.py checks the edges (n = kd - 1, kd).
+double divisor_rcp(uint32_t d) { return d >= 2 ? (1.0 / (double)d) * (1.0 + 0x1p-45) : 0.0; }
 
 int ready(jsp_engine* e, bool need_cls) {
     if (!e->have_topo) return set_err(JSP_ESTATE, "no topology uploaded");
@@ -1328,12 +1296,6 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     e->npad = npad;
     e->W = W;
     e->R = R;
-    e->fast_res = 0;
-    for (uint32_t r = 0; r < R; ++r) {
-        bool small = true;
-        for (uint32_t i = 0; i < N && small; ++i) small = nd->free_res[(size_t)r * N + i] < (1u << 31);
-        if (small) e->fast_res |= 1u << r;
-    }
     e->leaf_begin = nd->leaf_begin;
     e->n_leaves = NL;
     e->max_leaf_rows = max_rows;
@@ -1368,15 +1330,6 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
-    if (free_res) {  // a patched value >= 2^31 turns the 2-op division off for its resource
-        const uint32_t before = e->fast_res;
-        for (uint32_t r = 0; r < e->R; ++r)
-            for (uint32_t i = 0; i < n; ++i)
-                if (free_res[(size_t)r * n + i] >= (1u << 31)) e->fast_res &= ~(1u << r);
-        if (e->fast_res != before) {  // the resident service holds the old flags: restart it
-            if (int rc = svc_suspend(e)) return rc;
-        }
-    }
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->tmp_a, rows, n, s));
@@ -1423,8 +1376,7 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
         d.pods = x.pods;
         for (int r = 0; r < 4; ++r) {
             d.res[r] = x.req_res[r];
-            divisor_magic(x.req_res[r], &d.magic[r], &d.shift[r]);
-            divisor_magic31(x.req_res[r], &d.magic31[r], &d.shift31[r]);
+            d.rcp[r] = divisor_rcp(x.req_res[r]);
         }
         woff[c + 1] = woff[c] + (e->D[x.level] + 63) / 64;
     }
@@ -1512,11 +1464,15 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     const bool want_tally = (tally_out && e->C > 0) || occ_out;
+    bool svc_after = false;  // a cold start: the service is launched after the launch path answers
     if (!want_tally && svc_ok(e)) {
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
         const int src = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed);
-        if (src == kSvcUseLaunch) goto launch_path;
+        if (src == kSvcUseLaunch) {
+            svc_after = true;
+            goto launch_path;
+        }
         if (src != JSP_OK) {
             // the service could not answer (not co-resident, left, or a request
             // failed on the device): stop it, keep it off until the next upload,
@@ -1597,6 +1553,13 @@ launch_path:
     e->acc.host_launch_us += us(t2 - t1).count();
     e->acc.host_wait_us += us(t3 - t2).count();
     e->acc.host_post_us += us(t4 - t3).count();
+    if (svc_after && svc_start(e, J, n_runs, false) != JSP_OK) {
+        // cannot start here (not co-resident on this GPU, ...): the launch path
+        // answers until the next upload, as when a request fails
+        (void)svc_stop(e);
+        e->svc.broken = true;
+        e->acc.svc_fallbacks += 1;
+    }
     return JSP_OK;
 }
 

@@ -22,8 +22,8 @@ constexpr uint32_t kMaxTakenWords = 16384;         // 128 KiB of LDS: 1M domain 
 
 // Device copy of a jsp_job_class, pre-digested for the tally's inner loop:
 // one mask test per label word, one AND per taint word, and an exact
-// division-free floor(free / req) per resource (multiply-high by an
-// invariant-divisor magic number, branch-free form).
+// floor(free / req) per resource as one f64 multiply by a pre-rounded
+// reciprocal (no integer division).
 struct alignas(16) DevClass {
     uint64_t req[4];      // bits that must be set
     uint64_t mask[4];     // req | forbid: a row passes when (labels & mask) == req
@@ -32,12 +32,9 @@ struct alignas(16) DevClass {
     uint32_t pods;
     uint32_t pad;
     uint32_t res[4];      // per-pod request, 0 = none
-    uint32_t magic[4];    // floor(n / res) = (((n - mulhi(n, magic)) >> 1) + mulhi(n, magic)) >> shift
-    uint32_t shift[4];    // kDivIdentity marks res == 1
-    uint32_t magic31[4];  // floor(n / res) = mulhi(n, magic31) >> shift31, exact for n < 2^31
-    uint32_t shift31[4];  //   (TallyArgs::fast_res: every free value of the resource is below 2^31)
+    double rcp[4];        // res >= 2: floor(n / res) = (uint32)(double(n) * rcp), exact for every u32 n
+                          //   (rcp = 1/res (1 + 2^-45)); res == 1: n itself
 };
-constexpr uint32_t kDivIdentity = 0xFFFFFFFFu;
 
 // A long run's step gives away the taken bits of a window word: one record per
 // such word (assign_kernel), expanded to assign[] by expand_kernel. Each taken
@@ -75,7 +72,6 @@ struct TallyArgs {
     uint32_t ld, leaf_base;
     int W, R;
     int sc1_out;                // write cap/occ write-through (sc1): the fused kernel's hand-off to its tail
-    uint32_t fast_res;          // bit r: every free[r] of the snapshot < 2^31 (the 2-op division applies)
 };
 
 // Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks
@@ -232,14 +228,7 @@ hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 // (snapshots with a larger leaf use the workgroup tally), 1-4 classes and the
 // occupancy count in one pass; `grid` workgroups of 4 waves take them in turn. Every column's bytes must stay below 2^31
 // (buffer offsets; the host checks).
-// The wave-tile tally's classes, passed by value: kernel arguments are read by
-// scalar loads, so a class's fields reach SGPRs without LDS staging, a
-// workgroup barrier or readfirstlane (c[0..nc) = classes c0 .. c0 + nc - 1).
-struct WaveClasses {
-    DevClass c[4];
-};
-hipError_t launch_tally_wave(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
-                             uint32_t n_leaves, uint32_t grid,
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
                              hipStream_t s);
 size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);

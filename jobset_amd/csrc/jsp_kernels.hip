@@ -48,14 +48,21 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
     do {                                                                                  \
         if (threadIdx.x == 0 && (row) < 4096) jsp_dbg[(row) * 8 + (i)] = (unsigned long long)(v); \
     } while (0)
-// per-wave real-time stamp (lane 0 of each wave)
+// per-wave real-time stamp (lane 0 of each wave), and a shader-clock one
 #define JSP_WSTAMP(w, i)                                                                  \
     do {                                                                                  \
         if ((threadIdx.x & 63) == 0 && (w) < 4096) jsp_dbg[(w) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
+#define JSP_WCLK(w, i)                                                                    \
+    do {                                                                                  \
+        if ((threadIdx.x & 63) == 0 && (w) < 4096) jsp_dbg[(w) * 8 + (i)] = __builtin_amdgcn_s_memtime(); \
+    } while (0)
 #else
 #define JSP_WSTAMP(w, i) \
     do {                 \
+    } while (0)
+#define JSP_WCLK(w, i) \
+    do {               \
     } while (0)
 #define JSP_DBGV(row, i, v) \
     do {                    \
@@ -136,14 +143,6 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x142, 0xa, 0xf, false));
     x = min(x, (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x143, 0xc, 0xf, false));
     return (uint32_t)__builtin_amdgcn_readlane((int)x, 63);
-}
-
-// floor(n / d) for a divisor known per class, exact for every uint32 n
-// (branch-free invariant-divisor division: one multiply-high, shifts, adds).
-__device__ __forceinline__ uint32_t div_invariant(uint32_t n, uint32_t magic, uint32_t shift) {
-    const uint32_t q = __umulhi(n, magic);
-    const uint32_t t = (((n - q) >> 1) + q) >> (shift & 31u);
-    return shift == kDivIdentity ? n : t;
 }
 
 // Completion word of the host placement path: every wave's stores of this
@@ -317,8 +316,16 @@ __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool
 template <int W, int R>
 struct ClassRegs {
     uint64_t req[W], mask[W];
-    uint32_t tol_inv, pods, res[R], magic[R], shift[R], magic31[R], shift31[R];
+    uint32_t tol_inv, pods, res[R];
+    double rcp[R];
 };
+
+// floor(n / res) for one row of a resource, res >= 2: the f64 reciprocal,
+// truncated (exact for every u32 n: DESIGN.md §4.1). 3 VALU ops at the f64
+// rate; the invariant-divisor multiply-high it replaced issues v_mul_hi_u32 at
+// a quarter of the full rate on gfx950 (8.6 cycles per wave-instruction,
+// tools/valu_rate.hip) and took SGPRs for its constants.
+__device__ __forceinline__ uint32_t row_div(double rcp, uint32_t n) { return (uint32_t)((double)n * rcp); }
 
 __device__ __forceinline__ uint32_t to_sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t to_sgpr64(uint64_t x) {
@@ -338,10 +345,8 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         k.res[r] = to_sgpr(d.res[r]);
-        k.magic[r] = to_sgpr(d.magic[r]);
-        k.shift[r] = to_sgpr(d.shift[r]);
-        k.magic31[r] = to_sgpr(d.magic31[r]);
-        k.shift31[r] = to_sgpr(d.shift31[r]);
+        const uint32_t* rw = reinterpret_cast<const uint32_t*>(&d.rcp[r]);  // the two halves, moved to SGPRs
+        k.rcp[r] = __hiloint2double((int)to_sgpr(rw[1]), (int)to_sgpr(rw[0]));
     }
     return k;
 }
@@ -423,18 +428,12 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
 #pragma unroll
                 for (int r = 0; r < R; ++r) {
                     if (k.res[r] == 0) continue;  // scalar branches (SGPR operands), once per 4 rows
-                    if (k.shift[r] == kDivIdentity) {
+                    if (k.res[r] == 1) {
 #pragma unroll
                         for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], fr[r][i]);
-                    } else if ((a.fast_res >> r) & 1u) {  // every free value < 2^31: two ops
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(fr[r][i], k.magic31[r]) >> k.shift31[r]);
                     } else {
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const uint32_t n = fr[r][i], h = __umulhi(n, k.magic[r]);
-                            cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
-                        }
+                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], row_div(k.rcp[r], fr[r][i]));
                     }
                 }
 #pragma unroll
@@ -569,9 +568,12 @@ __device__ __forceinline__ void wave_issue(const TallyArgs& a, const WaveRsrc& r
 // Evaluate one tile from `v` and store its leaves' sums: NV values, the
 // first NV - 1 classes and the occupancy count (compile-time, so every store
 // of the unrolled loop is counted by the compiler's waits).
-// The fields of one class straight from the kernel arguments (scalar loads).
+// Class records read through the constant address space: uniform addresses
+// become scalar loads (s_load, scalar cache), so a class reaches SGPRs with
+// no LDS staging, workgroup barrier or readfirstlane (the wave tally).
+#define JSP_CONST __attribute__((address_space(4)))
 template <int W, int R>
-__device__ __forceinline__ ClassRegs<W, R> class_args(const DevClass& d) {
+__device__ __forceinline__ ClassRegs<W, R> class_regs_k(const JSP_CONST DevClass& d) {
     ClassRegs<W, R> k;
 #pragma unroll
     for (int w = 0; w < W; ++w) {
@@ -583,50 +585,46 @@ __device__ __forceinline__ ClassRegs<W, R> class_args(const DevClass& d) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         k.res[r] = d.res[r];
-        k.magic[r] = d.magic[r];
-        k.shift[r] = d.shift[r];
-        k.magic31[r] = d.magic31[r];
-        k.shift31[r] = d.shift31[r];
+        k.rcp[r] = d.rcp[r];
     }
     return k;
 }
 
 // Evaluate one tile from `v` and keep its leaves' sums: NV values, the first
 // NV - 1 classes and the occupancy count (compile-time, so every store of the
-// unrolled loop is counted by the compiler's waits). Rows outside the tile's
+// unrolled loop is counted by the compiler's waits). In three batched phases:
+// every value's 4-row partial sums, then the NV wave scans (independent DPP
+// chains the scheduler interleaves), then all row prefixes into the wave's LDS
+// slice behind ONE wave barrier and every leaf's difference read back (one
+// LDS round trip per tile instead of one per value). Rows outside the tile's
 // leaves are evaluated like any other and not masked: a leaf's sum is
 // prefix(its last row) - prefix(the row before its first), and a row before
 // the tile's first leaf is in both prefixes, a row after its last leaf in
 // neither (the u32 differences are exact: a tile's prefix stays below
 // 256 x 2^22 -- pods <= 2^22, checked at class upload).
 template <int W, int R, int NV>
-__device__ __forceinline__ void wave_eval(const TallyArgs& a, const WaveClasses& kc, JSP_LDS uint32_t* s_pre, uint4 bt,
+__device__ __forceinline__ void wave_eval(const TallyArgs& a, const JSP_CONST DevClass* k_cls, JSP_LDS uint32_t* s_pre, uint4 bt,
                                           int lane, const WaveSet<W, R>& v, uint32_t (&sums)[NV]) {
     constexpr int nc = NV - 1;
     const uint32_t base = bt.z & ~3u;
     const uint32_t nl = bt.y - bt.x;
     const bool has_leaf = (uint32_t)lane < nl;
+    uint32_t part[NV][4];  // inclusive sums of the lane's 4 rows, per value
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
         uint32_t val[4];
         if (c < nc) {
-            const ClassRegs<W, R> k = class_args<W, R>(kc.c[c]);
+            const ClassRegs<W, R> k = class_regs_k<W, R>(k_cls[c]);
             uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
 #pragma unroll
             for (int r = 0; r < R; ++r) {
                 if (k.res[r] == 0) continue;
-                if (k.shift[r] == kDivIdentity) {
+                if (k.res[r] == 1) {
 #pragma unroll
                     for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], v.x.fr[r][i]);
-                } else if ((a.fast_res >> r) & 1u) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], __umulhi(v.x.fr[r][i], k.magic31[r]) >> k.shift31[r]);
                 } else {
 #pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint32_t n = v.x.fr[r][i], h = __umulhi(n, k.magic[r]);
-                        cap[i] = min(cap[i], (((n - h) >> 1) + h) >> k.shift[r]);
-                    }
+                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], row_div(k.rcp[r], v.x.fr[r][i]));
                 }
             }
 #pragma unroll
@@ -640,25 +638,37 @@ __device__ __forceinline__ void wave_eval(const TallyArgs& a, const WaveClasses&
 #pragma unroll
             for (int i = 0; i < 4; ++i) val[i] = v.x.ex[i] != -1 ? 1u : 0u;
         }
-        const uint32_t p0 = val[0], p1 = p0 + val[1], p2 = p1 + val[2], p3 = p2 + val[3];
-        const uint32_t incl = wave_incl_scan(p3, lane);
-        const uint32_t wex = incl - p3;
-        reinterpret_cast<JSP_LDS u32x4*>(s_pre + c * kWaveTileRows)[lane] = u32x4{wex + p0, wex + p1, wex + p2, incl};
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        uint32_t sum = 0;
-        const uint32_t lo = v.ls_lo, hi = v.ls_hi;
-        if (has_leaf && lo < hi) {
-            const uint32_t hp = s_pre[c * kWaveTileRows + (hi - 1 - base)];
-            const uint32_t bp = lo > base ? s_pre[c * kWaveTileRows + (lo - 1 - base)] : 0u;
-            sum = hp - bp;
-        }
-        sums[c] = sum;
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        part[c][0] = val[0];
+        part[c][1] = part[c][0] + val[1];
+        part[c][2] = part[c][1] + val[2];
+        part[c][3] = part[c][2] + val[3];
     }
+    uint32_t incl[NV];
+#pragma unroll
+    for (int c = 0; c < NV; ++c) incl[c] = wave_incl_scan(part[c][3], lane);
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        const uint32_t wex = incl[c] - part[c][3];
+        reinterpret_cast<JSP_LDS u32x4*>(s_pre + c * kWaveTileRows)[lane] =
+            u32x4{wex + part[c][0], wex + part[c][1], wex + part[c][2], incl[c]};
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t lo = v.ls_lo, hi = v.ls_hi;
+    const bool live = has_leaf && lo < hi;
+    const bool before = lo > base;
+    // a lane without a leaf reads row 0 of each slice (and discards it)
+    const uint32_t ih = live ? hi - 1 - base : 0u, ib = live && before ? lo - 1 - base : 0u;
+#pragma unroll
+    for (int c = 0; c < NV; ++c) {
+        const uint32_t hp = s_pre[c * kWaveTileRows + ih];
+        const uint32_t bp = s_pre[c * kWaveTileRows + ib];
+        sums[c] = live ? hp - (before ? bp : 0u) : 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Store a tile's leaf sums: value c's column is cap[c0 + c][leaf] (occ[leaf]
@@ -679,8 +689,7 @@ __device__ __forceinline__ void wave_store(const TallyArgs& a, __amdgpu_buffer_r
 }
 
 template <int W, int R, int NV>
-__global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, WaveClasses kc,
-                                                                   const uint4* __restrict__ tiles,
+__global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, const uint4* __restrict__ tiles,
                                                                    uint32_t n_tiles, uint32_t n_leaves) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     constexpr int nc = NV - 1;  // this launch: NV - 1 classes and the occupancy count
@@ -692,14 +701,15 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     const uint32_t t0 = blockIdx.x * kTallyWaves + wid;
     // the wave's tiles are t0, t0 + waves, ...: lane k holds the k-th one's
     // descriptor (<= 64, checked by the host), loaded once, so no later tile
-    // waits on a descriptor load. No workgroup barrier: the classes come from
-    // the kernel arguments and each wave has its own LDS slice.
+    // waits on a descriptor load. No workgroup barrier: the classes are read
+    // by scalar loads and each wave has its own LDS slice.
     JSP_WSTAMP(t0, 0);
     if (t0 >= n_tiles) return;
     uint4 dl = make_uint4(0, 0, 0, 0);
     if (t0 + (uint32_t)lane * waves < n_tiles) dl = tiles[t0 + (uint32_t)lane * waves];
     JSP_WSTAMP(t0, 1);
     const uint32_t nt = (n_tiles - t0 + waves - 1) / waves;  // this wave's tiles
+    const JSP_CONST DevClass* k_cls = (const JSP_CONST DevClass*)(a.cls + a.c0);
     JSP_LDS uint32_t* s_pre = lds_ptr(lds + wid * nv * kWaveTileRows);
     auto desc = [&](uint32_t k) {
         const int l = (int)(k < nt ? k : nt - 1);
@@ -724,16 +734,27 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     uint32_t sums[NV];
     bool first = true;
     while (true) {
-        wave_eval<W, R, NV>(a, kc, s_pre, btA, lane, A, sums);
+        wave_eval<W, R, NV>(a, k_cls, s_pre, btA, lane, A, sums);
         if (first) JSP_WSTAMP(t0, 2);
-        first = false;
         const uint4 done_a = btA;
         kA = kB + 1;
         btA = desc(kA);
         wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, kA < nt, lane, A);
         wave_store<NV>(a, cap_r, occ_r, done_a, lane, sums);
         if (kB >= nt) break;
-        wave_eval<W, R, NV>(a, kc, s_pre, btB, lane, B, sums);
+#ifdef JSP_STAMPS
+        if (first) {  // diagnostic only: the next tile's rows in registers, then time its evaluation alone
+            __builtin_amdgcn_s_waitcnt(0);
+            JSP_WSTAMP(t0, 3);
+            JSP_WCLK(t0, 6);
+        }
+#endif
+        wave_eval<W, R, NV>(a, k_cls, s_pre, btB, lane, B, sums);
+        if (first) {
+            JSP_WSTAMP(t0, 4);
+            JSP_WCLK(t0, 7);
+        }
+        first = false;
         const uint4 done_b = btB;
         kB = kA + 1;
         btB = desc(kB);
@@ -741,7 +762,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
         wave_store<NV>(a, cap_r, occ_r, done_b, lane, sums);
         if (kA >= nt) break;
     }
-    JSP_WSTAMP(t0, 3);
+    JSP_WSTAMP(t0, 5);
 }
 
 // ----------------------------------------------------------------- feasibility
@@ -2859,16 +2880,16 @@ static hipError_t launch_tally_wr(const TallyArgs& a, hipStream_t s) {
 }
 
 template <int W, int R>
-static hipError_t launch_tally_wave_wr(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
-                                       uint32_t n_leaves, uint32_t grid, hipStream_t s) {
+static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves,
+                                       uint32_t grid, hipStream_t s) {
     const size_t lds = tally_wave_lds_bytes(a.nc, a.nc + 1);
     // a wave holds at most 64 tile descriptors, one per lane
     if ((uint64_t)grid * kTallyWaves * 64u < n_tiles) return hipErrorInvalidValue;
     switch (a.nc) {
-        case 1: jsp_launch((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
-        case 2: jsp_launch((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
-        case 3: jsp_launch((tally_wave_kernel<W, R, 4>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
-        case 4: jsp_launch((tally_wave_kernel<W, R, 5>), dim3(grid), dim3(kTallyThreads), lds, s, a, kc, tiles, n_tiles, n_leaves); break;
+        case 1: jsp_launch((tally_wave_kernel<W, R, 2>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 2: jsp_launch((tally_wave_kernel<W, R, 3>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 3: jsp_launch((tally_wave_kernel<W, R, 4>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+        case 4: jsp_launch((tally_wave_kernel<W, R, 5>), dim3(grid), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2916,9 +2937,9 @@ size_t tally_wave_lds_bytes(uint32_t /*nc*/, uint32_t nv) {
     return sizeof(uint32_t) * (size_t)kTallyWaves * nv * kWaveTileRows;
 }
 
-hipError_t launch_tally_wave(const TallyArgs& a, const WaveClasses& kc, const uint4* tiles, uint32_t n_tiles,
-                             uint32_t n_leaves, uint32_t grid, hipStream_t s) {
-    JSP_DISPATCH_WR(launch_tally_wave_wr, a, kc, tiles, n_tiles, n_leaves, grid, s)
+hipError_t launch_tally_wave(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves, uint32_t grid,
+                             hipStream_t s) {
+    JSP_DISPATCH_WR(launch_tally_wave_wr, a, tiles, n_tiles, n_leaves, grid, s)
 }
 
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s) {

@@ -252,11 +252,11 @@ def test_exact_division_boundaries(engine):
     np.testing.assert_array_equal(cap, exp)
 
 
-def test_exact_division_fast_path(engine):
-    """Every free value below 2^31: the tally takes the 2-op division
-    (mulhi + shift); it must equal floor(free/req) at the 2^31 edge and for
-    divisors up to 2^32-1 -- and stay exact after a patch brings a value
-    >= 2^31 in (the engine falls back to the 3-step form)."""
+def test_exact_division_boundaries(engine):
+    """floor(free/req) at the 2^31 edge and for divisors up to 2^32-1, and
+    after a patch brings values >= 2^31 in (the f64 reciprocal path covers
+    every u32 dividend; the multiply-high form it replaced needed a 2^31 bound
+    for its 2-op variant)."""
     rng = np.random.default_rng(31)
     vals = np.concatenate([np.array([0, 1, 2, 3, (1 << 31) - 1, (1 << 31) - 2, 1 << 30, (1 << 24) + 1,
                                      123456789, 999_999_937, 96_000, 1_024_000], dtype=np.uint64),
@@ -281,6 +281,44 @@ def test_exact_division_fast_path(engine):
     got = engine.place(p.job_class, want_tally=True)
     exp = np.minimum(vals[None, :] // np.array(reqs, dtype=np.uint64)[:, None], 1 << 22).astype(np.uint32)
     np.testing.assert_array_equal(got.cap, exp)
+
+
+def test_f64_division_exact(engine):
+    """floor(free / req) through fl(double(free) * rcp(req)) truncated to u32
+    equals the integer quotient at every edge: free = k*req - 1, k*req,
+    k*req + 1 up to 2^32 - 1, for divisors from 2 to 2^32 - 1 (DESIGN.md
+    §4.1) -- on the launch shapes (fused and three-launch tallies) and the
+    device tally."""
+    import torch
+    rng = np.random.default_rng(64)
+    reqs = [2, 3, 7, 10, 1000, 1024, 4097, 24_000, 200_000, (1 << 20) + 3, 65521, 1 << 30, (1 << 31) - 1,
+            (1 << 31) + 1, 4_000_000_001, (1 << 32) - 1]
+    M = (1 << 32) - 1
+    vals = [0, 1, 2, M, M - 1, 1 << 31, (1 << 31) - 1]
+    for d in reqs:
+        for k in [1, 2, 3, 1000, 12345, M // d - 1, M // d]:
+            for n in (k * d - 1, k * d, k * d + 1):
+                if 0 <= n <= M:
+                    vals.append(n)
+    vals = np.array(vals + list(rng.integers(0, 1 << 32, size=200, dtype=np.uint64)), dtype=np.uint64)
+    N = vals.shape[0]
+    topo = Topology(level_keys=["k"], n_domains=[N], first_leaf=[np.arange(N + 1, dtype=np.uint32)])
+    nodes = Nodes(leaf_start=np.arange(N + 1, dtype=np.uint32), labels=np.zeros((1, N), dtype=np.uint64),
+                  taints=np.zeros(N, dtype=np.uint32), free=vals.astype(np.uint32)[None, :],
+                  excl=np.full(N, -1, dtype=np.int32))
+    exp_all = np.minimum(vals[None, :] // np.array(reqs, dtype=np.uint64)[:, None], 1 << 22).astype(np.uint32)
+    for c0 in range(0, len(reqs), 4):  # <= 4 classes: the wave-tile device tally takes them in one pass
+        rq = reqs[c0:c0 + 4]
+        classes = [JobClass(pods=1 << 22, req_res=(r,)) for r in rq]
+        p = Problem(topology=topo, nodes=nodes, classes=classes, job_class=np.zeros(0, dtype=np.uint32))
+        got, a, cap, occ = run_both(engine, p)
+        np.testing.assert_array_equal(got.cap, exp_all[c0:c0 + 4])
+        np.testing.assert_array_equal(cap, exp_all[c0:c0 + 4])
+        C, L = len(rq), N
+        dcap = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
+        engine.tally_device(dcap.data_ptr(), dcap[-1].data_ptr(), L, 0)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(dcap[:C].cpu().numpy().astype(np.uint32), exp_all[c0:c0 + 4])
 
 
 def test_patch_then_place(engine):

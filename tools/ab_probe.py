@@ -19,13 +19,15 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave1": {"JSP_TALLY_WPS": "1"}, "wave2": {"JSP_TALLY_WPS": "2"},
-         "wave3": {"JSP_TALLY_WPS": "3"}, "wave4": {"JSP_TALLY_WPS": "4"},
-         "wave6": {"JSP_TALLY_WPS": "6"}, "wave8": {"JSP_TALLY_WPS": "8"}}
+AB = os.path.join(ROOT, "tools", "ablib")  # A/B builds (make tools/ablib/<name>/libjsplace.so)
+TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave2": {"JSP_TALLY_WPS": "2"}, "wave4": {"JSP_TALLY_WPS": "4"},
+         "wave8": {"JSP_TALLY_WPS": "8"}}
+# a variant can also load another build of the library: {"JSP_LIB_PATH": os.path.join(AB, name, "libjsplace.so")}
+# (make tools/ablib/<name>/libjsplace.so with AB_FLAGS_<name> in the Makefile)
 SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
        "svc_rows508": {"JSP_BLOCK_ROWS": "508"}, "svc_rows252": {"JSP_BLOCK_ROWS": "252"},
        "svc_split_rows252": {"JSP_SPLIT_COMPACT": "1", "JSP_BLOCK_ROWS": "252"},
-       "svc_cold_sync": {"JSP_COLD_LAUNCH": "0"}}
+       "svc_cold_launch": {"JSP_COLD_LAUNCH": "1"}}
 MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
