@@ -13,9 +13,13 @@ OBJ = build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o 
 
 all: $(LIB) oracle
 
+# -ffinite-math-only: the kernels' only floating point is the tally's f64
+# capacity minimum (finite, non-negative): v_min_f64 without the NaN-quieting
+# v_max_f64 the IEEE minNum semantics would put before each operand
+KFLAGS = -ffinite-math-only
 build/jsp_kernels.o: jobset_amd/csrc/jsp_kernels.hip $(HDR)
 	@mkdir -p build
-	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -c -o $@ $<
 
 build/jsp_engine.o: jobset_amd/csrc/jsp_engine.cc jobset_amd/csrc/jsp_walk.h $(HDR)
 	@mkdir -p build
@@ -48,7 +52,7 @@ tools/bin/dispatch_probe: tools/dispatch_probe.hip
 	$(HIPCC) --offload-arch=gfx950 -O3 -o $@ $<
 tools/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip jobset_amd/csrc/jsp_engine.cc $(HOST_SRC) $(HDR) $(HOST_HDR)
 	@mkdir -p build/diag tools/diag
-	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -c -o build/diag/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_STAMPS -c -o build/diag/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -DJSP_STAMPS -x hip -c -o build/diag/e.o jobset_amd/csrc/jsp_engine.cc
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag/k.o build/diag/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ)
 
@@ -91,5 +95,5 @@ tools/bin/valu_rate: tools/valu_rate.hip
 # through JSP_LIB_PATH): tools/ablib/<name>/libjsplace.so
 tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
 	@mkdir -p build/ab_$* tools/ablib/$*
-	$(HIPCC) $(HIPFLAGS) $(AB_FLAGS_$*) -c -o build/ab_$*/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(AB_FLAGS_$*) -c -o build/ab_$*/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_$*/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

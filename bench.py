@@ -108,10 +108,11 @@ def evidence_dirs():
     return out
 
 
-def pmc_traffic(kernel: str, cfg: int):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
-    passes (latest round under profiles/): FETCH_SIZE (KiB, x2 on gfx950) +
-    WRITE_SIZE (KiB), averaged over that kernel's dispatches."""
+def pmc_traffic(kernel, cfg: int):
+    """HBM bytes per launch of `kernel` (a name prefix or a tuple of them) from
+    the committed rocprofv3 PMC passes (latest round under profiles/):
+    FETCH_SIZE (KiB, x2 on gfx950) + WRITE_SIZE (KiB), averaged over that
+    kernel's dispatches."""
     def avg(path):
         vals = []
         with open(path, newline="") as f:
@@ -601,7 +602,7 @@ def main() -> None:
                 "cold_note": "cold: a 512 MiB read-only scrub before each launch (as tools/stream_ceiling.hip); "
                              "cold_dirty: the scrub also writes it, so the launch's misses pay its write-backs",
                 "copy_ceiling_same_bytes": copy_ceiling,
-                "tally_traffic": pmc_traffic("tally_kernel", 4) if world == 1 else None,
+                "tally_traffic": pmc_traffic(("tally_wave_kernel", "tally_kernel"), 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
                 "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
                 "allreduce_us": sp.allreduce_us(), "shards": world, "cpu_baseline": cpu4}

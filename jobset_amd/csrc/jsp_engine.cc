@@ -996,7 +996,7 @@ int check_runs(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len
 // needs (n/d)(1 + e + 2^-52) < q + 1, i.e. e < 1/(n + d) - 2^-52, which holds
 // for e < 2^-34 as n + d < 2^33. r = fl(fl(1/d) (1 + 2^-45)) has e within
 // 2^-45 +- 2^-52. tests/test_engine_gpu.py checks the edges (n = kd - 1, kd).
-double divisor_rcp(uint32_t d) { return d >= 2 ? (1.0 / (double)d) * (1.0 + 0x1p-45) : 0.0; }
+double divisor_rcp(uint32_t d) { return d >= 2 ? (1.0 / (double)d) * (1.0 + 0x1p-45) : d == 1 ? 1.0 : 0.0; }
 
 int ready(jsp_engine* e, bool need_cls) {
     if (!e->have_topo) return set_err(JSP_ESTATE, "no topology uploaded");

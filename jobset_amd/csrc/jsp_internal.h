@@ -33,7 +33,7 @@ struct alignas(16) DevClass {
     uint32_t pad;
     uint32_t res[4];      // per-pod request, 0 = none
     double rcp[4];        // res >= 2: floor(n / res) = (uint32)(double(n) * rcp), exact for every u32 n
-                          //   (rcp = 1/res (1 + 2^-45)); res == 1: n itself
+                          //   (rcp = 1/res (1 + 2^-45)); res == 1: 1.0
 };
 
 // A long run's step gives away the taken bits of a window word: one record per

@@ -325,7 +325,25 @@ struct ClassRegs {
 // rate; the invariant-divisor multiply-high it replaced issues v_mul_hi_u32 at
 // a quarter of the full rate on gfx950 (8.6 cycles per wave-instruction,
 // tools/valu_rate.hip) and took SGPRs for its constants.
-__device__ __forceinline__ uint32_t row_div(double rcp, uint32_t n) { return (uint32_t)((double)n * rcp); }
+// A class's capacity on 4 rows: min(pods, min over its requested resources of
+// floor(free / req)). floor is monotone, so the minimum is taken over the f64
+// products fl(free * rcp) -- each floors to the exact quotient (rcp = 1.0 for
+// req == 1) -- and ONE truncation to u32 ends it: per resource and row one
+// v_mul_f64 and one v_min_f64, per row one v_cvt_u32_f64 (the per-resource
+// truncation and integer min it replaces cost two more instructions each).
+template <int W, int R>
+__device__ __forceinline__ void row_caps(const ClassRegs<W, R>& k, const uint32_t (&fr)[R][4], uint32_t (&cap)[4]) {
+    const double pods = (double)k.pods;
+    double m[4] = {pods, pods, pods, pods};
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        if (k.res[r] == 0) continue;  // scalar branch (SGPR operand)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) m[i] = __builtin_fmin(m[i], (double)fr[r][i] * k.rcp[r]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) cap[i] = (uint32_t)m[i];
+}
 
 __device__ __forceinline__ uint32_t to_sgpr(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t to_sgpr64(uint64_t x) {
@@ -424,18 +442,8 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
             uint32_t v[4];
             if (c < nc) {
                 const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
-                uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    if (k.res[r] == 0) continue;  // scalar branches (SGPR operands), once per 4 rows
-                    if (k.res[r] == 1) {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], fr[r][i]);
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], row_div(k.rcp[r], fr[r][i]));
-                    }
-                }
+                uint32_t cap[4];
+                row_caps<W, R>(k, fr, cap);
 #pragma unroll
                 for (int i = 0; i < 4; ++i) {
                     bool ok = valid[i] & ((tn[i] & k.tol_inv) == 0);
@@ -610,23 +618,18 @@ __device__ __forceinline__ void wave_eval(const TallyArgs& a, const JSP_CONST De
     const uint32_t nl = bt.y - bt.x;
     const bool has_leaf = (uint32_t)lane < nl;
     uint32_t part[NV][4];  // inclusive sums of the lane's 4 rows, per value
+    // re-read the class records per tile (scalar-cache hits): hoisted out of
+    // the tile loop, 4 classes' constants overflow the SGPRs and every use
+    // becomes a v_readlane of a spill lane
+    const JSP_CONST DevClass* kc = k_cls;
+    asm volatile("" : "+s"(kc));
 #pragma unroll
     for (int c = 0; c < NV; ++c) {
         uint32_t val[4];
         if (c < nc) {
-            const ClassRegs<W, R> k = class_regs_k<W, R>(k_cls[c]);
-            uint32_t cap[4] = {k.pods, k.pods, k.pods, k.pods};
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                if (k.res[r] == 0) continue;
-                if (k.res[r] == 1) {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], v.x.fr[r][i]);
-                } else {
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) cap[i] = min(cap[i], row_div(k.rcp[r], v.x.fr[r][i]));
-                }
-            }
+            const ClassRegs<W, R> k = class_regs_k<W, R>(kc[c]);
+            uint32_t cap[4];
+            row_caps<W, R>(k, v.x.fr, cap);
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 bool ok = (v.x.tn[i] & k.tol_inv) == 0;
