@@ -5,6 +5,7 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py (default flags) -> bench.json
 #   driver    python bench.py --gpus 1 --steps 20 --warmup 5 (the driver's flags) -> bench_driver.json
+#   gpus2     python bench.py --gpus 2 on this 1-GPU box must exit non-zero (no silent 1-GPU line)
 #   ceiling   tools/bin/stream_ceiling (read / copy ceilings at the kernels' byte counts)
 #   bin:NAME  tools/bin/NAME (a compiled probe) -> NAME.json
 #   probes    tools/svc_probe.py + tools/host_api_probe.py
@@ -32,6 +33,9 @@ for step in "$@"; do
     smoke)   run 300 "$OUT/smoke.log" python -c "import __graft_entry__ as g; g.smoke()"; cat "$OUT/smoke.log" ;;
     bench)   run 500 "$OUT/bench.json" python bench.py; tail -c 600 "$OUT/bench.json" ;;
     driver)  run 500 "$OUT/bench_driver.json" python bench.py --gpus 1 --steps 20 --warmup 5; tail -c 400 "$OUT/bench_driver.json" ;;
+    gpus2)   timeout -k 10 120 python bench.py --gpus 2 --steps 2 --warmup 1 > "$OUT/gpus2.log" 2>&1
+             rc=$?; echo "bench.py --gpus 2 exit code $rc" >> "$OUT/gpus2.log"; tail -2 "$OUT/gpus2.log"
+             if [ $rc -eq 0 ] || [ $rc -ge 124 ]; then echo "FAILED: --gpus 2 should fail loudly"; exit 1; fi ;;
     ceiling) run 120 "$OUT/stream_ceiling.json" tools/bin/stream_ceiling; cat "$OUT/stream_ceiling.json" ;;
     bin:*)   b="${step#bin:}"; run 120 "$OUT/$b.json" "tools/bin/$b"; cat "$OUT/$b.json" ;;
     probes)  run 200 "$OUT/svc_probe.txt" python3 tools/svc_probe.py 2000
