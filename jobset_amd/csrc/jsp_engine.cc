@@ -709,10 +709,13 @@ int svc_suspend(jsp_engine* e) {
 
 int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready);
 int svc_wait_ready(jsp_engine* e);
+// The upload returns once the new service polls, so the recovery's "post-delete
+// snapshot uploaded -> jsp_place" finds it ready instead of waiting for its
+// launch inside the placement (a failure here resurfaces at the next jsp_place).
 void svc_resume(jsp_engine* e) {
     if (e->svc.resume && svc_ok(e)) {
         e->svc.resume = false;
-        (void)svc_start(e, 0, 0, false);  // a failure here resurfaces at the next jsp_place
+        (void)svc_start(e, 0, 0, true);
     }
 }
 
