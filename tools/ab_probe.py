@@ -28,6 +28,9 @@ SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
        "svc_rows508": {"JSP_BLOCK_ROWS": "508"}, "svc_rows252": {"JSP_BLOCK_ROWS": "252"},
        "svc_split_rows252": {"JSP_SPLIT_COMPACT": "1", "JSP_BLOCK_ROWS": "252"},
        "svc_cold_launch": {"JSP_COLD_LAUNCH": "1"}}
+SVC2 = {"svc_default_1": {}, "svc_split_compact_1": {"JSP_SPLIT_COMPACT": "1"},
+        "svc_default_2": {}, "svc_split_compact_2": {"JSP_SPLIT_COMPACT": "1"},
+        "svc_default_3": {}, "svc_split_compact_3": {"JSP_SPLIT_COMPACT": "1"}}
 MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
@@ -146,12 +149,12 @@ def main():
     mode = sys.argv[1]
     if mode == "one":
         key = sys.argv[2]
-        for d in (TALLY, SVC, MARK):  # the variant's environment (also when run directly, e.g. under rocprofv3)
+        for d in (TALLY, SVC, SVC2, MARK):  # the variant's environment (also when run directly, e.g. under rocprofv3)
             os.environ.update(d.get(key, {}))
-        res = child_tally() if key in TALLY else child_svc() if key in SVC else child_mark()
+        res = child_tally() if key in TALLY else child_svc() if key in SVC or key in SVC2 else child_mark()
         print(json.dumps({key: res}), flush=True)
         return
-    variants = TALLY if mode == "tally" else SVC if mode == "svc" else MARK
+    variants = TALLY if mode == "tally" else SVC if mode == "svc" else SVC2 if mode == "svc2" else MARK
     for key, env in variants.items():
         e = dict(os.environ)
         e.update(env)
