@@ -121,6 +121,7 @@ struct jsp_engine {
     std::vector<uint32_t> h_fl[JSP_MAX_LEVELS], h_cs[JSP_MAX_LEVELS];
     std::vector<int32_t> h_par[JSP_MAX_LEVELS];
     std::vector<uint32_t> blk_l0, blk_l1;  // leaf range of each tally row block
+    uint32_t max_blk_span = 0;             // rows a tally block's first chunk spans, max over blocks
     jsp::HostWalk walk;
 
     // snapshot
@@ -187,6 +188,7 @@ struct jsp_engine {
         uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
         int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
+        bool rows_dirty = true;  // a patch since the last request: its tiles reload their rows from memory
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
         std::chrono::steady_clock::time_point t_launch{};
@@ -793,7 +795,12 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     jsp::TallyArgs ta{};
     jsp::SplitArgs sp{};
     if (shape == 2) {
-        lds = jsp::compact_lds_bytes(e->blk_leaves);
+        // the tiles keep their rows in LDS between requests when each is one
+        // chunk (JSP_SVC_ROW_CACHE=0: reload every request, A/B)
+        static const bool row_cache = [] { const char* c = std::getenv("JSP_SVC_ROW_CACHE"); return !(c && c[0] == '0'); }();
+        const bool rc = row_cache && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
+        a.row_cache_words = rc ? jsp::service_row_cache_words(e->blk_leaves) : 0u;
+        lds = jsp::service_lds_bytes(e->blk_leaves, (int)e->W, (int)e->R, rc);
         grid = nb + 1;
     } else if (shape == 3) {
         sp.groups = v.groups;
@@ -940,7 +947,11 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         // second half first: the dispatcher reads both halves in one 16-byte load
         __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq,
                          __ATOMIC_RELEASE);
-        __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)J << 32) | seq, __ATOMIC_RELEASE);
+        // the compaction tiles keep their rows in LDS: bit 31 of J tells them the
+        // snapshot was patched since their previous request (J < 2^30)
+        const uint32_t jw = J | (shape == 2 && v.rows_dirty ? 0x80000000u : 0u);
+        v.rows_dirty = false;
+        __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
         const int rc = svc_wait(e, seq);
         if (rc == kSvcGone && attempt == 0) {
             v.running = false;
@@ -1262,7 +1273,11 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     }
     HIP_TRY(upload(e->leaf_start, ls, (size_t)NL + 1, s));
     std::vector<uint4> bt(blk.size() > 0 ? blk.size() - 1 : 0);
-    for (size_t b = 0; b + 1 < blk.size(); ++b) bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
+    uint32_t span = 0;
+    for (size_t b = 0; b + 1 < blk.size(); ++b) {
+        bt[b] = make_uint4(blk[b], blk[b + 1], ls[blk[b]], ls[blk[b + 1]]);
+        span = std::max(span, bt[b].w - (bt[b].z & ~3u));
+    }
     e->blk_l0.assign(blk.begin(), blk.end() - (blk.empty() ? 0 : 1));
     e->blk_l1.assign(blk.begin() + (blk.empty() ? 0 : 1), blk.end());
     if (bt.empty()) bt.push_back(make_uint4(0, 0, 0, 0));  // no rows: never read
@@ -1303,6 +1318,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     e->n_leaves = NL;
     e->max_leaf_rows = max_rows;
     e->n_blocks = (uint32_t)blk.size() - 1;
+    e->max_blk_span = span;
     {
         uint32_t most = 1;
         for (size_t b = 0; b + 1 < blk.size(); ++b) most = std::max(most, blk[b + 1] - blk[b]);
@@ -1333,6 +1349,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
+    e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
     HIP_TRY(upload(e->tmp_a, rows, n, s));

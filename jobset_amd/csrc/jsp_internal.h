@@ -163,6 +163,7 @@ struct ServiceArgs {
     uint32_t gen;                       // service launch number
     uint32_t* nruns;                    // device word: the request's run count (fused shape), or null
     unsigned long long* counter;        // device: finished tiles over all requests (fused shape)
+    uint32_t row_cache_words;           // compaction shape: LDS word offset of the tiles' row copy, 0 = none
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay
@@ -234,6 +235,10 @@ size_t tally_wave_lds_bytes(uint32_t nc, uint32_t nv);
 hipError_t launch_fused(const TallyArgs& a, const FusedArgs& f, hipStream_t s);
 hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t s);
 hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t s);
+// LDS of the compaction service: the compaction's, then (row_cache) the tile's
+// rows kept between requests, from word service_row_cache_words(la) on
+uint32_t service_row_cache_words(uint32_t la);
+size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache);
 hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
 hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);

@@ -81,6 +81,8 @@ __device__ unsigned long long jsp_dbg[4096 * 8];
 // emit flat loads and atomics (each waiting on both the vector and the LDS
 // counters; a release or acquire on one also drains global traffic)
 #define JSP_LDS __attribute__((address_space(3)))
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a 16-B LDS store in any address space
+
 template <typename T>
 __device__ __forceinline__ JSP_LDS T* lds_ptr(T* p) {
     return (JSP_LDS T*)p;
@@ -309,6 +311,49 @@ __device__ __forceinline__ void load_rows(const TallyArgs& a, uint32_t row, bool
     }
 }
 
+// On-chip copy of a thread's 4 rows (the resident compaction service keeps
+// its tile's rows in LDS between requests while no patch touched the
+// snapshot): 2W + 2 + R uint4 per thread, column-major by thread so each
+// 16-B access of a wave is contiguous (no bank conflicts).
+template <int W, int R>
+constexpr int row_cache_vecs() { return 2 * W + 2 + R; }
+
+template <int W, int R>
+__device__ __forceinline__ void rows_to_lds(JSP_LDS u32x4* c, int tid, const RowRegs<W, R>& x) {
+    int k = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        c[(k++) * kTallyThreads + tid] = u32x4{(uint32_t)x.lab[w][0], (uint32_t)(x.lab[w][0] >> 32),
+                                               (uint32_t)x.lab[w][1], (uint32_t)(x.lab[w][1] >> 32)};
+        c[(k++) * kTallyThreads + tid] = u32x4{(uint32_t)x.lab[w][2], (uint32_t)(x.lab[w][2] >> 32),
+                                               (uint32_t)x.lab[w][3], (uint32_t)(x.lab[w][3] >> 32)};
+    }
+    c[(k++) * kTallyThreads + tid] = u32x4{x.tn[0], x.tn[1], x.tn[2], x.tn[3]};
+#pragma unroll
+    for (int r = 0; r < R; ++r) c[(k++) * kTallyThreads + tid] = u32x4{x.fr[r][0], x.fr[r][1], x.fr[r][2], x.fr[r][3]};
+    c[k * kTallyThreads + tid] = u32x4{(uint32_t)x.ex[0], (uint32_t)x.ex[1], (uint32_t)x.ex[2], (uint32_t)x.ex[3]};
+}
+
+template <int W, int R>
+__device__ __forceinline__ void rows_from_lds(const JSP_LDS u32x4* c, int tid, RowRegs<W, R>& x) {
+    int k = 0;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+        const u32x4 u = c[(k++) * kTallyThreads + tid], v = c[(k++) * kTallyThreads + tid];
+        x.lab[w][0] = ((uint64_t)u[1] << 32) | u[0]; x.lab[w][1] = ((uint64_t)u[3] << 32) | u[2];
+        x.lab[w][2] = ((uint64_t)v[1] << 32) | v[0]; x.lab[w][3] = ((uint64_t)v[3] << 32) | v[2];
+    }
+    const u32x4 t4 = c[(k++) * kTallyThreads + tid];
+    x.tn[0] = t4[0]; x.tn[1] = t4[1]; x.tn[2] = t4[2]; x.tn[3] = t4[3];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const u32x4 f4 = c[(k++) * kTallyThreads + tid];
+        x.fr[r][0] = f4[0]; x.fr[r][1] = f4[1]; x.fr[r][2] = f4[2]; x.fr[r][3] = f4[3];
+    }
+    const u32x4 e4 = c[k * kTallyThreads + tid];
+    x.ex[0] = (int32_t)e4[0]; x.ex[1] = (int32_t)e4[1]; x.ex[2] = (int32_t)e4[2]; x.ex[3] = (int32_t)e4[3];
+}
+
 // The fields of one class the row pass reads, moved to SGPRs: every lane
 // reads the same LDS words, so readfirstlane is exact, and the row pass then
 // takes them as scalar operands and branches on them without exec masking
@@ -373,9 +418,13 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 // already in LDS (staged once per service lifetime: they change only with an
 // upload, which restarts the service) and `bt` is the tile's geometry, so the
 // first chunk's row loads are the request's first memory access.
+// row_cache (resident compaction service, single-chunk tiles only): the
+// tile's rows are read from this LDS copy when use_cache, else loaded and
+// copied into it.
 template <int W, int R, bool STAGED = false, bool SC1 = STAGED>
 __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds,
-                                            uint4 bt_staged = make_uint4(0, 0, 0, 0), uint32_t* clk = nullptr) {
+                                            uint4 bt_staged = make_uint4(0, 0, 0, 0), uint32_t* clk = nullptr,
+                                            JSP_LDS u32x4* row_cache = nullptr, bool use_cache = false) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
     DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
@@ -410,9 +459,12 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     // so its HBM latency hides behind the row and leaf passes.
     const uint32_t base0 = r0 & ~3u;
     RowRegs<W, R> cur;
-    {
+    if (row_cache != nullptr && use_cache) {
+        rows_from_lds<W, R>(row_cache, tid, cur);
+    } else {
         const uint32_t row = base0 + 4u * tid;
         load_rows<W, R, SC1>(a, row, (row < r1) && (row + 3 >= r0), cur);
+        if (row_cache != nullptr) rows_to_lds<W, R>(row_cache, tid, cur);
     }
     for (int i = tid; i < nv * la; i += kTallyThreads) s_acc[i] = 0;
     if (st_cls) reinterpret_cast<uint4*>(s_cls)[tid] = cls_v;
@@ -509,7 +561,6 @@ __global__ __launch_bounds__(kTallyThreads) void tally_kernel(TallyArgs a) {
     JSP_STAMP(blockIdx.x, 5);
 }
 
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // a 16-B LDS store in any address space
 
 // ---- wave-tile tally (the three-launch shape's tally: large snapshots)
 // Every wave works alone -- no workgroup barrier after the class records are
@@ -2348,9 +2399,11 @@ template <int W, int R, bool STAGED = false>
 __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
-                                             uint32_t* s_x, uint32_t* clk = nullptr) {
+                                             uint32_t* s_x, uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
+                                             bool use_cache = false) {
     const int tid = threadIdx.x, lane = tid & 63;
-    tally_block<W, R, STAGED>(a, tile, lds, bt, clk);  // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+    // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+    tally_block<W, R, STAGED>(a, tile, lds, bt, clk, row_cache, use_cache);
     JSP_STAMP(tile, 2);
     svc_stamp(clk, 2);
 
@@ -2525,6 +2578,12 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
     uint32_t seq = v.seq0;
     // the tile's constants, staged once: geometry, class record, leaf starts
     const uint4 bt = a.blk[tile];
+    // the tile's rows stay in LDS between requests (v.row_cache_words != 0:
+    // every tile is one chunk); a request whose bell carries the "rows
+    // patched" bit (bit 63: the host patched the snapshot since its previous
+    // request) reloads them
+    JSP_LDS u32x4* row_cache = v.row_cache_words ? lds_ptr(reinterpret_cast<u32x4*>(lds + v.row_cache_words)) : nullptr;
+    bool cached = false;
     {
         constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
         const int tid = threadIdx.x;
@@ -2548,7 +2607,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
                 if (q == kSvcStop) break;
                 if (q != seq && q != 0) {
                     next = q;
-                    J = (uint32_t)(m >> 32);
+                    J = (uint32_t)(m >> 32);  // bit 31: rows patched since the previous request
                     break;
                 }
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
@@ -2561,13 +2620,16 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             s_x[17] = J;
         }
         __syncthreads();
-        const uint32_t next = s_x[16], J = s_x[17];
+        const uint32_t next = s_x[16], Jw = s_x[17];
         if (next == 0) return;
+        const uint32_t J = Jw & 0x7FFFFFFFu;
+        const bool use_cache = cached && (Jw >> 31) == 0u;
         uint32_t* clk = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
         compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
-                                 v.assign, v.stats, v.err, true, lds, s_x, clk);
+                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache);
+        cached = row_cache != nullptr;
         if (clk) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -2955,8 +3017,8 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 
 template <int W, int R>
 static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
-    jsp_launch((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads), compact_lds_bytes(a.la),
-                       s, a, v);
+    jsp_launch((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads),
+               service_lds_bytes(a.la, a.W, a.R, v.row_cache_words != 0), s, a, v);
     return hipGetLastError();
 }
 
@@ -3005,6 +3067,13 @@ hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, in
 }
 
 size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_words(1, 2, (int)la) + 4 + 2 * kTallyWaves + 8); }
+
+uint32_t service_row_cache_words(uint32_t la) { return (uint32_t)((compact_lds_bytes(la) + 15) / 16 * 4); }
+
+size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache) {
+    if (!row_cache) return compact_lds_bytes(la);
+    return sizeof(uint32_t) * service_row_cache_words(la) + (size_t)(2 * W + 2 + R) * 16 * kTallyThreads;
+}
 
 
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,

@@ -28,9 +28,9 @@ SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
        "svc_rows508": {"JSP_BLOCK_ROWS": "508"}, "svc_rows252": {"JSP_BLOCK_ROWS": "252"},
        "svc_split_rows252": {"JSP_SPLIT_COMPACT": "1", "JSP_BLOCK_ROWS": "252"},
        "svc_cold_launch": {"JSP_COLD_LAUNCH": "1"}}
-SVC2 = {"svc_default_1": {}, "svc_split_compact_1": {"JSP_SPLIT_COMPACT": "1"},
-        "svc_default_2": {}, "svc_split_compact_2": {"JSP_SPLIT_COMPACT": "1"},
-        "svc_default_3": {}, "svc_split_compact_3": {"JSP_SPLIT_COMPACT": "1"}}
+SVC2 = {"svc_default_1": {}, "svc_no_row_cache_1": {"JSP_SVC_ROW_CACHE": "0"},
+        "svc_default_2": {}, "svc_no_row_cache_2": {"JSP_SVC_ROW_CACHE": "0"},
+        "svc_default_3": {}, "svc_no_row_cache_3": {"JSP_SVC_ROW_CACHE": "0"}}
 MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
