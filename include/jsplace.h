@@ -141,7 +141,7 @@ typedef struct jsp_timing {
     double host_prep_us;       /* entry to launch: checks, run list into the pinned staging buffer */
     double host_launch_us;     /* the kernel launch call(s) */
     double host_wait_us;       /* launch return to completion seen (completion words or stream sync) */
-    double host_post_us;       /* assign[] (and tallies) out, stats */
+    double host_post_us;       /* assign[] (and tallies) out, stats; the split service: its host walk (inside wait) */
     /* resident service (jsp_engine_set_service) */
     uint64_t svc_calls;        /* jsp_place calls it answered */
     uint64_t svc_starts;       /* service launches (first use, after uploads, idle exits, restarts) */

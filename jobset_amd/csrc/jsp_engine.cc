@@ -875,9 +875,13 @@ int svc_wait(jsp_engine* e, uint32_t seq) {
     auto& v = e->svc;
     const uint32_t* words = v.words.as<uint32_t>();
     const uint32_t n = v.shape == 1 ? 1u : v.nb;  // fused: the tail's one word
+    const bool split = v.shape == 3;
     uint32_t i = 0;
     for (uint64_t spins = 1;; ++spins) {
-        while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) ++i;
+        while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) {
+            if (split) e->walk.prefetch_tile(v.split.as<uint64_t>(), i);  // its slots are final: start their misses
+            ++i;
+        }
         if (i == n) return JSP_OK;
         if ((spins & 255) == 0) {
             const hipError_t q = hipStreamQuery(v.stream);
@@ -963,7 +967,10 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         break;
     }
     if (v.shape == 3) {  // the tiles answered: the walk, into the caller's buffer
+        const auto tw = std::chrono::steady_clock::now();
         *placed = e->walk.place(v.split.as<uint64_t>(), run_class, run_len, n_runs, assign_out);
+        // the host walk's share of the wait (jsp_timing.host_post_us on this path)
+        e->acc.host_post_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tw).count();
         e->acc.svc_calls += 1;
         return JSP_OK;
     }

@@ -98,6 +98,20 @@ void HostWalk::set_tiles(const std::vector<uint32_t>& blk_l0, const std::vector<
     cpg_ = cpg;
 }
 
+void HostWalk::prefetch_tile(const uint64_t* slots, uint32_t t) const {
+    const uint32_t b = t / groups_;
+    if (b >= l0_.size()) return;
+    const uint32_t nl = l1_[b] - l0_[b];
+    const uint32_t blocks = (nl + 63) / 64;  // wave blocks of the tile that hold leaves
+    const uint64_t* s = slots + (size_t)t * (cpg_ + 1) * kSplitSlot;
+    for (uint32_t j = 0; j <= cpg_; ++j)
+        for (uint32_t w = 0; w < blocks; ++w) {
+            const uint64_t* p = s + (size_t)j * kSplitSlot + (size_t)w * kSplitWave;
+            __builtin_prefetch(p, 0, 3);
+            __builtin_prefetch(p + 8, 0, 3);  // an upper class's first records run into the next line
+        }
+}
+
 void HostWalk::build_feasibility(const uint64_t* slots) {
     const size_t tile_words = (size_t)(cpg_ + 1) * kSplitSlot;
     const uint32_t nb = (uint32_t)l0_.size();

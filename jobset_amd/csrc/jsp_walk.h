@@ -33,6 +33,12 @@ public:
     uint32_t place(const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                    int32_t* assign);
 
+    // Tile t (= row block t / groups, class group t % groups) has answered:
+    // start loading its slot lines into the host cache while the other tiles
+    // finish (pinned memory the device just wrote misses every cache level;
+    // read one by one in the walk, the misses cost cfg3 ~3.9 us, cfg5 ~7.4 us).
+    void prefetch_tile(const uint64_t* slots, uint32_t t) const;
+
     // The feasibility bitmaps of the last request (tests / diagnostics):
     // words [woff[c], woff[c+1]) of class c.
     const std::vector<uint64_t>& feas() const { return feas_; }
