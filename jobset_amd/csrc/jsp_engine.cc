@@ -721,6 +721,14 @@ void svc_resume(jsp_engine* e) {
     }
 }
 
+// Resident tiles keep their rows in LDS between requests (JSP_SVC_ROW_CACHE=0:
+// reload every request; read at each service start, so an A/B can switch it
+// inside one process).
+bool svc_row_cache() {
+    const char* c = std::getenv("JSP_SVC_ROW_CACHE");
+    return !(c && c[0] == '0');
+}
+
 int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     auto& v = e->svc;
     if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
@@ -795,10 +803,8 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     jsp::TallyArgs ta{};
     jsp::SplitArgs sp{};
     if (shape == 2) {
-        // the tiles keep their rows in LDS between requests when each is one
-        // chunk (JSP_SVC_ROW_CACHE=0: reload every request, A/B)
-        static const bool row_cache = [] { const char* c = std::getenv("JSP_SVC_ROW_CACHE"); return !(c && c[0] == '0'); }();
-        const bool rc = row_cache && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
+        // the tiles keep their rows in LDS between requests when each is one chunk
+        const bool rc = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
         a.row_cache_words = rc ? jsp::service_row_cache_words(e->blk_leaves) : 0u;
         lds = jsp::service_lds_bytes(e->blk_leaves, (int)e->W, (int)e->R, rc);
         grid = nb + 1;
@@ -808,7 +814,9 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
         sp.C = e->C;
         sp.out = v.split.as<uint64_t>();
         sp.topo = e->topo;
-        lds = jsp::split_lds_bytes(v.cpg, e->blk_leaves);
+        const bool rc = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
+        a.row_cache_words = rc ? jsp::split_row_cache_words(v.cpg, e->blk_leaves) : 0u;
+        lds = jsp::split_service_lds_bytes(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, rc);
         grid = n_tiles + 1;
     } else {
         const size_t cl = (size_t)std::max<uint32_t>(e->C, 1) * std::max<uint32_t>(e->L_total, 1);
@@ -960,9 +968,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         // second half first: the dispatcher reads both halves in one 16-byte load
         __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq,
                          __ATOMIC_RELEASE);
-        // the compaction tiles keep their rows in LDS: bit 31 of J tells them the
-        // snapshot was patched since their previous request (J < 2^30)
-        const uint32_t jw = J | (shape == 2 && v.rows_dirty ? 0x80000000u : 0u);
+        // the compaction and split tiles keep their rows in LDS: bit 31 of J tells
+        // them the snapshot was patched since their previous request (J < 2^30)
+        const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? 0x80000000u : 0u);
         v.rows_dirty = false;
         __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
         const int rc = svc_wait(e, seq, J);

@@ -243,6 +243,9 @@ hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const Se
 size_t compact_lds_bytes(uint32_t la);
 hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);
 size_t split_lds_bytes(uint32_t cpg, uint32_t la);
+// the split service's LDS: split_lds_bytes, then (row_cache) the tile's rows
+uint32_t split_row_cache_words(uint32_t cpg, uint32_t la);
+size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache);
 // Workgroups of the resident service kernel (shape 2 compaction, 1 fused, 3 split) of
 // this W/R that one CU holds at once with lds_bytes each (occupancy API).
 hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, int* blocks_per_cu);

@@ -2801,9 +2801,14 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     const uint4 bt = a.blk[ft.blk];
     uint64_t* out = sp.out + (size_t)tile * (sp.cpg + 1) * kSplitSlot;
     uint32_t seq = v.seq0;
+    // the tile's rows stay in LDS between requests (as the compaction
+    // service's; bit 63 of the bell: the snapshot was patched since the
+    // previous request)
+    JSP_LDS u32x4* row_cache = v.row_cache_words ? lds_ptr(reinterpret_cast<u32x4*>(lds + v.row_cache_words)) : nullptr;
+    bool cached = false;
     while (true) {
         if (threadIdx.x == 0) {
-            uint32_t next = 0;  // 0: leave
+            uint32_t next = 0, dirty = 0;  // next 0: leave
             const uint64_t t0 = wall_clock64();
             while (true) {
                 const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2811,17 +2816,21 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
                 if (q == kSvcStop) break;
                 if (q != seq && q != 0) {
                     next = q;
+                    dirty = (uint32_t)(m >> 63);
                     break;
                 }
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
                 __builtin_amdgcn_s_sleep(1);
             }
             s_x[0] = next;
+            s_x[1] = dirty;
         }
         __syncthreads();
         const uint32_t next = s_x[0];
         if (next == 0) return;
-        tally_block<W, R, false, true>(ag, ft.blk, lds);
+        const bool use_cache = cached && s_x[1] == 0u;
+        tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, row_cache, use_cache);
+        cached = row_cache != nullptr;
         split_emit(ag, sp, bt, out, lds, s_x);
         signal_host(v.done + tile, next, false);
         // drop this CU's L1 lines before the next request (patches come from
@@ -3042,11 +3051,18 @@ size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
     return sizeof(uint32_t) * ((size_t)tally_lds_words((int)cpg, (int)cpg + 1, (int)la) + 16 + kTallyThreads + 4);
 }
 
+uint32_t split_row_cache_words(uint32_t cpg, uint32_t la) { return (uint32_t)((split_lds_bytes(cpg, la) + 15) / 16 * 4); }
+
+size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache) {
+    if (!row_cache) return split_lds_bytes(cpg, la);
+    return sizeof(uint32_t) * split_row_cache_words(cpg, la) + (size_t)(2 * W + 2 + R) * 16 * kTallyThreads;
+}
+
 template <int W, int R>
 static hipError_t launch_split_service_wr(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v,
                                           hipStream_t s) {
     jsp_launch((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups + 1), dim3(kTallyThreads),
-                       split_lds_bytes(sp.cpg, a.la), s, a, sp, v);
+               split_service_lds_bytes(sp.cpg, a.la, a.W, a.R, v.row_cache_words != 0), s, a, sp, v);
     return hipGetLastError();
 }
 
