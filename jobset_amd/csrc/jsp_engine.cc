@@ -189,6 +189,8 @@ struct jsp_engine {
         int shape = 0;   // 2 compaction, 1 fused
         bool clk = false;
         bool rows_dirty = true;  // a patch since the last request: its tiles reload their rows from memory
+        uint32_t pending = 0;    // a compaction request answered early: its tiles' done words still to come
+        bool early = true;       // compaction answers read from the tagged entries (JSP_SVC_EARLY=0: done words)
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
         std::chrono::steady_clock::time_point t_launch{};
@@ -693,6 +695,7 @@ bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
 int svc_stop(jsp_engine* e) {
     auto& v = e->svc;
+    v.pending = 0;  // the stop waits for the kernel to leave, i.e. for every tile to finish
     if (!v.running) return JSP_OK;
     v.running = false;
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
@@ -735,7 +738,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     const uint32_t nb = e->n_blocks;
     if (J > v.cap || !v.assign.p) {
         const uint32_t cap = std::max<uint32_t>(4096, J + J / 2);
-        HIP_TRY(v.assign.reserve((size_t)cap * 4));
+        HIP_TRY(v.assign.reserve((size_t)cap * 8));  // compaction: u64 (seq << 32 | domain) entries
         v.cap = cap;
     }
     const int shape = svc_shape(e);
@@ -788,6 +791,10 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.ready = ready;
     a.gen = v.gen;
     v.err_ack = 0;
+    {
+        const char* c = std::getenv("JSP_SVC_EARLY");  // read per service start (in-process A/B)
+        v.early = !(c && c[0] == '0');
+    }
     v.nb = n_tiles;
     v.blocks = nb;
     v.clk = e->timing;
@@ -895,7 +902,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             if (split) e->walk.prefetch_tile(v.split.as<uint64_t>(), i);  // its slots are final: start their misses
             ++i;
             if (as) {
-                const size_t upto = ((size_t)J * 4 * i / n) & ~size_t(63);
+                const size_t upto = ((size_t)J * 8 * i / n) & ~size_t(63);
                 for (; pf + 64 <= upto; pf += 64) __builtin_prefetch(as + pf, 0, 3);
             }
         }
@@ -905,6 +912,66 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             if (q == hipSuccess) {
                 for (; i < n; ++i)
                     if (__atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq) return kSvcGone;
+                return JSP_OK;
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
+        }
+    }
+}
+
+// The compaction request the host returned from early (its assign[] entries
+// had all arrived): wait for its tiles' done words before anything that needs
+// them idle -- the next request (tiles past the J-th feasible leaf may still be
+// tallying, and the look-back granules are per tile), a patch of the rows.
+int svc_settle(jsp_engine* e) {
+    auto& v = e->svc;
+    if (v.pending == 0) return JSP_OK;
+    const uint32_t q = v.pending;
+    v.pending = 0;
+    if (!v.running) return JSP_OK;
+    const int rc = svc_wait(e, q, 0);
+    if (rc == kSvcGone) {  // it left after answering: nothing is outstanding
+        v.running = false;
+        return JSP_OK;
+    }
+    return rc;
+}
+
+constexpr int kSvcFailed = 3;  // svc_wait_entries: a tile reported a look-back time-out (err word)
+
+// The compaction service's answer read from the entries themselves: entry j
+// is (seq << 32 | domain) in one 8-byte store, so the host copies each out as
+// soon as it carries this request's seq and returns when all J have -- before
+// the tiles drain and publish their done words (those gate the next request:
+// svc_settle). kSvcGone: the service left; kSvcFailed: a tile timed out.
+int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_t* placed) {
+    auto& v = e->svc;
+    const unsigned long long* a = v.assign.as<unsigned long long>();
+    const uint32_t* w = v.words.as<uint32_t>();
+    uint32_t i = 0, n = 0;
+    for (uint64_t spins = 1;; ++spins) {
+        while (i < J) {
+            const unsigned long long x = __atomic_load_n(a + i, __ATOMIC_ACQUIRE);
+            if ((uint32_t)(x >> 32) != seq) break;
+            const int32_t d = (int32_t)(uint32_t)x;
+            out[i++] = d;
+            n += d >= 0 ? 1u : 0u;
+        }
+        if (i == J) {
+            *placed = n;
+            return JSP_OK;
+        }
+        if ((spins & 255) == 0) {
+            if (__atomic_load_n(w + v.nb + 2, __ATOMIC_ACQUIRE) != v.err_ack) return kSvcFailed;
+            const hipError_t q = hipStreamQuery(v.stream);
+            if (q == hipSuccess) {  // it left: whatever arrived is all there is
+                for (; i < J; ++i) {
+                    const unsigned long long x = __atomic_load_n(a + i, __ATOMIC_ACQUIRE);
+                    if ((uint32_t)(x >> 32) != seq) return kSvcGone;
+                    out[i] = (int32_t)(uint32_t)x;
+                    n += out[i] >= 0 ? 1u : 0u;
+                }
+                *placed = n;
                 return JSP_OK;
             }
             if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
@@ -951,8 +1018,12 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     }
     if (!restart) {
         if (int rc = svc_wait_ready(e)) return rc;
+        if (int rc = svc_settle(e)) return rc;
     }
-    uint32_t seq = 0;
+    // the compaction answer is read from its tagged entries (timing on: the
+    // done words, which carry the per-tile stamps)
+    const bool early = shape == 2 && J > 0 && !e->timing && v.early;
+    uint32_t seq = 0, n_early = 0;
     for (int attempt = 0;; ++attempt) {
         if (restart) {
             if (int rc = svc_stop(e)) return rc;
@@ -973,7 +1044,13 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? 0x80000000u : 0u);
         v.rows_dirty = false;
         __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
-        const int rc = svc_wait(e, seq, J);
+        const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
+        if (rc == kSvcFailed) {
+            v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
+            (void)svc_stop(e);
+            return set_err(JSP_EHIP, "placement service request %u failed: the compaction look-back timed out; "
+                                     "its assign[] is invalid", seq);
+        }
         if (rc == kSvcGone && attempt == 0) {
             v.running = false;
             restart = true;
@@ -991,6 +1068,12 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         e->acc.svc_calls += 1;
         return JSP_OK;
     }
+    if (early) {
+        v.pending = seq;
+        *placed = n_early;
+        e->acc.svc_calls += 1;
+        return JSP_OK;
+    }
     const uint32_t* w = v.words.as<uint32_t>();
     const uint32_t ew = __atomic_load_n(w + v.nb + 2, __ATOMIC_ACQUIRE);
     if (ew != v.err_ack) {
@@ -1000,7 +1083,12 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
                                  "its assign[] is invalid", seq);
     }
     const auto tc = std::chrono::steady_clock::now();
-    if (J > 0) std::memcpy(assign_out, v.assign.p, (size_t)J * 4);
+    if (v.shape == 2) {  // u64 entries: the domain is the low half
+        const unsigned long long* a = v.assign.as<unsigned long long>();
+        for (uint32_t j = 0; j < J; ++j) assign_out[j] = (int32_t)(uint32_t)a[j];
+    } else if (J > 0) {
+        std::memcpy(assign_out, v.assign.p, (size_t)J * 4);
+    }
     *placed = __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
     // the copy-out's share of the wait (jsp_timing.host_post_us on this path)
     e->acc.host_post_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count();
@@ -1376,6 +1464,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
+    if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
@@ -1750,6 +1839,7 @@ int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) return jspm::sync(e->multi);
     std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = svc_settle(e)) return rc;  // the service's last request finished on every tile
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->have_last && e->last_foreign) {
         if (int rc = wait_last_foreign(e)) return rc;

@@ -2395,12 +2395,18 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoc
 // for the feasible leaves before it, scatter its jobs' domains. `sys`: assign[]
 // and stats are in pinned host memory (system-scope stores). s_x: the small
 // LDS words after the tally carve ([2] prefix [3] timeout [4..16] scan).
+// tag != 0 (the resident service): assign is a u64 array and entry j is
+// written as (tag << 32) | domain in ONE system-scope store, so the host knows
+// each entry has arrived from the entry itself and returns without waiting for
+// the tiles' done words (which then only gate the next request).
 template <int W, int R, bool STAGED = false>
 __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
                                              uint32_t* s_x, uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
-                                             bool use_cache = false) {
+                                             bool use_cache = false, uint32_t tag = 0) {
+    unsigned long long* assign64 = reinterpret_cast<unsigned long long*>(assign);
+    const unsigned long long tag_hi = (unsigned long long)tag << 32;
     const int tid = threadIdx.x, lane = tid & 63;
     // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     tally_block<W, R, STAGED>(a, tile, lds, bt, clk, row_cache, use_cache);
@@ -2454,10 +2460,17 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     const uint32_t prefix = s_x[2];
     const bool failed = s_x[3] != 0;
     if (!failed) {
-        if (ok && prefix + rank < J) store_out(assign + prefix + rank, (int32_t)(a.leaf_base + l0 + tid), sys);
+        if (ok && prefix + rank < J) {
+            const uint32_t d = a.leaf_base + l0 + tid;
+            if (tag) store_out(assign64 + prefix + rank, tag_hi | d, true);
+            else store_out(assign + prefix + rank, (int32_t)d, sys);
+        }
         if (tile + 1 == a.n_blocks) {
             const uint32_t placed = prefix + total < J ? prefix + total : J;
-            for (uint32_t j = placed + tid; j < J; j += kTallyThreads) store_out(assign + j, -1, sys);
+            for (uint32_t j = placed + tid; j < J; j += kTallyThreads) {
+                if (tag) store_out(assign64 + j, tag_hi | 0xFFFFFFFFull, true);
+                else store_out(assign + j, -1, sys);
+            }
             if (tid == 0 && stats) {
                 store_out(stats, n_runs, sys);
                 store_out(stats + 1, placed, sys);
@@ -2628,7 +2641,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
         compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
-                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache);
+                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next);
         cached = row_cache != nullptr;
         if (clk) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

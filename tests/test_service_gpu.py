@@ -219,6 +219,32 @@ def test_service_after_device_path_and_patch(svc_engine):
     svc_engine.check()
 
 
+def test_service_early_answer_then_patch_and_varying_jobs(svc_engine):
+    """The compaction service answers from its seq-tagged assign[] entries and
+    returns before the tiles' done words; tiles past the J-th feasible leaf may
+    still be tallying then. A patch right after such an answer -- of the rows
+    of the LAST tiles -- and requests whose J alternates (1, fewer than the
+    feasible racks, all of them, more than the racks: the -1 tail) must all
+    equal the oracle on the snapshot as patched so far."""
+    p = synth.config2()
+    svc_engine.load(p)
+    warm(svc_engine, p.job_class)
+    rng = np.random.default_rng(5)
+    n = p.nodes.n_nodes
+    for step in range(60):
+        J = [1, 300, 990, 1500][step % 4]
+        jc = np.zeros(J, dtype=np.uint32)
+        got = svc_engine.place(jc)
+        np.testing.assert_array_equal(got.assign, O.place_c(dataclasses.replace(p, job_class=jc))[0])
+        assert got.placed == int((got.assign >= 0).sum())
+        if step % 3 == 0:  # right after the early answer: rows of the last tiles
+            rows = np.sort(rng.choice(np.arange(n - 2000, n), size=50, replace=False)).astype(np.uint32)
+            taints = rng.integers(0, 2, size=50).astype(np.uint32)
+            svc_engine.patch_rows(rows, taints=taints)
+            p.nodes.taints[rows] = taints
+    svc_engine.check()
+
+
 # ---------------------------------------------------------------- fused shape (cfg3, cfg5)
 # Two resident forms: the split service (default: tiles hand back per-domain
 # feasibility, the host walks; stats.fused 5) and the fused service (the walk

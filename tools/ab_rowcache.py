@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
-"""Interleaved in-process A/B of the resident tiles' LDS row cache
-(JSP_SVC_ROW_CACHE, read at each service start): for cfg2, cfg3, cfg5, ROUNDS
-alternations of 300 host-API calls with the cache on and off (the service is
-restarted at each switch). Prints per variant the median of the per-round
-p50 and p99 (µs). Diagnostic only."""
+"""Interleaved in-process A/B of a resident-service switch read at each
+service start: JSP_SVC_ROW_CACHE (the tiles' LDS row cache, default) or
+JSP_SVC_EARLY (python tools/ab_rowcache.py ROUNDS early: the compaction answer
+read from its tagged entries). For cfg2, cfg3, cfg5, ROUNDS alternations of
+300 host-API calls with the switch on and off (the service is restarted at
+each switch). Prints per variant the median of the per-round p50 and p99
+(µs). Diagnostic only."""
 import json
 import os
 import sys
@@ -16,13 +18,14 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+    var_env = "JSP_SVC_EARLY" if len(sys.argv) > 2 and sys.argv[2] == "early" else "JSP_SVC_ROW_CACHE"
     from jobset_amd import synth
     from jobset_amd.engine import Engine
     from jobset_amd.snapshot import job_runs
     from oracle import oracle as O
     eng = Engine(0)
     out = {}
-    for cfg in (2, 3, 5):
+    for cfg in ((1, 2) if var_env == "JSP_SVC_EARLY" else (2, 3, 5)):
         p = synth.CONFIGS[cfg]()
         eng.load(p)
         a = O.place_c(p)[0]
@@ -30,7 +33,7 @@ def main():
         res = {"on": [], "off": []}
         for r in range(rounds):
             for var in (("on", "off") if r % 2 == 0 else ("off", "on")):
-                os.environ["JSP_SVC_ROW_CACHE"] = "1" if var == "on" else "0"
+                os.environ[var_env] = "1" if var == "on" else "0"
                 eng.service_stop()
                 for _ in range(30):
                     call()
