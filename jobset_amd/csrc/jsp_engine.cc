@@ -122,6 +122,7 @@ struct jsp_engine {
     std::vector<int32_t> h_par[JSP_MAX_LEVELS];
     std::vector<uint32_t> blk_l0, blk_l1;  // leaf range of each tally row block
     uint32_t max_blk_span = 0;             // rows a tally block's first chunk spans, max over blocks
+    bool tally_one = true;                 // one-tile-per-wave tally kernel when the tiles fit (JSP_TALLY_ONE)
     jsp::HostWalk walk;
 
     // snapshot
@@ -458,6 +459,10 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
 // over the CUs, never more than the tiles need and never fewer than 64 tiles
 // per wave allow.
 uint32_t tally_wave_grid(jsp_engine* e) {
+    // one tile per wave (grid 0: the one-set kernel) while every tile fits
+    // 6 waves per SIMD (JSP_TALLY_ONE=0 at engine creation: the
+    // double-buffered kernel, A/B and tests)
+    if (e->tally_one && e->n_wtiles <= (uint32_t)std::max(e->n_cu, 1) * 4u * 6u) return 0;
     static const uint32_t wps = [] {
         const char* v = std::getenv("JSP_TALLY_WPS");
         const long x = v ? std::strtol(v, nullptr, 10) : 4;
@@ -1193,6 +1198,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
     if (const char* v = std::getenv("JSP_SERVICE"))
         e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : std::strcmp(v, "2") == 0 ? JSP_SERVICE_DEVICE_WALK
                                                                                            : JSP_SERVICE_AUTO;
+    if (const char* v = std::getenv("JSP_TALLY_ONE")) e->tally_one = v[0] != '0';
     // test hook: CUs the service may count on (stands in for a smaller GPU or a partition)
     if (const char* v = std::getenv("JSP_SVC_CU_LIMIT")) e->n_cu = std::min<int>(e->n_cu, (int)std::strtol(v, nullptr, 10));
     // test hook: the service's first request number (tests start it next to 2^30)

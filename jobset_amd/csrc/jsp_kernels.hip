@@ -819,6 +819,35 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
     JSP_WSTAMP(t0, 5);
 }
 
+// One tile per wave (the grid covers every tile): a single register set, no
+// descriptor table in lanes -- the tile's descriptor is one scalar load -- so
+// the kernel holds fewer VGPRs and more waves stay resident per SIMD to hide
+// each other's row latency and evaluation.
+template <int W, int R, int NV>
+__global__ __launch_bounds__(kTallyThreads) void tally_wave1_kernel(TallyArgs a, const uint4* __restrict__ tiles,
+                                                                    uint32_t n_tiles, uint32_t n_leaves) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    constexpr int nc = NV - 1;
+    constexpr int nv = NV;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t t = blockIdx.x * kTallyWaves + wid;
+    if (t >= n_tiles) return;
+    const uint4 bt = tiles[t];
+    const JSP_CONST DevClass* k_cls = (const JSP_CONST DevClass*)(a.cls + a.c0);
+    JSP_LDS uint32_t* s_pre = lds_ptr(lds + wid * nv * kWaveTileRows);
+    const WaveRsrc rs{make_rsrc(a.labels, (uint32_t)W * a.npad * 8u), make_rsrc(a.taints, a.npad * 4u),
+                      make_rsrc(a.freer, (uint32_t)R * a.npad * 4u), make_rsrc(a.excl, a.npad * 4u),
+                      make_rsrc(a.leaf_start, (n_leaves + 1u) * 4u)};
+    const __amdgpu_buffer_rsrc_t cap_r = make_rsrc(a.cap_out, (a.c0 + (uint32_t)nc) * a.ld * 4u);
+    const __amdgpu_buffer_rsrc_t occ_r = make_rsrc(a.occ_out, a.do_occ ? a.ld * 4u : 0u);
+    WaveSet<W, R> A;
+    wave_issue<W, R>(a, rs, bt.z & ~3u, bt.x, true, lane, A);
+    uint32_t sums[NV];
+    wave_eval<W, R, NV>(a, k_cls, s_pre, bt, lane, A, sums);
+    wave_store<NV>(a, cap_r, occ_r, bt, lane, sums);
+}
+
 // ----------------------------------------------------------------- feasibility
 // Bit d of class c's word w: capsum(c, d) >= pods[c] && occsum(d) == 0 over the
 // leaves of domain d = 64w + lane at level lvl. One wave computes one word.
@@ -2970,6 +2999,17 @@ template <int W, int R>
 static hipError_t launch_tally_wave_wr(const TallyArgs& a, const uint4* tiles, uint32_t n_tiles, uint32_t n_leaves,
                                        uint32_t grid, hipStream_t s) {
     const size_t lds = tally_wave_lds_bytes(a.nc, a.nc + 1);
+    if (grid == 0) {  // one tile per wave: the grid covers every tile
+        const uint32_t g1 = (n_tiles + kTallyWaves - 1) / kTallyWaves;
+        switch (a.nc) {
+            case 1: jsp_launch((tally_wave1_kernel<W, R, 2>), dim3(g1), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+            case 2: jsp_launch((tally_wave1_kernel<W, R, 3>), dim3(g1), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+            case 3: jsp_launch((tally_wave1_kernel<W, R, 4>), dim3(g1), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+            case 4: jsp_launch((tally_wave1_kernel<W, R, 5>), dim3(g1), dim3(kTallyThreads), lds, s, a, tiles, n_tiles, n_leaves); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     // a wave holds at most 64 tile descriptors, one per lane
     if ((uint64_t)grid * kTallyWaves * 64u < n_tiles) return hipErrorInvalidValue;
     switch (a.nc) {

@@ -321,6 +321,31 @@ def test_f64_division_exact(engine):
         np.testing.assert_array_equal(dcap[:C].cpu().numpy().astype(np.uint32), exp_all[c0:c0 + 4])
 
 
+@pytest.mark.parametrize("cfg", [4, 5])
+def test_double_buffered_wave_tally(monkeypatch, cfg):
+    """The tally's double-buffered wave kernel (several tiles per wave, the next
+    tile's rows in flight while one is evaluated): the default one-tile-per-wave
+    kernel covers snapshots up to ~6k tiles, so this path is forced here
+    (JSP_TALLY_ONE=0, read at engine creation) and 1-8 waves per SIMD are not
+    needed: the tally and the placement must equal the oracle's."""
+    import torch
+    monkeypatch.setenv("JSP_TALLY_ONE", "0")
+    e = Engine(0)
+    try:
+        p = synth.CONFIGS[cfg]()
+        got, a, cap, occ = run_both(e, p)
+        assert_same(got, a, cap, occ)
+        C, L = len(p.classes), p.topology.n_leaves
+        if C <= 4:
+            dcap = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
+            e.tally_device(dcap.data_ptr(), dcap[-1].data_ptr(), L, 0)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(dcap[:C].cpu().numpy().astype(np.uint32), cap)
+            np.testing.assert_array_equal(dcap[C].cpu().numpy().astype(np.uint32), occ)
+    finally:
+        e.close()
+
+
 def test_patch_then_place(engine):
     p = synth.config2()
     engine.load(p)

@@ -20,8 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 AB = os.path.join(ROOT, "tools", "ablib")  # A/B builds (make tools/ablib/<name>/libjsplace.so)
-TALLY = {"block": {"JSP_TALLY_BLOCK": "1"}, "wave2": {"JSP_TALLY_WPS": "2"}, "wave4": {"JSP_TALLY_WPS": "4"},
-         "wave8": {"JSP_TALLY_WPS": "8"}}
+TALLY = {"one": {}, "wave2": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "2"},
+         "wave4": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "4"}, "block": {"JSP_TALLY_BLOCK": "1"},
+         "one_b": {}, "wave4_b": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "4"}}
 # a variant can also load another build of the library: {"JSP_LIB_PATH": os.path.join(AB, name, "libjsplace.so")}
 # (make tools/ablib/<name>/libjsplace.so with AB_FLAGS_<name> in the Makefile)
 SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
