@@ -18,7 +18,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("JSP_LIB_PATH", os.path.join(ROOT, "tools", "diag", "libjsplace.so"))
-os.environ.setdefault("JSP_TALLY_WPS", "2")  # two tiles per wave (stamps 3 and 4 need a second tile)
+os.environ.setdefault("JSP_TALLY_WPS", "2")  # two tiles per wave (stamps 3 and 4 need a second tile),
+os.environ.setdefault("JSP_TALLY_ONE", "0")  # on the double-buffered kernel (the one-tile kernel has no stamps)
 
 
 def main():
