@@ -262,7 +262,7 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                         uint32_t* rec_count, AssignRec* recs, hipStream_t s);
+                         uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

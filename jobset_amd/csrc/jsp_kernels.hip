@@ -1183,8 +1183,13 @@ __device__ uint32_t long_run(uint32_t c, uint32_t j0, uint32_t jend, const uint6
             if (w == wb0) bits &= ~0ull << (cur & 63);
         }
         const uint32_t cnt = (uint32_t)__popcll(bits);
-        uint32_t total;
-        const uint32_t pre = block_excl_scan<NT>(cnt, m.s_w, &total);
+        // one scan counts both the ranks (low 20 bits: <= 64 NT) and the words
+        // holding any (high bits): a record's slot is its word's rank among the
+        // nonzero words, as the taking words are the first nonzero ones
+        const uint32_t rec_base = recs != nullptr ? m.s_misc[1] : 0u;  // read before the scan's barriers
+        uint32_t total_p;
+        const uint32_t pre_p = block_excl_scan<NT>(cnt | (cnt != 0u ? 1u << 20 : 0u), m.s_w, &total_p);
+        const uint32_t pre = pre_p & 0xFFFFFu, total = total_p & 0xFFFFFu;
         JSP_STAMP(4001u + (c & 7u), 1);
         const uint32_t used = total < cap ? total : cap;
         // the owner of each word marks the ranks [pre, min(pre + cnt, used)) taken
@@ -1196,13 +1201,10 @@ __device__ uint32_t long_run(uint32_t c, uint32_t j0, uint32_t jend, const uint6
         if (recs != nullptr) {
             // record mode: one {word, first job, taken bits} record per word that
             // gives domains away; expand_kernel turns them into assign[] with the
-            // whole GPU. Slots from an LDS counter (one add per wave).
-            const uint64_t has = __ballot(took != 0);
-            uint32_t slot0 = 0;
-            if ((tid & 63) == 0 && has != 0) slot0 = atomicAdd(&m.s_misc[1], (uint32_t)__popcll(has));
-            slot0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)slot0);
+            // whole GPU. The last taking word publishes the next record base.
             if (took != 0) {
-                const uint32_t slot = slot0 + (uint32_t)__popcll(has & ((1ull << (tid & 63)) - 1ull));
+                const uint32_t slot = rec_base + (pre_p >> 20);
+                if (pre + cnt >= used) m.s_misc[1] = slot + 1u;
                 AssignRec r;
                 r.dom0 = w * 64;
                 r.base = jpos + pre;
@@ -1524,7 +1526,9 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
                              uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
                              uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs,
-                             uint32_t* __restrict__ rec_count, uint32_t pipe_allowed) {
+                             uint32_t* __restrict__ rec_count, uint32_t pipe_allowed, uint32_t len0 = ~0u,
+                             uint32_t rc0 = 0u) {
+    // len0 != ~0u: the caller loaded the first tile's run (thread tid's) already
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t K = topo.K;
     // the pipelined walk keeps its batch table and progress words in the stage
@@ -1566,8 +1570,9 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
     for (uint32_t r0 = 0; r0 < n_runs; r0 += NT) {
         // ---- a tile of runs: job offsets (block scan of run lengths) and the long-run list
         const uint32_t ri = r0 + tid;
-        const uint32_t len = ri < n_runs ? run_len[ri] : 0u;
-        const uint32_t rc = ri < n_runs ? run_class[ri] : 0u;
+        const bool pre = r0 == 0 && len0 != ~0u;
+        const uint32_t len = pre ? len0 : ri < n_runs ? run_len[ri] : 0u;
+        const uint32_t rc = pre ? rc0 : ri < n_runs ? run_class[ri] : 0u;
         m.s_rc[tid] = rc;
         uint32_t tile_total, n_long;
         const uint32_t off = block_excl_scan<NT>(len, m.s_w, &tile_total);
@@ -1813,7 +1818,6 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const uint32_t cls = job ? m.s_bcls[my_start] : 0u;
-                const uint32_t woff = (uint32_t)__shfl((int)my_woff, (int)cls);
                 q += nrb;
                 // live classes of the batch; the scan starts at their lowest cursor
                 // (every class's domains below its cursor are taken or infeasible)
@@ -1986,35 +1990,64 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     uint32_t* s_topo = s_small + assign_small_words(kAssignThreads);
     uint32_t* s_stage = s_topo + (topo_in_lds ? topo_words : 0u);
     JSP_STAMP(4000u, 0);
+    // the first tile of runs and up to 4 feasibility words per thread are
+    // loaded before any staging store, so their latencies overlap (the run
+    // table otherwise waited for the staging barrier)
+    const uint32_t tid = threadIdx.x;
+    const uint32_t len0 = tid < n_runs ? run_len[tid] : 0u;
+    const uint32_t rc0 = tid < n_runs ? run_class[tid] : 0u;
+    uint64_t f4[4];
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = tid + k * kAssignThreads;
+        f4[k] = i < fw ? feas[i] : 0ull;
+    }
     stage_meta<kAssignThreads>(m, cls, C, word_off, topo);
-    if (threadIdx.x == 0) m.s_misc[1] = 0;
+    if (tid == 0) m.s_misc[1] = 0;
     if (topo_in_lds) stage_topo<kAssignThreads>(s_topo, topo);
-    for (uint32_t i = threadIdx.x; i < tw; i += kAssignThreads) s_dyn[i] = 0;
-    for (uint32_t i = threadIdx.x; i < fw; i += kAssignThreads) s_feas[i] = feas[i];
+    for (uint32_t i = tid; i < tw; i += kAssignThreads) s_dyn[i] = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = tid + k * kAssignThreads;
+        if (i < fw) s_feas[i] = f4[k];
+    }
+    for (uint32_t i = tid + 4 * kAssignThreads; i < fw; i += kAssignThreads) s_feas[i] = feas[i];
     __syncthreads();
     JSP_STAMP(4000u, 1);
     const uint64_t* F = feas_in_lds ? s_feas : feas;
     if (topo_in_lds)
         assign_block<kAssignThreads, true>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m, s_topo,
-                                           s_win, s_stage, stage_cap, recs, rec_count, pipe);
+                                           s_win, s_stage, stage_cap, recs, rec_count, pipe, len0, rc0);
     else
         assign_block<kAssignThreads, false>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m,
-                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count, pipe);
+                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count, pipe, len0, rc0);
 }
 
-// Expansion of assign_kernel's records (grid-stride, one wave per record):
-// lane b of a record with bit b taken writes job base + (taken bits below b).
-// Each record's jobs are consecutive, so a wave's stores are one run.
+// Expansion of assign_kernel's records: a wave owns rpw (<= 64) consecutive
+// records of the host's bound (records <= min(J, feas_words + runs)); lane i
+// loads record r0 + i in one coalesced load issued beside the count's, then
+// the wave writes them one at a time: lane b of a record with bit b taken
+// writes job base + (taken bits below b), so each store is one run. A small
+// grid (tens of blocks, not one wave per job) is most of this kernel's time.
 __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict__ recs,
-                                                     const uint32_t* __restrict__ rec_count,
-                                                     int32_t* __restrict__ assign) {
-    const uint32_t n = *rec_count;
+                                                     const uint32_t* __restrict__ rec_count, uint32_t bound,
+                                                     uint32_t rpw, int32_t* __restrict__ assign) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint32_t waves = gridDim.x * (blockDim.x >> 6);
-    for (uint32_t r = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += waves) {
-        const AssignRec x = recs[r];
-        if ((x.took >> lane) & 1ull)
-            assign[x.base + (uint32_t)__popcll(x.took & ((1ull << lane) - 1ull))] = (int32_t)(x.dom0 + lane);
+    const uint32_t r0 = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rpw;
+    if (r0 >= bound) return;  // wave-uniform
+    AssignRec x{0u, 0u, 0ull};
+    if (lane < rpw && r0 + lane < bound) x = recs[r0 + lane];
+    const uint32_t n = *rec_count;
+    if (r0 >= n) return;
+    const uint32_t m = n - r0 < rpw ? n - r0 : rpw;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t t_lo = (uint32_t)x.took, t_hi = (uint32_t)(x.took >> 32);
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint64_t t = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t_hi, (int)i) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)t_lo, (int)i);
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)x.base, (int)i);
+        const uint32_t dom0 = (uint32_t)__builtin_amdgcn_readlane((int)x.dom0, (int)i);
+        if ((t >> lane) & 1ull) assign[base + (uint32_t)__popcll(t & below)] = (int32_t)(dom0 + lane);
     }
 }
 
@@ -3206,7 +3239,7 @@ bool pipe_walk_enabled() {
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                         uint32_t* rec_count, AssignRec* recs, hipStream_t s) {
+                         uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s) {
     const uint32_t topo_words = topo.K > 1 ? topo_table_words(topo.K, topo.D) : 0u;
     const AssignPlan p = plan_assign(t_words, feas_words, topo_words);
     if (p.lds_bytes == 0) return hipErrorInvalidValue;
@@ -3214,9 +3247,14 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
                        run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
                        topo_words, p.stage_cap, recs, rec_count, pipe_walk_enabled() ? 1u : 0u);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
-    // records never outnumber the placed jobs (each taken domain is in one record)
-    const uint32_t waves = J < 8192u ? J : 8192u;
-    jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, assign);
+    // Records never outnumber the placed jobs (each taken domain is in one
+    // record), nor the feasibility words plus one per run (a run's records are
+    // distinct words of its class; the next run of the class may share one).
+    const uint64_t wb = (uint64_t)feas_words + n_runs;
+    const uint32_t bound = wb < J ? (uint32_t)wb : J;
+    const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
+    const uint32_t waves = (bound + rpw - 1) / rpw;
+    jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
     return hipGetLastError();
 }
 

@@ -346,6 +346,25 @@ def test_double_buffered_wave_tally(monkeypatch, cfg):
         e.close()
 
 
+@pytest.mark.parametrize("rpw", ["1", "7", "64"])
+def test_expand_records_per_wave(monkeypatch, rpw):
+    """The three-launch path's record expansion with 1, 7 (records straddling
+    waves unevenly) and 64 records per wave (JSP_EXPAND_RPW, read at engine
+    creation; default 16): each configuration places as the oracle does."""
+    monkeypatch.setenv("JSP_EXPAND_RPW", rpw)
+    e = Engine(0)
+    try:
+        e.set_fused(False)
+        probs = [synth.CONFIGS[cfg]() for cfg in (1, 2, 4, 5)]
+        probs += [synth.random_problem(7000 + s, max_nodes=100_000, max_jobs=20_000) for s in range(6)]
+        for p in probs:
+            got, a, cap, occ = run_both(e, p)
+            assert got.fused == 0
+            assert_same(got, a, cap, occ)
+    finally:
+        e.close()
+
+
 def test_patch_then_place(engine):
     p = synth.config2()
     engine.load(p)

@@ -8,6 +8,8 @@ its own child process because the engine reads its tuning variables once.
                                      before each of 20 launches), bit-exact vs oracle
   python tools/ab_probe.py mark      device path (jsp_place_device) per-call host and
                                      GPU time with each caller-stream marker
+  python tools/ab_probe.py step      cfg4 three-launch step (place_device) GPU time
+                                     per call with 1/4/16/64 records per expand wave
   python tools/ab_probe.py one KEY   one variant (the child side)
 """
 import json
@@ -32,6 +34,8 @@ SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
 SVC2 = {"svc_default_1": {}, "svc_no_row_cache_1": {"JSP_SVC_ROW_CACHE": "0"},
         "svc_default_2": {}, "svc_no_row_cache_2": {"JSP_SVC_ROW_CACHE": "0"},
         "svc_default_3": {}, "svc_no_row_cache_3": {"JSP_SVC_ROW_CACHE": "0"}}
+STEP = {"rpw1": {"JSP_EXPAND_RPW": "1"}, "rpw4": {"JSP_EXPAND_RPW": "4"}, "rpw16": {"JSP_EXPAND_RPW": "16"},
+        "rpw64": {"JSP_EXPAND_RPW": "64"}, "rpw1_b": {"JSP_EXPAND_RPW": "1"}, "rpw16_b": {"JSP_EXPAND_RPW": "16"}}
 MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
@@ -103,6 +107,36 @@ def child_mark():
     return out
 
 
+def child_step():
+    """cfg4 device path (tally -> feas -> assign -> expand) GPU time per call
+    over 500 back-to-back calls, bit-exact vs the oracle."""
+    import numpy as np
+    import torch
+
+    import bench
+    from jobset_amd import synth
+    from jobset_amd.engine import Engine
+    from jobset_amd.snapshot import job_runs
+    from oracle import oracle as O
+    p = synth.config4()
+    eng = Engine(0)
+    eng.load(p)
+    stream = torch.cuda.current_stream().cuda_stream
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    o = torch.empty(max(p.n_jobs, 1), dtype=torch.int32, device="cuda")
+    fn = lambda: eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs,  # noqa: E731
+                                  o.data_ptr(), stream)
+    for _ in range(20):
+        fn()
+    torch.cuda.synchronize()
+    exact = bool(np.array_equal(o.cpu().numpy(), O.place_c(p)[0]))
+    gpu = bench.event_loop_us(fn, 500, stream)
+    eng.check()
+    return {"exact": exact, "gpu_us_per_call": round(gpu, 2)}
+
+
 def child_svc():
     """Host-API jsp_place p50/p99 (resident service) on cfg1/2/3/5, 1000 calls
     each, plus 40 cold calls (the service idle-exited, a row patched)."""
@@ -150,12 +184,13 @@ def main():
     mode = sys.argv[1]
     if mode == "one":
         key = sys.argv[2]
-        for d in (TALLY, SVC, SVC2, MARK):  # the variant's environment (also when run directly, e.g. under rocprofv3)
+        for d in (TALLY, SVC, SVC2, MARK, STEP):  # the variant's environment (also when run directly, e.g. under rocprofv3)
             os.environ.update(d.get(key, {}))
-        res = child_tally() if key in TALLY else child_svc() if key in SVC or key in SVC2 else child_mark()
+        res = (child_tally() if key in TALLY else child_svc() if key in SVC or key in SVC2
+               else child_step() if key in STEP else child_mark())
         print(json.dumps({key: res}), flush=True)
         return
-    variants = TALLY if mode == "tally" else SVC if mode == "svc" else SVC2 if mode == "svc2" else MARK
+    variants = {"tally": TALLY, "svc": SVC, "svc2": SVC2, "step": STEP}.get(mode, MARK)
     for key, env in variants.items():
         e = dict(os.environ)
         e.update(env)
