@@ -992,29 +992,32 @@ __device__ void lds_set_range(uint64_t* t, uint32_t lo, uint32_t hi) {
     }
 }
 
+// Block-wide exclusive scan with ONE barrier: each wave publishes its total
+// in region `slot` of s_w, then every wave combines the NT/64 totals itself
+// (lanes < NT/64 read them) instead of waiting for wave 0 to scan them behind
+// a second barrier. A region is free again after the next barrier, so two
+// scans with no barrier between them use different slots (0, 1).
 template <int NT>
-__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total) {
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t x, uint32_t* s_w, uint32_t* total, int slot = 0) {
     constexpr int NW = NT / 64;
-    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t* w = s_w + slot * NW;
     const uint32_t incl = wave_incl_scan(x, lane);
-    if (lane == 63) s_w[wid] = incl;
+    if (lane == 63) w[wid] = incl;
     __syncthreads();
-    if (wid == 0) {
-        const uint32_t v = lane < NW ? s_w[lane] : 0u;
-        const uint32_t s = wave_incl_scan(v, lane);
-        if (lane < NW) s_w[NW + lane] = s - v;  // exclusive
-        if (lane == NW - 1) s_w[2 * NW] = s;
-    }
-    __syncthreads();
-    *total = s_w[2 * NW];
-    return s_w[NW + wid] + incl - x;
+    const uint32_t v = lane < NW ? w[lane] : 0u;
+    const uint32_t sc = wave_incl_scan(v, lane);
+    *total = (uint32_t)__builtin_amdgcn_readlane((int)sc, NW - 1);
+    const uint32_t before = wid > 0 ? (uint32_t)__builtin_amdgcn_readlane((int)sc, wid - 1) : 0u;
+    return before + incl - x;
 }
 
 // Small LDS tables of the assignment (all filled in one round of loads):
 // per class its level, pods, bitmap word offset and cursor; per level the
 // offset of its taken bitmap (computed from topo.D, no memory).
 struct AssignMeta {
-    uint32_t* s_w;       // 2*NW + 4 (block scans)
+    uint32_t* s_w;       // 2*NW + 4 (block scans: two NW-word slots)
     uint32_t* s_misc;    // 4
     uint32_t* s_cursor;  // kMaxClasses
     uint32_t* s_lvl;     // kMaxClasses
@@ -1578,7 +1581,7 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
         const uint32_t off = block_excl_scan<NT>(len, m.s_w, &tile_total);
         m.s_ro[tid] = off;
         const bool is_long = len > kWaveRunMax && rc < C;
-        const uint32_t lrank = block_excl_scan<NT>(is_long ? 1u : 0u, m.s_w, &n_long);
+        const uint32_t lrank = block_excl_scan<NT>(is_long ? 1u : 0u, m.s_w, &n_long, 1);
         if (is_long) m.s_long[lrank] = (uint32_t)tid;
         __syncthreads();
         const uint32_t nr = (n_runs - r0) < (uint32_t)NT ? (n_runs - r0) : (uint32_t)NT;
