@@ -124,6 +124,7 @@ struct jsp_engine {
     uint32_t max_blk_span = 0;             // rows a tally block's first chunk spans, max over blocks
     bool tally_one = true;                 // one-tile-per-wave tally kernel when the tiles fit (JSP_TALLY_ONE)
     uint32_t expand_rpw = 16;              // assignment records per expand wave (JSP_EXPAND_RPW, 1..64)
+    bool assign_records = true;            // long runs as records + expand_kernel (JSP_ASSIGN_RECORDS=0: staged stores)
     jsp::HostWalk walk;
 
     // snapshot
@@ -513,8 +514,8 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
                                e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
                                d_assign,
-                               stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(),
-                               e->expand_rpw, s));
+                               stats_ptr(e), e->stats.as<uint32_t>() + 3,
+                               e->assign_records ? e->recs.as<jsp::AssignRec>() : nullptr, e->expand_rpw, s));
     ev_end(p, s);
     return JSP_OK;
 }
@@ -1201,6 +1202,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : std::strcmp(v, "2") == 0 ? JSP_SERVICE_DEVICE_WALK
                                                                                            : JSP_SERVICE_AUTO;
     if (const char* v = std::getenv("JSP_TALLY_ONE")) e->tally_one = v[0] != '0';
+    if (const char* v = std::getenv("JSP_ASSIGN_RECORDS")) e->assign_records = v[0] != '0';
     if (const char* v = std::getenv("JSP_EXPAND_RPW")) e->expand_rpw = (uint32_t)std::clamp(std::atol(v), 1L, 64L);
     // test hook: CUs the service may count on (stands in for a smaller GPU or a partition)
     if (const char* v = std::getenv("JSP_SVC_CU_LIMIT")) e->n_cu = std::min<int>(e->n_cu, (int)std::strtol(v, nullptr, 10));

@@ -346,12 +346,15 @@ def test_double_buffered_wave_tally(monkeypatch, cfg):
         e.close()
 
 
-@pytest.mark.parametrize("rpw", ["1", "7", "64"])
+@pytest.mark.parametrize("rpw", ["1", "7", "64", "staged"])
 def test_expand_records_per_wave(monkeypatch, rpw):
     """The three-launch path's record expansion with 1, 7 (records straddling
     waves unevenly) and 64 records per wave (JSP_EXPAND_RPW, read at engine
     creation; default 16): each configuration places as the oracle does."""
-    monkeypatch.setenv("JSP_EXPAND_RPW", rpw)
+    if rpw == "staged":  # long runs through the LDS stage and coalesced stores, no records
+        monkeypatch.setenv("JSP_ASSIGN_RECORDS", "0")
+    else:
+        monkeypatch.setenv("JSP_EXPAND_RPW", rpw)
     e = Engine(0)
     try:
         e.set_fused(False)

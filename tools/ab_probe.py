@@ -9,7 +9,7 @@ its own child process because the engine reads its tuning variables once.
   python tools/ab_probe.py mark      device path (jsp_place_device) per-call host and
                                      GPU time with each caller-stream marker
   python tools/ab_probe.py step      cfg4 three-launch step (place_device) GPU time
-                                     per call with 1/4/16/64 records per expand wave
+                                     per call with 1/4/16/64 records per expand wave, or staged stores
   python tools/ab_probe.py one KEY   one variant (the child side)
 """
 import json
@@ -35,7 +35,8 @@ SVC2 = {"svc_default_1": {}, "svc_no_row_cache_1": {"JSP_SVC_ROW_CACHE": "0"},
         "svc_default_2": {}, "svc_no_row_cache_2": {"JSP_SVC_ROW_CACHE": "0"},
         "svc_default_3": {}, "svc_no_row_cache_3": {"JSP_SVC_ROW_CACHE": "0"}}
 STEP = {"rpw1": {"JSP_EXPAND_RPW": "1"}, "rpw4": {"JSP_EXPAND_RPW": "4"}, "rpw16": {"JSP_EXPAND_RPW": "16"},
-        "rpw64": {"JSP_EXPAND_RPW": "64"}, "rpw1_b": {"JSP_EXPAND_RPW": "1"}, "rpw16_b": {"JSP_EXPAND_RPW": "16"}}
+        "rpw64": {"JSP_EXPAND_RPW": "64"}, "staged": {"JSP_ASSIGN_RECORDS": "0"}, "rpw16_b": {"JSP_EXPAND_RPW": "16"},
+        "staged_b": {"JSP_ASSIGN_RECORDS": "0"}}
 MARK = {"launch_stop": {}, "record": {"JSP_STREAM_MARK": "record"}, "event_sys": {"JSP_EVENT_FLAGS": "sys"}, "event_dev": {"JSP_EVENT_FLAGS": "dev"},
         "event_nofence": {"JSP_EVENT_FLAGS": "nofence"}, "value": {"JSP_STREAM_MARK": "value"},
         "none": {"JSP_STREAM_MARK": "none"}}
