@@ -93,6 +93,7 @@ tools/bin/valu_rate: tools/valu_rate.hip
 
 # A/B builds of the kernels with one build flag (tools/ab_probe.py loads them
 # through JSP_LIB_PATH): tools/ablib/<name>/libjsplace.so
+AB_FLAGS_fakedesc = -DJSP_AB_FAKE_DESC
 tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
 	@mkdir -p build/ab_$* tools/ablib/$*
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(AB_FLAGS_$*) -c -o build/ab_$*/k.o jobset_amd/csrc/jsp_kernels.hip

@@ -833,7 +833,16 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave1_kernel(TallyArgs a,
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint32_t t = blockIdx.x * kTallyWaves + wid;
     if (t >= n_tiles) return;
+#ifdef JSP_AB_FAKE_DESC
+    // diagnostic A/B build only (wrong sums): the descriptor from the tile
+    // index (12 leaves in 252 rows, cfg4's shape), no dependent load before
+    // the rows -- what a fixed-window tiling would save cold
+    (void)tiles;
+    const uint32_t fl0 = t * 12u < n_leaves ? t * 12u : n_leaves;
+    const uint4 bt = make_uint4(fl0, fl0 + 12u < n_leaves ? fl0 + 12u : n_leaves, t * 252u, t * 252u + 252u);
+#else
     const uint4 bt = tiles[t];
+#endif
     const JSP_CONST DevClass* k_cls = (const JSP_CONST DevClass*)(a.cls + a.c0);
     JSP_LDS uint32_t* s_pre = lds_ptr(lds + wid * nv * kWaveTileRows);
     const WaveRsrc rs{make_rsrc(a.labels, (uint32_t)W * a.npad * 8u), make_rsrc(a.taints, a.npad * 4u),

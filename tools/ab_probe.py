@@ -24,7 +24,10 @@ sys.path.insert(0, ROOT)
 AB = os.path.join(ROOT, "tools", "ablib")  # A/B builds (make tools/ablib/<name>/libjsplace.so)
 TALLY = {"one": {}, "wave2": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "2"},
          "wave4": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "4"}, "block": {"JSP_TALLY_BLOCK": "1"},
-         "one_b": {}, "wave4_b": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "4"}}
+         "one_b": {}, "wave4_b": {"JSP_TALLY_ONE": "0", "JSP_TALLY_WPS": "4"},
+         # diagnostic build: descriptors from the tile index (wrong sums, exact false): the cost of the dependent load
+         "fakedesc": {"JSP_LIB_PATH": os.path.join(AB, "fakedesc", "libjsplace.so")}, "one_c": {},
+         "fakedesc_b": {"JSP_LIB_PATH": os.path.join(AB, "fakedesc", "libjsplace.so")}}
 # a variant can also load another build of the library: {"JSP_LIB_PATH": os.path.join(AB, name, "libjsplace.so")}
 # (make tools/ablib/<name>/libjsplace.so with AB_FLAGS_<name> in the Makefile)
 SVC = {"svc_default": {}, "svc_split_compact": {"JSP_SPLIT_COMPACT": "1"},
