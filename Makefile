@@ -98,3 +98,6 @@ tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o 
 	@mkdir -p build/ab_$* tools/ablib/$*
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) $(AB_FLAGS_$*) -c -o build/ab_$*/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_$*/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+tools/bin/block_probe: tools/block_probe.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<

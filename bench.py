@@ -108,6 +108,12 @@ def evidence_dirs():
     return out
 
 
+def latest_dir():
+    """The evidence directory profiles/LATEST names (None when absent)."""
+    f = os.path.join(ROOT, "profiles", "LATEST")
+    return os.path.join(ROOT, open(f).read().strip()) if os.path.exists(f) else None
+
+
 def pmc_traffic(kernel, cfg: int):
     """HBM bytes per launch of `kernel` (a name prefix or a tuple of them) from
     the committed rocprofv3 PMC passes (latest round under profiles/):
@@ -130,7 +136,8 @@ def pmc_traffic(kernel, cfg: int):
         if os.path.exists(fp) and os.path.exists(wp):
             fa, wa = avg(fp), avg(wp)
             if fa is not None and wa is not None:
-                return {"bytes": round((2 * fa + wa) * 1024), "source": os.path.relpath(d, ROOT)}
+                return {"bytes": round((2 * fa + wa) * 1024), "source": os.path.relpath(d, ROOT),
+                        "latest": d == latest_dir()}
     return None
 
 
@@ -257,31 +264,136 @@ def settled_place(eng, job_class):
     return r
 
 
-def cold_recovery_latency(eng, p, trials: int):
+def _pcts(lat):
+    lat = sorted(lat)
+    pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 1)  # noqa: E731
+    return {"p50_us": pct(0.50), "p99_us": pct(0.99), "max_us": round(lat[-1], 1), "n": len(lat)}
+
+
+COLD_GAPS_MS = (0.0, 1.0, 10.0)
+
+
+def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
     """The realistic recovery (failures are hours apart,
     keps/262-ConfigurableFailurePolicy/README.md:232-234): the resident
     service has idle-exited (the host sleeps past JSP_SERVICE_IDLE_MS), a
     watch event patches one row (the failed job's node back to schedulable),
-    then jsp_place on host wall. Untimed: the sleep and the patch."""
+    then the recreate calls jsp_place. Timed: the patch call plus the place
+    call (host wall). Between them a gap: 0 (the place right behind the patch)
+    or the time the reconciler needs before it recreates -- the deletions
+    that produce the patches are foreground deletes whose completion triggers
+    the recreate (pkg/controllers/jobset_controller.go:553-576, 698-709), at
+    least one API-server round trip (1 and 10 ms here); the gap itself is not
+    counted. The patch wakes the service (jsp_snapshot_patch, ABI v5)."""
     from jobset_amd.snapshot import job_runs
     if trials <= 0:
         return None
     idle_ms = float(os.environ.get("JSP_SERVICE_IDLE_MS", "50"))
     call = eng.host_placer(*job_runs(p.job_class))
     call()
-    lat = []
-    row = np.zeros(1, dtype=np.uint32)
-    for t in range(trials):
-        time.sleep((idle_ms + 10.0) * 1e-3)
-        row[0] = (t * 7919) % max(p.nodes.n_nodes, 1)
-        eng.patch_rows(row, taints=p.nodes.taints[row])  # same value: the snapshot is unchanged
-        t0 = time.perf_counter()
+    out = {}
+    for gap in gaps_ms:
+        tot, pat, pla, gaps, shapes = [], [], [], [], {}
+        for t in range(trials):
+            row = np.array([(t * 7919 + int(gap * 13)) % max(p.nodes.n_nodes, 1)], dtype=np.uint32)
+            patch = eng.host_patcher(row, taints=p.nodes.taints[row])  # same value: the snapshot is unchanged
+            time.sleep((idle_ms + 10.0) * 1e-3)
+            t0 = time.perf_counter()
+            patch()
+            t1 = time.perf_counter()
+            if gap > 0:
+                time.sleep(gap * 1e-3)
+            t2 = time.perf_counter()
+            st = call()
+            t3 = time.perf_counter()
+            tot.append(((t1 - t0) + (t3 - t2)) * 1e6)
+            pat.append((t1 - t0) * 1e6)
+            pla.append((t3 - t2) * 1e6)
+            gaps.append((t2 - t1) * 1e3)
+            shapes[int(st.fused)] = shapes.get(int(st.fused), 0) + 1
+        line = _pcts(tot)
+        line.update({"patch_p50_us": _pcts(pat)["p50_us"], "place_p50_us": _pcts(pla)["p50_us"],
+                     "place_p99_us": _pcts(pla)["p99_us"], "gap_ms_p50": round(float(np.median(gaps)), 3),
+                     "shapes": {str(k): v for k, v in sorted(shapes.items())}})
+        out[f"gap_{gap:g}ms"] = line
+    out["note"] = (f"service idle-exited (sleep {idle_ms + 10:.0f} ms), then a one-row patch (jsp_snapshot_patch) and, "
+                   "after the stated gap, jsp_place; timed = patch call + place call (host wall), the gap excluded")
+    return out
+
+
+def cpu_cold_recovery(p, trials: int, threads, idle_ms: float):
+    """The same recovery on the CPU evaluator: after the same idle sleep, the
+    same one-row patch (written into the evaluator's columns), then one
+    placement; timed = patch + placement."""
+    from oracle import oracle as O
+    out = {}
+    for th in threads:
+        fc = O.FastCPU(th)
+        fc.prepare(p)
+        fc.run()
+        taints = fc.pk.arrs["taints"]
+        lat = []
+        for t in range(trials):
+            row = (t * 7919) % max(p.nodes.n_nodes, 1)
+            v = int(taints[row])
+            time.sleep((idle_ms + 10.0) * 1e-3)
+            t0 = time.perf_counter()
+            taints[row] = v
+            fc.run()
+            lat.append((time.perf_counter() - t0) * 1e6)
+        fc.close()
+        out[f"{th}t"] = _pcts(lat)
+    return out
+
+
+def patched_step_us(eng, p, steps: int):
+    """Host-API steps with one row patched before each placement (a watch
+    event between recoveries): the resident tiles reload their rows from
+    memory instead of their LDS copies. µs per (patch + place)."""
+    from jobset_amd.snapshot import job_runs
+    call = eng.host_placer(*job_runs(p.job_class))
+    rows = [np.array([(i * 7919) % p.nodes.n_nodes], dtype=np.uint32) for i in range(16)]
+    patches = [eng.host_patcher(r, taints=p.nodes.taints[r]) for r in rows]
+    for i in range(20):
+        patches[i % 16]()
         call()
-        lat.append((time.perf_counter() - t0) * 1e6)
-    lat.sort()
-    pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 1)  # noqa: E731
-    return {"p50_us": pct(0.50), "p99_us": pct(0.99), "max_us": round(lat[-1], 1), "n": len(lat),
-            "note": f"service idle-exited (sleep {idle_ms + 10:.0f} ms), one row patched, then jsp_place"}
+    t0 = time.perf_counter()
+    for i in range(steps):
+        patches[i % 16]()
+        call()
+    return (time.perf_counter() - t0) * 1e6 / steps
+
+
+def device_set_leg(p4, ref_assign, steps: int):
+    """cfg4 through jsp_engine_create_multi over every visible GPU of this
+    process (RCCL all-reduce between distinct devices; ids {0, 0} on a
+    one-GPU box: two shards and the on-device add). Host-API step time and
+    bit-exactness against the single-device engine's answer."""
+    import torch
+    from jobset_amd.engine import Engine
+    from jobset_amd.snapshot import job_runs
+    n_dev = torch.cuda.device_count()
+    ids = list(range(n_dev)) if n_dev > 1 else [0, 0]
+    try:
+        with Engine(devices=ids) as ds:
+            ds.load(p4)
+            call = ds.host_placer(*job_runs(p4.job_class))
+            for _ in range(3):
+                call()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                call()
+            us = (time.perf_counter() - t0) * 1e6 / steps
+            sh, nd = ds.shards()
+            exact = bool(np.array_equal(call.assign, ref_assign))
+            return {"device_ids": ids, "shards": sh, "devices": nd,
+                    "combine": "RCCL all-reduce (ncclCommInitAll in this process)" if nd > 1 else "on-device add",
+                    "us_per_step": round(us, 1), "placed": int((call.assign >= 0).sum()),
+                    "placements_per_s": round(int((call.assign >= 0).sum()) / (us * 1e-6), 1),
+                    "bit_exact_vs_single_device": exact, "steps": steps,
+                    "note": "host API (jsp_place): run list in, assign[] back in host memory"}
+    except Exception as ex:  # noqa: BLE001 -- reported in the line, never hidden
+        return {"device_ids": ids, "error": str(ex)}
 
 
 def relaunch_with_torchrun(n: int) -> int:
@@ -416,6 +528,11 @@ def main() -> None:
                "note": "device time of one request inside the resident kernel (stamps on, which add "
                        "~0.5-1 us); the host-API wall adds the host-link hand-offs"}
 
+    # one row patched before each call (the resident tiles reload their rows
+    # from memory instead of their LDS copies); not the timed loop
+    patched = round(patched_step_us(eng, p, max(200, args.steps * 5)), 3) if shape == 3 else None
+    eng.service_stop()
+
     # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
     step, out = device_step(p)
     for _ in range(args.warmup):
@@ -435,13 +552,24 @@ def main() -> None:
     # the persistent kernel, which HIP events cannot bracket per request: the
     # roofline is the launch-path compaction kernel's, the service's own
     # per-request device time is under "service".
+    # The launch's own duration: events on its dispatch packets
+    # (jsp_place_device_timed, the engine stream), back to back, none of the
+    # host's submit time between them -- what a kernel trace reports; the
+    # event loop around ctypes-issued launches is kept beside it.
+    n_dev_iters = max(200, args.steps)
     if shape in (1, 2, 3, 4):
-        dom_us = event_loop_us(step, args.steps, stream)
+        rc_np, rl_np = job_runs(p.job_class)
+        rct = torch.from_numpy(rc_np.astype(np.int32)).cuda()
+        rlt = torch.from_numpy(rl_np.astype(np.int32)).cuda()
+        dom_med, dom_us = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc_np.shape[0], J, out.data_ptr(),
+                                                 n_dev_iters)
+        loop_us = event_loop_us(step, args.steps, stream)
         tb = compact_bytes(p) if shape in (2, 3) else tally_bytes(p) + placement_tail_bytes(p)
     else:
         cap = torch.empty((len(p.classes) + 1, p.topology.n_leaves), dtype=torch.int32, device="cuda")
-        dom_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
-                                                        stream), args.steps, stream)
+        dom_med, dom_us = eng.tally_device_timed(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves, n_dev_iters)
+        loop_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
+                                                         stream), args.steps, stream)
         tb = tally_bytes(p)
     eng.check()
     achieved = tb / (dom_us * 1e-6) / 1e9
@@ -453,6 +581,14 @@ def main() -> None:
     lat2 = host_api_latency(eng, p, args.trials, synth.config2) if rank == 0 and args.trials > 0 else None
     cold2 = cold_recovery_latency(eng, p, args.cold_trials) if rank == 0 and args.cold_trials > 0 else None
     eng.service_stop()
+    idle_ms = float(os.environ.get("JSP_SERVICE_IDLE_MS", "50"))
+    if cold2 is not None and world == 1 and args.cpu_seconds > 0:
+        cold2["cpu"] = cpu_cold_recovery(p, max(10, args.cold_trials // 2), sorted({1, 2, cpu_threads()}), idle_ms)
+        cold2["cpu_note"] = ("oracle/cpu_fast.c after the same idle sleep: the same one-row patch written into its "
+                             "columns, then one placement; timed = patch + placement")
+        best = min(v["p99_us"] for v in cold2["cpu"].values())
+        cold2["gpu_p99_over_best_cpu_p99"] = {k: round(best / v["p99_us"], 3) for k, v in cold2.items()
+                                              if k.startswith("gap_")}
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
     cpu = None
@@ -508,6 +644,9 @@ def main() -> None:
             if cfg in (3, 5):
                 line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
                 line["host_api_cold_recovery"] = cold_recovery_latency(eng, pc, args.cold_trials // 2)
+                if line["host_api_cold_recovery"] is not None and world == 1 and args.cpu_seconds > 0:
+                    line["host_api_cold_recovery"]["cpu"] = cpu_cold_recovery(
+                        pc, max(10, args.cold_trials // 4), sorted({1, 2, T}), idle_ms)
                 # A/B: the same placements with the walk on the GPU (the fused resident kernel)
                 eng.set_service(True, device_walk=True)
                 ab_shape = SHAPES[settled_place(eng, pc.job_class).fused]
@@ -558,11 +697,33 @@ def main() -> None:
         tally_fn = lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream)  # noqa: E731
         for _ in range(10):  # untimed: the first launches into a new output buffer pay its first touch
             tally_fn()
-        tally_us = event_loop_us(tally_fn, tally_loop, stream)
+        # the kernel's own time: events on the dispatch packets of back-to-back
+        # launches on the engine stream (jsp_tally_device_timed) -- what the
+        # kernel trace reports; the event loop around 200 ctypes-issued
+        # launches (host submit in the gaps) is kept beside it
+        tally_med, tally_mean = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, tally_loop)
+        tally_loop_us = event_loop_us(tally_fn, tally_loop, stream)
+        tally_us = tally_mean
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
-        tally_cold = cold_us(tally_fn, 20, stream, scrub)
+        # cold: the library's read-only sweep of the 512 MiB buffer before each launch, dispatch events
+        tally_cold, tally_cold_mean = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, 20,
+                                                                   scrub.data_ptr(), scrub.numel() * 4)
         tally_cold_dirty = cold_us(tally_fn, 20, stream, scrub, dirty=True)
+        step_dev = None
+        if world == 1:  # the whole single-GPU step on the device (first dispatch -> last), warm and cold
+            rc4, rl4 = job_runs(p4.job_class)
+            rc4t = torch.from_numpy(rc4.astype(np.int32)).cuda()
+            rl4t = torch.from_numpy(rl4.astype(np.int32)).cuda()
+            a4t = torch.empty(p4.n_jobs, dtype=torch.int32, device="cuda")
+            sw = eng.place_device_timed(rc4t.data_ptr(), rl4t.data_ptr(), rc4.shape[0], p4.n_jobs, a4t.data_ptr(), 100)
+            sc = eng.place_device_timed(rc4t.data_ptr(), rl4t.data_ptr(), rc4.shape[0], p4.n_jobs, a4t.data_ptr(), 20,
+                                        scrub.data_ptr(), scrub.numel() * 4)
+            step_dev = {"warm_median_us": round(sw[0], 2), "warm_mean_us": round(sw[1], 2),
+                        "cold_median_us": round(sc[0], 2),
+                        "note": "device span of one three-launch step (first dispatch start -> last dispatch end, "
+                                "dispatch-packet events, engine stream)"}
+            del rc4t, rl4t, a4t
         copy_ceiling = None
         if world == 1:  # achievable streaming rate: a cold copy of the same byte count
             src = torch.empty(tb4 // 2 // 16 * 4, dtype=torch.int32, device="cuda").fill_(1)
@@ -596,20 +757,34 @@ def main() -> None:
                               "bit-exact with the engine", "legs": legs4}
         cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
                 "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
-                "placed": placed4, "tally_us": round(tally_us, 2),
+                "placed": placed4, "tally_us": round(tally_us, 2), "tally_median_us": round(tally_med, 2),
+                "tally_event_loop_us": round(tally_loop_us, 2),
+                "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
+                              "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
+                              "around 200 ctypes-issued launches (includes host submit gaps)",
                 "tally_gbs": round(tb4 / (tally_us * 1e-6) / 1e9, 1),
                 "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "tally_cold_us": round(tally_cold, 2),
                 "tally_cold_gbs": round(tb4 / (tally_cold * 1e-6) / 1e9, 1),
                 "tally_cold_frac": round(tb4 / (tally_cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                 "tally_cold_dirty_us": round(tally_cold_dirty, 2),
-                "cold_note": "cold: a 512 MiB read-only scrub before each launch (as tools/stream_ceiling.hip); "
-                             "cold_dirty: the scrub also writes it, so the launch's misses pay its write-backs",
+                "cold_note": "cold: the library's read-only sweep of a 512 MiB buffer before each of 20 launches, "
+                             "median of the dispatch-packet events; cold_dirty: torch writes the buffer before each "
+                             "launch (events around it), so the launch's misses pay its write-backs",
+                "step_device": step_dev,
                 "copy_ceiling_same_bytes": copy_ceiling,
-                "tally_traffic": pmc_traffic(("tally_wave_kernel", "tally_kernel"), 4) if world == 1 else None,
+                "tally_traffic": pmc_traffic(("tally_wave",), 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
                 "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
                 "allreduce_us": sp.allreduce_us(), "shards": world, "cpu_baseline": cpu4}
+        # the device-set engine inside the C ABI (what the Go manager's one
+        # process would drive, main.go:161-190): rank 0 opens every visible GPU
+        # (ids {0, 0} on a one-GPU box: two shards, on-device add), the others
+        # wait at a barrier
+        barrier(world)
+        if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
+            cfg4["device_set"] = device_set_leg(p4, sp.assign(), max(20, args.steps))
+        barrier(world)
 
     if rank == 0:
         line = {
@@ -636,12 +811,23 @@ def main() -> None:
                          "frac": round(achieved / HBM_PEAK_GBS, 5),
                          "traffic": traffic["bytes"] if traffic else None,
                          "traffic_source": traffic["source"] if traffic else None,
+                         "traffic_is_latest": traffic["latest"] if traffic else None,
                          "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
+                         "median_us": round(dom_med, 3), "event_loop_us": round(loop_us, 3),
                          "trace_median_us": tr_us, "trace_source": tr_src,
-                         "note": "latency-bound: one launch moving 0.43 MB; see DESIGN.md §8"},
+                         "note": "avg_us / median_us: events on the dispatch packets of back-to-back launches "
+                                 "(jsp_place_device_timed, the engine stream); event_loop_us: HIP events around "
+                                 "ctypes-issued launches. Latency-bound: one launch moving 0.43 MB; DESIGN.md §8"},
             "service": svc,
+            "rows_note": "the timed loop places the same snapshot repeatedly: the resident tiles keep their rows in "
+                         "LDS between requests (no row traffic); patched_step_us times one row patched before "
+                         "each call (rows reloaded from memory)",
+            "patched_step_us": patched,
             "p50_recovery_us": lat2["p50_us"] if lat2 else None,
             "p99_recovery_us": lat2["p99_us"] if lat2 else None,
+            "p99_recovery_leg": "warm: 1000 seeded trial snapshots, each uploaded untimed (the upload restarts the "
+                                "service and returns once it polls), then jsp_place on host wall; the realistic "
+                                "cold recovery is cold_recovery",
             "recovery_trials": lat2["n"] if lat2 else 0,
             "cold_recovery": cold2,
             "cpu_baseline": cpu,

@@ -64,7 +64,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 4
+#define JSP_ABI_VERSION 5
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -148,8 +148,9 @@ typedef struct jsp_timing {
     double svc_us;             /* summed in-kernel request time (first tile saw the request -> last tile
                                   done, 100 MHz device clock); accumulated while timing is on */
     uint64_t svc_fallbacks;    /* jsp_place calls the service could not answer (its grid does not fit the
-                                  CUs, it left, or a request failed on the device): answered by the launch
-                                  path instead; the service stays off until the next upload */
+                                  CUs, it left twice, or a request failed on the device): answered by the
+                                  launch path instead. When its grid cannot be co-resident the service stays
+                                  off until the next upload; otherwise the next call starts it again */
     double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
 } jsp_timing;
 
@@ -165,10 +166,13 @@ typedef struct jsp_timing {
  * assign[] goes back into pinned memory -- no launch per placement. It is started by the first such
  * jsp_place, stopped by every upload, jsp_engine_set_service/set_fused and
  * jsp_engine_destroy, and leaves by itself after JSP_SERVICE_IDLE_MS
- * (default 50 ms) without a request; jsp_place restarts it when needed.
+ * (default 50 ms) without a request; jsp_place restarts it when needed, and
+ * so does a jsp_snapshot_patch after a placement it answered (the deletions of
+ * a recovery patch the snapshot before the recreate places it).
  * While it runs, a device-wide synchronize (hipDeviceSynchronize,
  * torch.cuda.synchronize) waits for it to leave: call
- * jsp_engine_service_stop first. */
+ * jsp_engine_service_stop first (which also keeps patches from restarting it
+ * until the next jsp_place it answers). */
 #define JSP_SERVICE_OFF 0
 #define JSP_SERVICE_AUTO 1     /* default: the multi-class / multi-level shapes are answered by the split
                                   service -- resident tiles tally and hand back per-domain feasibility,
@@ -205,8 +209,13 @@ void jsp_engine_destroy(jsp_engine* e);
 int jsp_topology_upload(jsp_engine* e, const jsp_topology* topo);
 int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nodes);
 /* Overwrite n rows (ids in `rows`, local to this shard) of the resident
- * snapshot. delta columns are [W][n], [n], [R][n], [n]; structure (leaf
- * ranges) is unchanged. */
+ * snapshot. delta columns are [W][n], [n], [R][n], [n] (NULL: column
+ * unchanged); structure (leaf ranges) is unchanged. The call copies the delta
+ * and returns without waiting for the device: every later call sees the
+ * patched rows (launches are stream-ordered after it, service requests wait
+ * for its completion word). A patch is the first sign of a recovery, so while
+ * the resident service is armed (the last jsp_place was answered by it) a
+ * patch also (re)starts the service without waiting for it (ABI v5). */
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n,
                        const uint64_t* labels, const uint32_t* taints,
                        const uint32_t* free_res, const int32_t* excl_owner);
@@ -266,6 +275,20 @@ int jsp_engine_service_stop(jsp_engine* e);
  * scanned, 4 look-back done, 5 assign[] drained; 6-7 unused). Copies up to
  * cap/8 tiles; *n_tiles = how many (0 when no timed request is held). */
 int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles);
+/* Device time of `iters` back-to-back steps on the engine stream (the bench's
+ * kernel-time legs): each step carries a start event on its first dispatch and
+ * a stop event on its last (hipExtLaunchKernel: the dispatch packets' own
+ * timestamps, as a kernel trace reports them, with no host submit time between
+ * them). d_scrub (nullable): a device buffer larger than the caches, read
+ * (never written) before every step, so each step starts cold.
+ * out_us[0] = median, out_us[1] = mean per step, in microseconds.
+ * jsp_tally_device_timed: the tally of jsp_tally_device.
+ * jsp_place_device_timed: the whole placement of jsp_place_device. */
+int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+                           const void* d_scrub, size_t scrub_bytes, double* out_us);
+int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
+                           uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub,
+                           size_t scrub_bytes, double* out_us);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

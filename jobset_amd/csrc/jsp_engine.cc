@@ -40,7 +40,24 @@ int set_err(int code, const char* fmt, ...) {
                            __FILE__, __LINE__);                                              \
     } while (0)
 
-// Grow-only device buffer.
+// Buffers a grow-only buffer gave up while the resident service ran: hipFree
+// and hipHostFree wait for every kernel on the device, the resident service
+// included, which leaves only after JSP_SERVICE_IDLE_MS without a request --
+// a free while it runs stalls the caller for up to that long
+// (tools/block_probe.hip). They are freed once the service has stopped.
+struct Grave {
+    std::vector<void*> dev, host;
+    void flush() {
+        for (void* p : dev) (void)hipFree(p);
+        for (void* p : host) (void)hipHostFree(p);
+        dev.clear();
+        host.clear();
+    }
+    ~Grave() { flush(); }
+};
+
+// Grow-only device buffer. `g`: where the old buffer goes when it must grow
+// while a kernel that never ends by itself runs (nullptr: freed at once).
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -50,8 +67,13 @@ struct DevBuf {
         p = nullptr;
         bytes = 0;
     }
-    hipError_t reserve(size_t n) {
+    hipError_t reserve(size_t n, Grave* g = nullptr) {
         if (n <= bytes && p) return hipSuccess;
+        if (g && p) {
+            g->dev.push_back(p);
+            p = nullptr;
+            bytes = 0;
+        }
         release();
         hipError_t e = hipMalloc(&p, n ? n : 16);
         if (e == hipSuccess) bytes = n ? n : 16;
@@ -73,8 +95,13 @@ struct HostBuf {
         p = nullptr;
         bytes = 0;
     }
-    hipError_t reserve(size_t n) {
+    hipError_t reserve(size_t n, Grave* g = nullptr) {
         if (n <= bytes && p) return hipSuccess;
+        if (g && p) {
+            g->host.push_back(p);
+            p = nullptr;
+            bytes = 0;
+        }
         release();
         hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) bytes = n ? n : 16;
@@ -149,6 +176,14 @@ struct jsp_engine {
     HostBuf h_runs, h_assign, h_stats;  // zero-copy staging of the host placement path
     HostBuf h_done;                     // [n_blocks] completion words of the host placement path
     HostBuf h_err;                      // [1] error word: a failed launch writes its epoch (sticky)
+    // snapshot patches run asynchronously: the delta is staged in pinned
+    // memory the patch kernel reads in place, whose last workgroup writes
+    // patch_seq to h_patch_done (patch_wait)
+    HostBuf h_patch, h_patch_done;
+    DevBuf patch_ctr;                   // workgroups of every patch launch so far (device counter)
+    unsigned long long patch_target = 0;
+    uint32_t patch_seq = 0;
+    bool patch_pending = false;
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
     int fused_mode = JSP_FUSED_AUTO;
@@ -197,14 +232,19 @@ struct jsp_engine {
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
         std::chrono::steady_clock::time_point t_launch{};
-        bool broken = false;  // a start or a request failed on this geometry: the launch path answers until
-                              // the next upload (every upload clears it)
+        bool broken = false;  // the service cannot run on this geometry (its grid is not co-resident): the
+                              // launch path answers until the next upload (every upload clears it)
+        bool start_failed = false;  // the last start never saw its dispatcher poll (-> broken)
+        bool armed = false;   // the host API was answered by the service: a patch (re)starts it (svc_wake)
         std::chrono::steady_clock::time_point last{};
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
+    Grave grave;  // buffers replaced while the service ran: freed when it stops
 
     // timing
     bool timing = false;
+    std::vector<EvPair> tev;  // jsp_*_device_timed: one start/stop pair per step
+    DevBuf tmp_scrub;         // the scrub kernel's sink word
     std::vector<EvPair> ev;
     size_t ev_used = 0;
     jsp_timing acc{};
@@ -212,10 +252,11 @@ struct jsp_engine {
     ~jsp_engine() {
         if (multi) jspm::destroy(multi);
         (void)hipSetDevice(device);
-        for (auto& p : ev) {
-            if (p.a) (void)hipEventDestroy(p.a);
-            if (p.b) (void)hipEventDestroy(p.b);
-        }
+        for (auto* v : {&ev, &tev})
+            for (auto& p : *v) {
+                if (p.a) (void)hipEventDestroy(p.a);
+                if (p.b) (void)hipEventDestroy(p.b);
+            }
         if (ev_switch) (void)hipEventDestroy(ev_switch);
         if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
@@ -425,9 +466,13 @@ int check_engine(jsp_engine* e) {
     return JSP_OK;
 }
 
+// Where a buffer that must grow now leaves its old allocation: the grave
+// while the resident service runs (freed when it stops), else nowhere.
+Grave* grave(jsp_engine* e) { return e->svc.running ? &e->grave : nullptr; }
+
 template <class T>
-hipError_t upload(DevBuf& b, const T* src, size_t n, hipStream_t s) {
-    hipError_t err = b.reserve(n * sizeof(T));
+hipError_t upload(DevBuf& b, const T* src, size_t n, hipStream_t s, Grave* g = nullptr) {
+    hipError_t err = b.reserve(n * sizeof(T), g);
     if (err != hipSuccess || n == 0) return err;
     return hipMemcpyAsync(b.p, src, n * sizeof(T), hipMemcpyHostToDevice, s);
 }
@@ -509,7 +554,7 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
                              e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
     ev_end(p, s);
     p = ev_begin(e, 2, s);
-    if (e->recs.reserve(sizeof(jsp::AssignRec) * (size_t)std::max<uint32_t>(J, 1)) != hipSuccess)
+    if (e->recs.reserve(sizeof(jsp::AssignRec) * (size_t)std::max<uint32_t>(J, 1), grave(e)) != hipSuccess)
         return set_err(JSP_ENOMEM, "assignment records (%u jobs)", J);
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
                                e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
@@ -708,6 +753,7 @@ int svc_stop(jsp_engine* e) {
     v.running = false;
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
     HIP_TRY(hipStreamSynchronize(v.stream));
+    e->grave.flush();  // nothing resident any more: a free no longer waits
     return JSP_OK;
 }
 
@@ -793,7 +839,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.done = w;
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;
-    a.clk = e->timing && shape == 2 ? w + n_tiles + 3 : nullptr;
+    a.clk = e->timing && (shape == 2 || shape == 3) ? w + n_tiles + 3 : nullptr;
     a.spin_limit = e->spin_limit;
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
     a.ready = ready;
@@ -882,6 +928,7 @@ int svc_wait_ready(jsp_engine* e) {
             }
             if (std::chrono::steady_clock::now() - t_start > std::chrono::seconds(2)) {
                 (void)svc_stop(e);
+                v.start_failed = true;  // not co-resident on this GPU as launched: off until the next upload
                 return set_err(JSP_EHIP, "placement service did not start polling within 2 s");
             }
         }
@@ -942,6 +989,11 @@ int svc_settle(jsp_engine* e) {
         v.running = false;
         return JSP_OK;
     }
+    // The early answer had all J entries, so a tile past them that timed out
+    // in its look-back (it scattered nothing) did not touch it: acknowledge
+    // its error word here rather than blame the next request for it.
+    if (rc == JSP_OK && v.words.p)
+        v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
     return rc;
 }
 
@@ -998,10 +1050,50 @@ uint32_t next_seq(uint32_t q) {
     return s;
 }
 
+// Wait for the last snapshot patch's completion word (the rows are then in
+// memory for every later reader, the resident tiles' `sc1` loads included).
+int patch_wait(jsp_engine* e) {
+    if (!e->patch_pending) return JSP_OK;
+    const uint32_t* w = e->h_patch_done.as<uint32_t>();
+    for (uint64_t spins = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) != e->patch_seq; ++spins) {
+        if ((spins & 255) == 0) {
+            const hipError_t q = hipStreamQuery(e->stream);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == e->patch_seq) break;
+            e->patch_pending = false;
+            if (q == hipSuccess) return set_err(JSP_EHIP, "snapshot patch %u ended without its completion word", e->patch_seq);
+            return set_err(JSP_EHIP, "snapshot patch %u failed: %s", e->patch_seq, hipGetErrorString(q));
+        }
+    }
+    e->patch_pending = false;
+    return JSP_OK;
+}
+
+// A snapshot patch is the first sign of a recovery: the watch events of the
+// deleted Jobs' pods arrive while the reconciler deletes them in the
+// foreground, before it recreates and places them
+// (pkg/controllers/jobset_controller.go:553-576, 698-709). When the host API
+// has been answered by the resident service (armed), a patch (re)starts it
+// here without waiting: the GPU wakes from idle and the grid comes up while
+// the deletions finish, and the recreate's jsp_place finds it polling.
+// JSP_SVC_WAKE=0 turns this off (A/B).
+void svc_wake(jsp_engine* e) {
+    static const bool on = [] { const char* v = std::getenv("JSP_SVC_WAKE"); return !(v && v[0] == '0'); }();
+    auto& v = e->svc;
+    if (!on || !v.armed || !svc_ok(e)) return;
+    const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
+    if (v.running && since <= 0.5 * svc_idle_ms()) return;  // up, and not about to idle out
+    if (svc_stop(e) != JSP_OK || svc_start(e, 0, 0, false) != JSP_OK) {
+        (void)svc_stop(e);  // the next jsp_place starts it (or answers on the launch path)
+        g_err.clear();
+    }
+}
+
 // One placement through the service: J jobs of the engine's one class.
 int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
               int32_t* assign_out, uint32_t* placed) {
     auto& v = e->svc;
+    if (int rc = patch_wait(e)) return rc;  // the request's tiles must read the patched rows
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
@@ -1068,6 +1160,17 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         if (rc) return rc;
         break;
     }
+    if (v.clk && (v.shape == 2 || v.shape == 3) && v.nb > 0) {
+        // the request's device time: first tile saw it -> last tile drained
+        const uint32_t* clk = v.words.as<uint32_t>() + v.nb + 3;
+        const uint32_t ref = clk[0];
+        int32_t lo = 0, hi = 0;
+        for (uint32_t t = 0; t < v.nb; ++t) {
+            lo = std::min(lo, (int32_t)(clk[jsp::kSvcClkSlots * t] - ref));
+            hi = std::max(hi, (int32_t)(clk[jsp::kSvcClkSlots * t + 5] - ref));
+        }
+        e->acc.svc_us += (double)(hi - lo) / 100.0;
+    }
     if (v.shape == 3) {  // the tiles answered: the walk, into the caller's buffer
         const auto tw = std::chrono::steady_clock::now();
         *placed = e->walk.place(v.split.as<uint64_t>(), run_class, run_len, n_runs, assign_out);
@@ -1101,16 +1204,6 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     // the copy-out's share of the wait (jsp_timing.host_post_us on this path)
     e->acc.host_post_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count();
     e->acc.svc_calls += 1;
-    if (v.clk && v.shape == 2 && v.nb > 0) {
-        const uint32_t* clk = w + v.nb + 3;
-        const uint32_t ref = clk[0];
-        int32_t lo = 0, hi = 0;
-        for (uint32_t t = 0; t < v.nb; ++t) {
-            lo = std::min(lo, (int32_t)(clk[jsp::kSvcClkSlots * t] - ref));
-            hi = std::max(hi, (int32_t)(clk[jsp::kSvcClkSlots * t + 5] - ref));
-        }
-        e->acc.svc_us += (double)(hi - lo) / 100.0;
-    }
     return JSP_OK;
 }
 
@@ -1142,6 +1235,51 @@ int ready(jsp_engine* e, bool need_cls) {
     return JSP_OK;
 }
 
+// `iters` back-to-back device steps on the engine stream, each bracketed by
+// a start event on its first dispatch and a stop event on its last
+// (hipExtLaunchKernel: the dispatch packets' own timestamps, as a kernel
+// trace reports them -- no host submit time, no marker packets). With a
+// scrub buffer, a read-only sweep of it precedes every step (cold caches).
+// out_us[0] median, out_us[1] mean over the steps.
+template <class Step>
+int time_steps(jsp_engine* e, uint32_t iters, const void* d_scrub, size_t scrub_bytes, double* out_us, Step step) {
+    if (iters == 0 || iters > 4096) return set_err(JSP_EINVAL, "iters %u out of range [1,4096]", iters);
+    if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
+    if (scrub_bytes > 0 && !d_scrub) return set_err(JSP_EINVAL, "scrub buffer is NULL");
+    if (int rc = check_launch_error(e)) return rc;
+    hipStream_t s = e->stream;
+    if (int rc = use_engine_stream(e)) return rc;
+    while (e->tev.size() < iters) {
+        EvPair p;
+        HIP_TRY(hipEventCreate(&p.a));
+        HIP_TRY(hipEventCreate(&p.b));
+        e->tev.push_back(p);
+    }
+    if (scrub_bytes > 0) HIP_TRY(e->tmp_scrub.reserve(64, grave(e)));
+    int rc = JSP_OK;
+    for (uint32_t i = 0; i < iters && rc == JSP_OK; ++i) {
+        if (scrub_bytes > 0) HIP_TRY(jsp::launch_scrub(d_scrub, scrub_bytes, e->tmp_scrub.as<uint32_t>(), s));
+        jsp::set_launch_start(e->tev[i].a);
+        jsp::set_launch_stop(e->tev[i].b);
+        rc = step(s);
+        jsp::set_launch_start(nullptr);
+        jsp::set_launch_stop(nullptr);
+    }
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<double> us(iters);
+    double sum = 0.0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        float ms = 0.f;
+        HIP_TRY(hipEventElapsedTime(&ms, e->tev[i].a, e->tev[i].b));
+        us[i] = ms * 1e3;
+        sum += us[i];
+    }
+    std::sort(us.begin(), us.end());
+    out_us[0] = us[iters / 2];
+    out_us[1] = sum / iters;
+    return check_launch_error(e);
+}
 }  // namespace
 
 extern "C" {
@@ -1476,21 +1614,53 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
     if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
+    if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
-    HIP_TRY(upload(e->tmp_a, rows, n, s));
-    if (labels) HIP_TRY(upload(e->tmp_b, labels, (size_t)e->W * n, s));
-    if (taints) HIP_TRY(upload(e->tmp_c, taints, n, s));
-    if (free_res) HIP_TRY(upload(e->tmp_d, free_res, (size_t)e->R * n, s));
-    if (excl_owner) HIP_TRY(upload(e->tmp_e, excl_owner, n, s));
-    HIP_TRY(jsp::launch_patch(e->tmp_a.as<uint32_t>(), n, e->npad, e->W, e->R,
-                              labels ? e->tmp_b.as<uint64_t>() : nullptr, taints ? e->tmp_c.as<uint32_t>() : nullptr,
-                              free_res ? e->tmp_d.as<uint32_t>() : nullptr,
-                              excl_owner ? e->tmp_e.as<int32_t>() : nullptr, e->labels.as<uint64_t>(),
-                              e->taints.as<uint32_t>(), e->freer.as<uint32_t>(), e->excl.as<int32_t>(), s));
-    HIP_TRY(hipStreamSynchronize(s));
+    // the delta into pinned staging, which the patch kernel reads in place
+    const uint32_t W = e->W, R = e->R;
+    const size_t off_lab = ((size_t)n * 4 + 7) & ~size_t(7), off_t = off_lab + (size_t)W * n * 8,
+                 off_f = off_t + (size_t)n * 4, off_x = off_f + (size_t)R * n * 4, bytes = off_x + (size_t)n * 4;
+    HIP_TRY(e->h_patch.reserve(bytes, grave(e)));
+    char* hp = static_cast<char*>(e->h_patch.p);
+    std::memcpy(hp, rows, (size_t)n * 4);
+    if (labels) std::memcpy(hp + off_lab, labels, (size_t)W * n * 8);
+    if (taints) std::memcpy(hp + off_t, taints, (size_t)n * 4);
+    if (free_res) std::memcpy(hp + off_f, free_res, (size_t)R * n * 4);
+    if (excl_owner) std::memcpy(hp + off_x, excl_owner, (size_t)n * 4);
+    if (!e->patch_ctr.p) {
+        HIP_TRY(e->patch_ctr.reserve(64));
+        HIP_TRY(hipMemsetAsync(e->patch_ctr.p, 0, 64, s));
+        HIP_TRY(e->h_patch_done.reserve(64));
+        std::memset(e->h_patch_done.p, 0, 64);
+    }
+    jsp::PatchArgs a{};
+    a.rows = reinterpret_cast<const uint32_t*>(hp);
+    a.n = n;
+    a.npad = e->npad;
+    a.W = W;
+    a.R = R;
+    a.dlab = labels ? reinterpret_cast<const uint64_t*>(hp + off_lab) : nullptr;
+    a.dtaint = taints ? reinterpret_cast<const uint32_t*>(hp + off_t) : nullptr;
+    a.dfree = free_res ? reinterpret_cast<const uint32_t*>(hp + off_f) : nullptr;
+    a.dexcl = excl_owner ? reinterpret_cast<const int32_t*>(hp + off_x) : nullptr;
+    a.labels = e->labels.as<uint64_t>();
+    a.taints = e->taints.as<uint32_t>();
+    a.freer = e->freer.as<uint32_t>();
+    a.excl = e->excl.as<int32_t>();
+    a.counter = e->patch_ctr.as<unsigned long long>();
+    e->patch_target += (n + 255) / 256;
+    a.target = e->patch_target;
+    a.done = e->h_patch_done.as<uint32_t>();
+    e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
+    a.seq = e->patch_seq;
+    HIP_TRY(jsp::launch_patch(a, s));
+    e->patch_pending = true;
+    // No wait here: later work is ordered after the patch -- launches by the
+    // stream, service requests by the patch's completion word (patch_wait).
     svc_resume(e);
+    svc_wake(e);
     return JSP_OK;
 }
 
@@ -1596,6 +1766,35 @@ int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t*
     return rc;
 }
 
+
+int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+                           const void* d_scrub, size_t scrub_bytes, double* out_us) {
+    if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: time its shard engines");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
+    if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    return time_steps(e, iters, d_scrub, scrub_bytes, out_us,
+                      [&](hipStream_t s) { return tally_impl(e, d_cap, d_occ, ld, s); });
+}
+
+int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
+                           uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub, size_t scrub_bytes,
+                           double* out_us) {
+    if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: use jsp_place");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
+        return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
+    if (n_runs > 0 && (!d_run_class || !d_run_len)) return set_err(JSP_EINVAL, "run buffers are NULL");
+    if (n_jobs > 0 && !d_assign) return set_err(JSP_EINVAL, "assign buffer is NULL");
+    return time_steps(e, iters, d_scrub, scrub_bytes, out_us, [&](hipStream_t s) {
+        return place_impl(e, d_run_class, d_run_len, n_runs, n_jobs, d_assign, s);
+    });
+}
+
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (int rc = check_engine(e)) return rc;
@@ -1621,16 +1820,21 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             goto launch_path;
         }
         if (src != JSP_OK) {
-            // the service could not answer (not co-resident, left, or a request
-            // failed on the device): stop it, keep it off until the next upload,
-            // and answer this call on the launch path
+            // the service could not answer: stop it and answer this call on the
+            // launch path. A geometry failure (its grid cannot be co-resident,
+            // JSP_ERANGE, or its dispatcher never polled) keeps it off until
+            // the next upload; a transient one (it left twice, a look-back
+            // timed out) lets the next call start it again.
             (void)svc_stop(e);
-            e->svc.broken = true;
+            if (src == JSP_ERANGE || e->svc.start_failed) e->svc.broken = true;
+            e->svc.start_failed = false;
             e->acc.svc_fallbacks += 1;
+            g_err.clear();  // answered: the call succeeds (jsp_timing.svc_fallbacks counts it)
             goto launch_path;
         }
         {
         const auto t2 = std::chrono::steady_clock::now();
+        e->svc.armed = true;
         e->last_shape = e->svc.shape == 1 ? 4 : e->svc.shape == 3 ? 5 : 3;
         if (stats) {
             stats->jobs = J;
@@ -1654,8 +1858,8 @@ launch_path:
     // launch sequence, no DMA round trips. The single-launch shapes signal
     // completion through host words (wait_done); the others, and calls that
     // copy the tallies out, synchronise the stream.
-    HIP_TRY(e->h_runs.reserve((size_t)std::max<uint32_t>(n_runs, 1) * 8));
-    HIP_TRY(e->h_assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
+    HIP_TRY(e->h_runs.reserve((size_t)std::max<uint32_t>(n_runs, 1) * 8, grave(e)));
+    HIP_TRY(e->h_assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4, grave(e)));
     HIP_TRY(e->h_stats.reserve(16));
     uint32_t* h_rc = e->h_runs.as<uint32_t>();
     uint32_t* h_rl = h_rc + std::max<uint32_t>(n_runs, 1);
@@ -1700,12 +1904,17 @@ launch_path:
     e->acc.host_launch_us += us(t2 - t1).count();
     e->acc.host_wait_us += us(t3 - t2).count();
     e->acc.host_post_us += us(t4 - t3).count();
-    if (svc_after && svc_start(e, J, n_runs, false) != JSP_OK) {
-        // cannot start here (not co-resident on this GPU, ...): the launch path
-        // answers until the next upload, as when a request fails
-        (void)svc_stop(e);
-        e->svc.broken = true;
-        e->acc.svc_fallbacks += 1;
+    if (svc_after) {
+        const int sr = svc_start(e, J, n_runs, false);
+        if (sr != JSP_OK) {
+            // cannot start here: not co-resident on this GPU (the launch path
+            // answers until the next upload) or a transient failure (the next
+            // call tries again); this call's answer stands either way
+            (void)svc_stop(e);
+            if (sr == JSP_ERANGE) e->svc.broken = true;
+            e->acc.svc_fallbacks += 1;
+            g_err.clear();
+        }
     }
     return JSP_OK;
 }
@@ -1734,9 +1943,9 @@ int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const 
     if (!leader_rows || !levels || !domain_out) return set_err(JSP_EINVAL, "NULL buffer");
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
-    HIP_TRY(upload(e->tmp_a, leader_rows, n, s));
-    HIP_TRY(upload(e->tmp_b, levels, n, s));
-    HIP_TRY(e->tmp_c.reserve((size_t)n * 4));
+    HIP_TRY(upload(e->tmp_a, leader_rows, n, s, grave(e)));
+    HIP_TRY(upload(e->tmp_b, levels, n, s, grave(e)));
+    HIP_TRY(e->tmp_c.reserve((size_t)n * 4, grave(e)));
     HIP_TRY(jsp::launch_resolve(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), n, e->N, e->leaf_start.as<uint32_t>(),
                                 e->n_leaves, e->leaf_begin, e->topo, e->tmp_c.as<int32_t>(), s));
     HIP_TRY(hipMemcpyAsync(domain_out, e->tmp_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
@@ -1760,12 +1969,12 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
     if (M > 0 && !follower_domains) return set_err(JSP_EINVAL, "follower_domains is NULL");
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
-    HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s));
-    HIP_TRY(upload(e->tmp_b, levels, n_jobs, s));
-    HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s));
-    HIP_TRY(e->tmp_d.reserve((size_t)std::max<uint32_t>(M, 1) * 4));
+    HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s, grave(e)));
+    HIP_TRY(upload(e->tmp_b, levels, n_jobs, s, grave(e)));
+    HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s, grave(e)));
+    HIP_TRY(e->tmp_d.reserve((size_t)std::max<uint32_t>(M, 1) * 4, grave(e)));
     if (M > 0) HIP_TRY(hipMemcpyAsync(e->tmp_d.p, follower_domains, (size_t)M * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(e->tmp_e.reserve((size_t)n_jobs * 4));
+    HIP_TRY(e->tmp_e.reserve((size_t)n_jobs * 4, grave(e)));
     HIP_TRY(jsp::launch_audit(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), e->tmp_c.as<uint32_t>(),
                               e->tmp_d.as<int32_t>(), n_jobs, e->N, e->leaf_start.as<uint32_t>(), e->n_leaves,
                               e->leaf_begin, e->topo, e->tmp_e.as<uint32_t>(), s));
@@ -1794,6 +2003,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
         return set_err(JSP_EINVAL, "service mode %d", mode);
     if (mode != e->svc_mode) {  // the running service's shape may change
         e->svc.resume = false;
+        e->svc.armed = false;
         if (int rc = svc_stop(e)) return rc;
     }
     e->svc_mode = mode;
@@ -1820,6 +2030,7 @@ int jsp_engine_service_stop(jsp_engine* e) {
     if (e->multi) return JSP_OK;
     std::lock_guard<std::mutex> g(e->mu);
     e->svc.resume = false;
+    e->svc.armed = false;  // no patch restarts it until a jsp_place is answered by it again
     return svc_stop(e);
 }
 

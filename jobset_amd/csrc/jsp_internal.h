@@ -222,7 +222,10 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 // (the device-path calls' end-of-call marker); launch_stop_used() says whether
 // a launch did since the last set.
 void set_launch_stop(hipEvent_t ev);
+void set_launch_start(hipEvent_t ev);  // the next launch's start event (then cleared)
 bool launch_stop_used();
+// read-only cache scrub of `bytes` (instrumentation: cold-cache timings)
+hipError_t launch_scrub(const void* p, size_t bytes, uint32_t* sink, hipStream_t s);
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);
 // Wave-tile tally (tally_wave_kernel): tiles {first leaf, end leaf, first row,
 // end row} of up to kWaveTileLeaves whole leaves in <= kWaveTileRows - 4 rows
@@ -273,8 +276,27 @@ hipError_t launch_audit(const int32_t* leader_rows, const uint32_t* levels, cons
 // dst += src (n words, 16-B aligned buffers): shards of a device set on one device
 hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStream_t s);
 
-hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
-                        const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
-                        uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s);
+// A snapshot patch: n rows overwritten from a dense delta in pinned host
+// memory ([n] rows, [W][n] labels, [n] taints, [R][n] free, [n] excl; a null
+// column is left as is). done != nullptr: the last workgroup to finish writes
+// seq there (host-mapped) after every row store has drained; counter is a
+// device word every launch adds its grid to, target = its value after this one.
+struct PatchArgs {
+    const uint32_t* rows;
+    uint32_t n, npad, W, R;
+    const uint64_t* dlab;
+    const uint32_t* dtaint;
+    const uint32_t* dfree;
+    const int32_t* dexcl;
+    uint64_t* labels;
+    uint32_t* taints;
+    uint32_t* freer;
+    int32_t* excl;
+    unsigned long long* counter;
+    unsigned long long target;
+    uint32_t* done;
+    uint32_t seq;
+};
+hipError_t launch_patch(const PatchArgs& a, hipStream_t s);
 
 }  // namespace jsp

@@ -201,9 +201,42 @@ constexpr uint32_t kSvcStaggerTicks = 50;  // 100 MHz ticks between the dispatch
 // stores; nothing waits on them). Slots: 0 request seen, 1 request broadcast
 // to the workgroup, 2 tallied, 3 feasible count scanned, 4 look-back done,
 // 5 assign[] drained, 6 row pass done, 7 leaf pass done.
-__device__ __forceinline__ void svc_stamp(uint32_t* clk, int slot) {
-    if (clk && threadIdx.x == 0)
-        __hip_atomic_store(clk + slot, (uint32_t)wall_clock64(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// The stamps are kept in LDS (s_clk, static) and go out with the request's
+// done word (signal_host_clk): a system-scope store in the request path would
+// put a host-link round trip into the next wait on vmcnt (the row pass's
+// register waits), which is what the round-3 stamps measured as the row pass.
+__device__ __forceinline__ void svc_stamp(JSP_LDS uint32_t* clk, int slot) {
+#ifdef JSP_AB_CLKFREQ
+    // A/B build: slots 6 and 7 carry the shader clock at slots 1 and 2 (the
+    // effective clock of the row and leaf passes), not the real-time stamps
+    if (clk && threadIdx.x == 0) {
+        if (slot == 1) clk[6] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (slot == 2) clk[7] = (uint32_t)__builtin_amdgcn_s_memtime();
+        if (slot != 6 && slot != 7) clk[slot] = (uint32_t)wall_clock64();
+    }
+#else
+    if (clk && threadIdx.x == 0) clk[slot] = (uint32_t)wall_clock64();
+#endif
+}
+
+// signal_host with the request's stamps: every wave's stores drained, then
+// lane 0 takes stamp 5 (drained), writes the tile's stamps to the host and,
+// once they have landed, the done word -- the host reads the stamps after it.
+__device__ __forceinline__ void signal_host_clk(uint32_t* word, uint32_t value, JSP_LDS uint32_t* s_clk,
+                                                uint32_t* clk_out) {
+    if (s_clk == nullptr || clk_out == nullptr) {
+        signal_host(word, value, false);
+        return;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        s_clk[5] = (uint32_t)wall_clock64();
+        for (int i = 0; i < (int)kSvcClkSlots; ++i)
+            __hip_atomic_store(clk_out + i, s_clk[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(word, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ----------------------------------------------------------------- A8 tally (one workgroup)
@@ -423,7 +456,7 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 // copied into it.
 template <int W, int R, bool STAGED = false, bool SC1 = STAGED>
 __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds,
-                                            uint4 bt_staged = make_uint4(0, 0, 0, 0), uint32_t* clk = nullptr,
+                                            uint4 bt_staged = make_uint4(0, 0, 0, 0), JSP_LDS uint32_t* clk = nullptr,
                                             JSP_LDS u32x4* row_cache = nullptr, bool use_cache = false) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
@@ -2477,7 +2510,7 @@ template <int W, int R, bool STAGED = false>
 __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
-                                             uint32_t* s_x, uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
+                                             uint32_t* s_x, JSP_LDS uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
                                              bool use_cache = false, uint32_t tag = 0) {
     unsigned long long* assign64 = reinterpret_cast<unsigned long long*>(assign);
     const unsigned long long tag_hi = (unsigned long long)tag << 32;
@@ -2663,6 +2696,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         return;
     }
     uint32_t seq = v.seq0;
+    // this request's phase stamps (timing on). One word in: the array sits at
+    // LDS address 0, which compares equal to a null LDS pointer
+    __shared__ uint32_t s_clk[kSvcClkSlots + 1];
+    JSP_LDS uint32_t* clk = v.clk ? lds_ptr(s_clk + 1) : nullptr;
+    uint32_t* clk_out = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
     // the tile's constants, staged once: geometry, class record, leaf starts
     const uint4 bt = a.blk[tile];
     // the tile's rows stay in LDS between requests (v.row_cache_words != 0:
@@ -2700,9 +2738,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (next != 0 && v.clk)
-                __hip_atomic_store(v.clk + kSvcClkSlots * tile, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            if (next != 0) svc_stamp(clk, 0);
             s_x[16] = next;
             s_x[17] = J;
         }
@@ -2711,18 +2747,12 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         if (next == 0) return;
         const uint32_t J = Jw & 0x7FFFFFFFu;
         const bool use_cache = cached && (Jw >> 31) == 0u;
-        uint32_t* clk = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
         compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
                                  v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next);
         cached = row_cache != nullptr;
-        if (clk) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            svc_stamp(clk, 5);
-        }
-        signal_host(v.done + tile, next, false);
+        signal_host_clk(v.done + tile, next, clk, clk_out);
         // The host may patch the snapshot before its next request (another
         // launch): drop this CU's L1 lines now, off the request path -- no
         // snapshot load happens until the next request, which the host posts
@@ -2893,6 +2923,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     // previous request)
     JSP_LDS u32x4* row_cache = v.row_cache_words ? lds_ptr(reinterpret_cast<u32x4*>(lds + v.row_cache_words)) : nullptr;
     bool cached = false;
+    // this request's phase stamps (timing on). One word in: the array sits at
+    // LDS address 0, which compares equal to a null LDS pointer
+    __shared__ uint32_t s_clk[kSvcClkSlots + 1];
+    JSP_LDS uint32_t* clk = v.clk ? lds_ptr(s_clk + 1) : nullptr;
+    uint32_t* clk_out = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
     while (true) {
         if (threadIdx.x == 0) {
             uint32_t next = 0, dirty = 0;  // next 0: leave
@@ -2909,6 +2944,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
                 __builtin_amdgcn_s_sleep(1);
             }
+            if (next != 0) svc_stamp(clk, 0);
             s_x[0] = next;
             s_x[1] = dirty;
         }
@@ -2916,10 +2952,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         const uint32_t next = s_x[0];
         if (next == 0) return;
         const bool use_cache = cached && s_x[1] == 0u;
-        tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, row_cache, use_cache);
+        svc_stamp(clk, 1);
+        tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), clk, row_cache, use_cache);
         cached = row_cache != nullptr;
+        svc_stamp(clk, 2);
         split_emit(ag, sp, bt, out, lds, s_x);
-        signal_host(v.done + tile, next, false);
+        svc_stamp(clk, 4);
+        signal_host_clk(v.done + tile, next, clk, clk_out);
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -2977,20 +3016,37 @@ __global__ void audit_kernel(const int32_t* __restrict__ leader_rows, const uint
 
 // ----------------------------------------------------------------- snapshot patch
 // Overwrite n rows of the resident columns from a dense delta (watch events).
-__global__ void patch_kernel(const uint32_t* __restrict__ rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
-                             const uint64_t* __restrict__ dlab, const uint32_t* __restrict__ dtaint,
-                             const uint32_t* __restrict__ dfree, const int32_t* __restrict__ dexcl,
-                             uint64_t* __restrict__ labels, uint32_t* __restrict__ taints,
-                             uint32_t* __restrict__ freer, int32_t* __restrict__ excl) {
+// The delta is read straight from pinned host memory (no copy launch), the
+// rows are written through to memory (agent-scope `sc1` stores: the resident
+// service's tiles re-read patched rows with `sc1` loads on any XCD), and the
+// workgroup whose arrival completes the launch's count publishes `seq` to a
+// host-mapped word once every workgroup's stores have drained
+// (MI355X_MICROARCH.md hand-off table, first row: each workgroup adds after
+// its own vmcnt wait, the last adder signals). The host orders its next
+// service request after that word instead of synchronising the stream.
+__global__ __launch_bounds__(256) void patch_kernel(PatchArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t row = rows[i];
-    if (dlab)
-        for (uint32_t w = 0; w < W; ++w) labels[(size_t)w * npad + row] = dlab[(size_t)w * n + i];
-    if (dtaint) taints[row] = dtaint[i];
-    if (dfree)
-        for (uint32_t r = 0; r < R; ++r) freer[(size_t)r * npad + row] = dfree[(size_t)r * n + i];
-    if (dexcl) excl[row] = dexcl[i];
+    if (i < a.n) {
+        const uint32_t row = a.rows[i];
+        if (a.dlab)
+            for (uint32_t w = 0; w < a.W; ++w)
+                __hip_atomic_store(a.labels + (size_t)w * a.npad + row, a.dlab[(size_t)w * a.n + i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (a.dtaint) __hip_atomic_store(a.taints + row, a.dtaint[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a.dfree)
+            for (uint32_t r = 0; r < a.R; ++r)
+                __hip_atomic_store(a.freer + (size_t)r * a.npad + row, a.dfree[(size_t)r * a.n + i], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (a.dexcl) __hip_atomic_store(a.excl + row, a.dexcl[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (a.done == nullptr) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old =
+            __hip_atomic_fetch_add(a.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1 == a.target) __hip_atomic_store(a.done, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // ----------------------------------------------------------------- shard tally sum
@@ -3009,6 +3065,19 @@ __global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst
         dst[i] += src[i];
 }
 
+// ----------------------------------------------------------------- cache scrub (instrumentation)
+// Reads n16 16-byte words (a buffer larger than the Infinity Cache), so the
+// next launch finds its bytes in HBM only; nothing is dirtied. The sum goes
+// to sink[0] only when it equals a value it never takes (keeps the loads).
+__global__ __launch_bounds__(256) void scrub_kernel(const uint4* __restrict__ p, size_t n16, uint32_t* sink) {
+    uint32_t acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+        const uint4 v = p[i];
+        acc += v.x ^ v.y ^ v.z ^ v.w;
+    }
+    if (acc == 0x9E3779B9u && sink) sink[0] = acc;
+}
+
 // ----------------------------------------------------------------- launchers
 // Every launch goes through jsp_launch. While a device-path call on a caller's
 // stream is being enqueued, the engine names an event (set_launch_stop): each
@@ -3016,20 +3085,26 @@ __global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst
 // completes with the call's last kernel -- the kernel's own completion signal,
 // with no marker packet behind it on the caller's stream (an hipEventRecord
 // after each call cost 2-3 us of GPU time per call, profiles/r03).
+// set_launch_start names a start event the NEXT launch carries (then
+// cleared): with a stop event it brackets the dispatches themselves, as a
+// kernel trace does (jsp_tally_device_timed).
 namespace {
 thread_local hipEvent_t t_stop = nullptr;
+thread_local hipEvent_t t_start = nullptr;
 thread_local bool t_stop_used = false;
 }  // namespace
 void set_launch_stop(hipEvent_t ev) {
     t_stop = ev;
     t_stop_used = false;
 }
+void set_launch_start(hipEvent_t ev) { t_start = ev; }
 bool launch_stop_used() { return t_stop_used; }
 
 template <typename F, typename... Args>
 static inline void jsp_launch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t s,
                               Args... args) {
-    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, nullptr, t_stop, 0u, args...);
+    hipExtLaunchKernelGGL(kernel, grid, block, lds, s, t_start, t_stop, 0u, args...);
+    t_start = nullptr;
     if (t_stop) t_stop_used = true;
 }
 
@@ -3295,12 +3370,15 @@ hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStrea
     return hipGetLastError();
 }
 
-hipError_t launch_patch(const uint32_t* rows, uint32_t n, uint32_t npad, uint32_t W, uint32_t R,
-                        const uint64_t* dlab, const uint32_t* dtaint, const uint32_t* dfree, const int32_t* dexcl,
-                        uint64_t* labels, uint32_t* taints, uint32_t* freer, int32_t* excl, hipStream_t s) {
-    if (n == 0) return hipSuccess;
-    jsp_launch(patch_kernel, dim3((n + 255) / 256), dim3(256), 0, s, rows, n, npad, W, R, dlab, dtaint,
-                       dfree, dexcl, labels, taints, freer, excl);
+hipError_t launch_scrub(const void* p, size_t bytes, uint32_t* sink, hipStream_t s) {
+    if (bytes < 16) return hipSuccess;
+    jsp_launch(scrub_kernel, dim3(4096), dim3(256), 0, s, static_cast<const uint4*>(p), bytes / 16, sink);
+    return hipGetLastError();
+}
+
+hipError_t launch_patch(const PatchArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+    jsp_launch(patch_kernel, dim3((a.n + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -39,14 +40,27 @@ struct Rccl {
     ErrStrFn err = nullptr;
 };
 
+// JSP_RCCL_LIB names the library to load instead of the default search (a
+// test hook: a name that does not exist stands in for a host without RCCL).
 int load_rccl(Rccl* r) {
     if (r->so) return JSP_OK;
-    for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
-        r->so = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
-        if (r->so) break;
+    const char* forced = std::getenv("JSP_RCCL_LIB");
+    const char* err = nullptr;
+    if (forced && forced[0]) {
+        r->so = dlopen(forced, RTLD_NOW | RTLD_GLOBAL);
+        if (!r->so) err = dlerror();
+    } else {
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            r->so = dlopen(name, RTLD_NOW | RTLD_GLOBAL);
+            if (r->so) break;
+            err = dlerror();
+        }
     }
-    if (!r->so) return jsp_internal_set_err(JSP_EHIP, "device set spans several GPUs but librccl.so.1 cannot be loaded: %s",
-                                            dlerror());
+    if (!r->so)
+        return jsp_internal_set_err(JSP_EHIP,
+                                    "device set spans several GPUs but RCCL (%s) cannot be loaded: %s; a device set "
+                                    "over one GPU (repeated ids) needs no RCCL",
+                                    forced && forced[0] ? forced : "librccl.so.1", err ? err : "?");
     r->init_all = (InitAllFn)dlsym(r->so, "ncclCommInitAll");
     r->all_reduce = (AllReduceFn)dlsym(r->so, "ncclAllReduce");
     r->group_start = (GroupFn)dlsym(r->so, "ncclGroupStart");
@@ -233,6 +247,12 @@ int snapshot_upload(Multi* m, const jsp_nodes* nd) {
         return jsp_internal_set_err(JSP_EINVAL, "a node column is NULL");
     const uint32_t* ls = nd->leaf_start;
     if (ls[0] != 0 || ls[m->L] != N) return jsp_internal_set_err(JSP_EINVAL, "leaf_start must run 0..%u", N);
+    // the cuts and the column slices below index the caller's columns by
+    // leaf_start: validate it whole first (as jsp_snapshot_upload does for a
+    // single engine), so no slice can wrap or read past a column
+    for (uint32_t l = 0; l < m->L; ++l)
+        if (ls[l] > ls[l + 1] || ls[l + 1] > N)
+            return jsp_internal_set_err(JSP_EINVAL, "leaf_start not monotone at %u", l);
     const uint32_t D0 = (uint32_t)m->fl0.size() - 1;
     std::vector<uint32_t> cuts{0};
     for (int r = 1; r < m->n; ++r) {

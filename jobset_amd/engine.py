@@ -194,6 +194,25 @@ class Engine:
         call.keep = (rc, rl, assign)
         return call
 
+    def host_patcher(self, rows: np.ndarray, labels: Optional[np.ndarray] = None,
+                     taints: Optional[np.ndarray] = None, free: Optional[np.ndarray] = None,
+                     excl: Optional[np.ndarray] = None):
+        """A pre-bound jsp_snapshot_patch for one delta (arrays converted once):
+        what a watch-event handler that patches the same rows repeatedly binds
+        (the bench's recovery legs). Returns a callable."""
+        rows = np.ascontiguousarray(rows, dtype=np.uint32)
+        arrs = [None if a is None else np.ascontiguousarray(a, dtype=dt)
+                for a, dt in ((labels, np.uint64), (taints, np.uint32), (free, np.uint32), (excl, np.int32))]
+        fn = self._lib.jsp_snapshot_patch
+        args = (self._h, rows.ctypes.data, rows.shape[0], *[_p(a) for a in arrs])
+
+        def call() -> None:
+            r = fn(*args)
+            if r:
+                check(r)
+        call.keep = (rows, arrs)
+        return call
+
     def shards(self) -> Tuple[int, int]:
         """(shards, distinct devices) of this engine (1, 1 unless a device set)."""
         a, b = ctypes.c_int(0), ctypes.c_int(0)
@@ -215,6 +234,26 @@ class Engine:
                       n_jobs: int, d_assign: int, stream: Optional[int] = None) -> None:
         check(self._lib.jsp_assign_device(self._h, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, n_jobs,
                                           d_assign, stream))
+
+    def tally_device_timed(self, d_cap: int, d_occ: int, ld: int, iters: int, scrub: int = 0,
+                           scrub_bytes: int = 0) -> Tuple[float, float]:
+        """(median, mean) device µs of `iters` back-to-back tallies on the
+        engine stream, timed by events on the dispatches themselves
+        (jsp_tally_device_timed); with a scrub buffer, each one cold."""
+        out = np.zeros(2, dtype=np.float64)
+        check(self._lib.jsp_tally_device_timed(self._h, d_cap, d_occ, ld, iters, scrub or None, scrub_bytes,
+                                               _p(out)))
+        return float(out[0]), float(out[1])
+
+    def place_device_timed(self, d_run_class: int, d_run_len: int, n_runs: int, n_jobs: int, d_assign: int,
+                           iters: int, scrub: int = 0, scrub_bytes: int = 0) -> Tuple[float, float]:
+        """(median, mean) device µs of `iters` back-to-back device-path
+        placements (first dispatch start -> last dispatch end each;
+        jsp_place_device_timed); with a scrub buffer, each one cold."""
+        out = np.zeros(2, dtype=np.float64)
+        check(self._lib.jsp_place_device_timed(self._h, d_run_class, d_run_len, n_runs, n_jobs, d_assign, iters,
+                                               scrub or None, scrub_bytes, _p(out)))
+        return float(out[0]), float(out[1])
 
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))

@@ -128,6 +128,7 @@ class PackedProblem:
         for k, a in arrs.items():
             self.keep.append(a)
             setattr(st, k, _ptr(a))
+        self.arrs = arrs  # the evaluator reads these in place: writing one patches its snapshot
         st.n_nodes = nodes.n_nodes
         st.W = nodes.n_label_words
         st.R = nodes.n_res
@@ -221,6 +222,11 @@ class FastCPU:
         if self.lib.jspf_prepare(self.h, ctypes.byref(self.pk.st)) != 0:
             raise MemoryError("jspf_prepare failed")
         self.assign = np.empty(max(self.pk.J, 1), dtype=np.int32)
+
+    def patch_taints(self, rows: np.ndarray, taints: np.ndarray) -> None:
+        """A watch event's row patch, as the engine gets it through
+        jsp_snapshot_patch: the evaluator reads the packed columns in place."""
+        self.pk.arrs["taints"][rows] = taints
 
     def run(self, want_tally: bool = False):
         pk = self.pk

@@ -35,7 +35,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     lib = native.lib()
-    assert lib.jsp_abi_version() == 4
+    assert lib.jsp_abi_version() == 5
     # layouts the Go cgo wrapper relies on
     assert ctypes.sizeof(native.JspJobClass) == 8 * 4 * 2 + 4 * 3 + 4 * 4 + 4  # 100 B + 4 pad
     assert ctypes.sizeof(native.JspTopology) == 4 + 4 * 4 + 4 + 8 * 4

@@ -708,3 +708,39 @@ def test_caller_stream_destroyed_between_calls(engine):
         engine.check()
         np.testing.assert_array_equal(out2.cpu().numpy(), a)
         engine.sync()
+
+
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_device_timed_entry_points(engine, cfg):
+    """jsp_tally_device_timed / jsp_place_device_timed (the bench's kernel-time
+    legs): back-to-back steps timed by events on their own dispatches, warm
+    and behind the library's cache scrub; the buffers they leave hold the
+    oracle's answer."""
+    import torch
+    from jobset_amd.snapshot import job_runs
+    p = synth.CONFIGS[cfg]()
+    engine.set_fused(True)
+    engine.load(p)
+    C, L = len(p.classes), p.topology.n_leaves
+    a, cap, occ = O.place_c(p)
+    t = torch.zeros((C + 1, L), dtype=torch.int32, device="cuda")
+    med, mean = engine.tally_device_timed(t.data_ptr(), t[-1].data_ptr(), L, 50)
+    assert 0.0 < med <= 2000.0 and 0.0 < mean <= 2000.0
+    scrub = torch.zeros(64 << 20, dtype=torch.int32, device="cuda")  # 256 MiB
+    cmed, _ = engine.tally_device_timed(t.data_ptr(), t[-1].data_ptr(), L, 5, scrub.data_ptr(), scrub.numel() * 4)
+    assert cmed > 0.0
+    engine.check()
+    got = t.cpu().numpy().view(np.uint32)
+    np.testing.assert_array_equal(got[:C], cap)
+    np.testing.assert_array_equal(got[C], occ)
+    rc, rl = job_runs(p.job_class)
+    rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+    rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+    out = torch.full((p.n_jobs,), -7, dtype=torch.int32, device="cuda")
+    pmed, pmean = engine.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 20)
+    assert 0.0 < pmed and 0.0 < pmean
+    engine.check()
+    np.testing.assert_array_equal(out.cpu().numpy(), a)
+    with pytest.raises(JspError) as ei:
+        engine.tally_device_timed(t.data_ptr(), t[-1].data_ptr(), L, 0)
+    assert ei.value.code == JSP_EINVAL

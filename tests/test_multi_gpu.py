@@ -111,3 +111,80 @@ def test_device_set_sizes(ids):
         assert e.shards() == (len(ids), 1)
     finally:
         e.close()
+
+
+def test_device_set_rejects_bad_leaf_start():
+    """leaf_start is validated whole before any shard slices the caller's
+    columns: non-monotone, or an interior offset past N, is
+    JSP_EINVAL -- never a wrapped slice or a read past a column."""
+    import dataclasses
+
+    from jobset_amd.native import JSP_EINVAL, JspError
+    p = synth.config2()
+    e = Engine(devices=[0, 0])
+    try:
+        e.upload_topology(p.topology)
+        for bad in ("swap", "past_n"):
+            ls = p.nodes.leaf_start.copy()
+            if bad == "swap":
+                ls[5], ls[6] = ls[6], ls[5]
+            else:
+                ls[500] = p.nodes.n_nodes + 1000
+            with pytest.raises(JspError) as ei:
+                e.upload_snapshot(dataclasses.replace(p.nodes, leaf_start=ls))
+            assert ei.value.code == JSP_EINVAL
+        e.load(p)  # a good snapshot still loads and places
+        np.testing.assert_array_equal(e.place(p.job_class).assign, O.place_c(p)[0])
+    finally:
+        e.close()
+
+
+def test_device_set_on_one_device_needs_no_rccl(monkeypatch):
+    """Repeated ids combine on the device: with the RCCL loader pointed at a
+    library that does not exist, the set still builds and places."""
+    monkeypatch.setenv("JSP_RCCL_LIB", "/nonexistent/librccl_missing.so")
+    p = synth.config5()
+    e = Engine(devices=[0, 0])
+    try:
+        e.load(p)
+        got = e.place(p.job_class)
+        assert got.fused == 6 and e.shards() == (2, 1)
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    finally:
+        e.close()
+
+
+def _gpus():
+    from jobset_amd import native
+    return native.device_count()
+
+
+@pytest.mark.skipif(_gpus() < 2, reason="needs two GPUs (the RCCL path between distinct devices)")
+def test_device_set_distinct_devices_without_rccl_fails_cleanly(monkeypatch):
+    from jobset_amd.native import JSP_EHIP, JspError
+    monkeypatch.setenv("JSP_RCCL_LIB", "/nonexistent/librccl_missing.so")
+    with pytest.raises(JspError) as ei:
+        Engine(devices=[0, 1])
+    assert ei.value.code == JSP_EHIP and "RCCL" in str(ei.value)
+
+
+@pytest.mark.skipif(_gpus() < 2, reason="needs two GPUs (the RCCL path between distinct devices)")
+@pytest.mark.parametrize("cfg", [2, 4, 5])
+def test_device_set_distinct_devices(cfg):
+    """The RCCL all-reduce between distinct devices (ncclCommInitAll in this
+    process), shards on every visible GPU: bit-exact with the oracle."""
+    n = min(_gpus(), 8)
+    p = synth.CONFIGS[cfg]()
+    a, cap, occ = O.place_c(p)
+    e = Engine(devices=list(range(n)))
+    try:
+        assert e.shards() == (n, n)
+        e.load(p)
+        for _ in range(2):
+            got = e.place(p.job_class, want_tally=True)
+            assert got.fused == 6
+            np.testing.assert_array_equal(got.assign, a)
+            np.testing.assert_array_equal(got.cap, cap)
+            np.testing.assert_array_equal(got.occ, occ)
+    finally:
+        e.close()

@@ -208,12 +208,9 @@ def test_service_after_device_path_and_patch(svc_engine):
         free = rng.integers(0, 4000, size=(p.nodes.free.shape[0], 200)).astype(np.uint32)
         svc_engine.patch_rows(rows, free=free)
         p.nodes.free[:, rows] = free
-        # a patch leaves the service running; a first-use stall on this box
-        # (> JSP_SERVICE_IDLE_MS / 2 since the last request) restarts it and
-        # the launch path answers once: both answers are checked
+        # the patch leaves the service running (its staging grows without a
+        # free while the service is resident: no stall), so the service answers
         got = svc_engine.place(p.job_class)
-        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
-        got = warm(svc_engine, p.job_class) if got.fused != 3 else got
         assert got.fused == 3
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
     svc_engine.check()
@@ -313,7 +310,7 @@ def test_fused_service_patch_and_device_path(svc_engine, device_walk):
     warm(svc_engine, p.job_class)
     for step in range(20):
         got = svc_engine.place(p.job_class)
-        assert got.fused in (walk_shape(device_walk), 1)  # 1: a cold start after a long host gap
+        assert got.fused == walk_shape(device_walk)
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
         svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
                                 side.cuda_stream)
@@ -410,3 +407,91 @@ def test_service_that_cannot_fit_falls_back(monkeypatch):
         assert got.fused == 3 and e.timing(reset=True).svc_fallbacks == 0
     finally:
         e.close()
+
+
+def test_patch_wakes_the_service(svc_engine):
+    """A patch after the service idle-exited starts it again without waiting
+    (the deletions of a recovery patch the snapshot before the recreate
+    places it): the next place finds it up and starts nothing. After an
+    explicit stop a patch starts nothing until a place is answered by it."""
+    p = synth.config2()
+    svc_engine.load(p)
+    a = O.place_c(p)[0]
+    assert warm(svc_engine, p.job_class).fused == 3
+    row = np.array([123], dtype=np.uint32)
+    patch = svc_engine.host_patcher(row, taints=p.nodes.taints[row])
+    for gap in (0.0, 0.002, 0.02):
+        svc_engine.timing(reset=True)
+        time.sleep(0.08)  # past JSP_SERVICE_IDLE_MS: the service has left
+        patch()
+        assert svc_engine.timing(reset=False).svc_starts == 1  # woken by the patch
+        time.sleep(gap)
+        got = svc_engine.place(p.job_class)
+        t = svc_engine.timing(reset=True)
+        assert got.fused == 3 and t.svc_starts == 1 and t.svc_calls == 1
+        np.testing.assert_array_equal(got.assign, a)
+    svc_engine.service_stop()  # disarmed
+    svc_engine.timing(reset=True)
+    patch()
+    assert svc_engine.timing(reset=False).svc_starts == 0
+    got = svc_engine.place(p.job_class)
+    assert got.fused == 3 and svc_engine.timing(reset=True).svc_starts == 1
+    np.testing.assert_array_equal(got.assign, a)
+
+
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 5000, 14999])
+def test_async_patch_sizes_then_place(svc_engine, n):
+    """The patch kernel reads the delta from pinned memory and its last
+    workgroup publishes the completion word the next service request waits
+    for: every column, 1 to ~all rows (one to 59 workgroups), placed at once
+    behind the patch -- bit-exact, answered by the service, and no call
+    stalls on a buffer that grew while the service was resident."""
+    p = synth.config2()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused == 3
+    rng = np.random.default_rng(n)
+    for _ in range(3):
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=n, replace=False)).astype(np.uint32)
+        W, R = p.nodes.labels.shape[0], p.nodes.free.shape[0]
+        lab = p.nodes.labels[:, rows].copy()
+        lab ^= (rng.integers(0, 2, size=lab.shape).astype(np.uint64) << np.uint64(rng.integers(0, 3)))
+        taints = rng.integers(0, 2, size=n).astype(np.uint32)
+        free = rng.integers(0, 200_000, size=(R, n)).astype(np.uint32)
+        excl = np.where(rng.random(n) < 0.01, 7, -1).astype(np.int32)
+        t0 = time.perf_counter()
+        svc_engine.patch_rows(rows, labels=lab, taints=taints, free=free, excl=excl)
+        got = svc_engine.place(p.job_class)
+        wall = time.perf_counter() - t0
+        p.nodes.labels[:, rows] = lab
+        p.nodes.taints[rows] = taints
+        p.nodes.free[:, rows] = free
+        p.nodes.excl[rows] = excl
+        assert got.fused == 3
+        assert wall < 0.02, f"patch + place took {wall * 1e3:.1f} ms"
+        a, cap, occ = O.place_c(p)
+        np.testing.assert_array_equal(got.assign, a)
+    full = svc_engine.place(p.job_class, want_tally=True)  # launch path, tallies out: the patched columns
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(full.cap, cap)
+    np.testing.assert_array_equal(full.occ, occ)
+
+
+def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
+    """Batched follower resolution / audits whose scratch outgrows its
+    buffers while the service is resident: the old buffers wait for the
+    service to stop instead of a free that waits for the service to leave."""
+    p = synth.config2()
+    svc_engine.load(p)
+    a = warm(svc_engine, p.job_class).assign
+    svc_engine.timing(reset=True)
+    for n in (10, 1000, 20_000, 200_000):
+        rows = (np.arange(n, dtype=np.int64) * 7919 % p.nodes.n_nodes).astype(np.int32)
+        lv = np.zeros(n, dtype=np.uint32)
+        t0 = time.perf_counter()
+        dom = svc_engine.resolve_leader_domains(rows, lv)
+        assert time.perf_counter() - t0 < 0.02
+        assert dom.shape[0] == n
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, a)
+    assert svc_engine.timing(reset=True).svc_starts == 0
