@@ -101,3 +101,8 @@ tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o 
 tools/bin/block_probe: tools/block_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
+# A/B build: the service's row/leaf-pass stamps carry the shader clock (tools/dbg_clk.py)
+tools/bin/ab_clk/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_clk tools/bin/ab_clk
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_CLKFREQ -c -o build/ab_clk/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_clk/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

@@ -172,7 +172,7 @@ struct jsp_engine {
     uint32_t feas_words = 0;
 
     // scratch
-    DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, recs, tmp_a, tmp_b, tmp_c, tmp_d, tmp_e;
+    DevBuf cap, occ, run_class, run_len, assign, stats, ticket, granules, recs;
     HostBuf h_runs, h_assign, h_stats;  // zero-copy staging of the host placement path
     HostBuf h_done;                     // [n_blocks] completion words of the host placement path
     HostBuf h_err;                      // [1] error word: a failed launch writes its epoch (sticky)
@@ -180,6 +180,7 @@ struct jsp_engine {
     // memory the patch kernel reads in place, whose last workgroup writes
     // patch_seq to h_patch_done (patch_wait)
     HostBuf h_patch, h_patch_done;
+    HostBuf h_batch;                    // pinned staging of the webhook / reconciler batches (A5, A9)
     DevBuf patch_ctr;                   // workgroups of every patch launch so far (device counter)
     unsigned long long patch_target = 0;
     uint32_t patch_seq = 0;
@@ -236,6 +237,9 @@ struct jsp_engine {
                               // launch path answers until the next upload (every upload clears it)
         bool start_failed = false;  // the last start never saw its dispatcher poll (-> broken)
         bool armed = false;   // the host API was answered by the service: a patch (re)starts it (svc_wake)
+        unsigned long long zero_key = ~0ull;  // geometry the granule / bell lines were last zeroed for
+        unsigned long long occ_key = ~0ull;   // (shape, LDS, grid) whose co-residency was last checked
+        int occ_fit = 0;
         std::chrono::steady_clock::time_point last{};
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
@@ -523,8 +527,27 @@ uint32_t tally_wave_grid(jsp_engine* e) {
 
 // The tally alone (three-launch shape, jsp_tally_device): the wave-tile
 // kernel; JSP_TALLY_BLOCK=1 runs the workgroup-block kernel instead (A/B).
-int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s) {
+// Whether the wave tally can fold the feasibility words into itself (the
+// three-launch shape on the engine's own unsharded tallies): at most 4
+// classes (one wave pass), all at the leaf level, wave tiles available.
+// JSP_FEAS_FOLD=0 keeps the feasibility launch (A/B).
+bool fold_ok(jsp_engine* e) {
+    static const bool on = [] { const char* v = std::getenv("JSP_FEAS_FOLD"); return !(v && v[0] == '0'); }();
+    if (!on || e->C < 1 || e->C > 4 || e->n_wtiles == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total)
+        return false;
+    static const bool block = [] { const char* v = std::getenv("JSP_TALLY_BLOCK"); return v && v[0] == '1'; }();
+    if (block) return false;
+    for (const auto& c : e->cls_h)
+        if (c.level + 1 != e->K) return false;
+    return (uint64_t)(e->C + 1) * e->L_total * 4 < (1ull << 31);
+}
+
+int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s, bool fold = false) {
     jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
+    if (fold) {
+        a.feas_fold = e->feas.as<uint64_t>();
+        a.fold_nw = (e->L_total + 63) / 64;
+    }
     if (e->n_blocks == 0) return JSP_OK;
     static const bool block = [] { const char* v = std::getenv("JSP_TALLY_BLOCK"); return v && v[0] == '1'; }();
     EvPair* p = ev_begin(e, 0, s);
@@ -546,16 +569,37 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
 
 uint32_t* stats_ptr(jsp_engine* e) { return e->stats_override ? e->stats_override : e->stats.as<uint32_t>(); }
 
+// The level walker's shape: every class at one level of <= kLevelMaxWords
+// words, <= kLevelMaxRuns runs, records on (JSP_ASSIGN_LEVEL=0: off, A/B).
+bool level_walk_ok(jsp_engine* e, uint32_t n_runs) {
+    static const bool on = [] { const char* v = std::getenv("JSP_ASSIGN_LEVEL"); return !(v && v[0] == '0'); }();
+    if (!on || !e->assign_records || e->C < 1 || n_runs > jsp::kLevelMaxRuns) return false;
+    const uint32_t lvl = e->cls_h[0].level;
+    for (const auto& c : e->cls_h)
+        if (c.level != lvl) return false;
+    const uint32_t nw = (e->D[lvl] + 63) / 64;
+    return nw >= 1 && nw <= jsp::kLevelMaxWords && jsp::level_walk_lds_bytes(e->C, nw) <= 128u * 1024u;
+}
+
 int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
                 const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
-                int32_t* d_assign, hipStream_t s) {
+                int32_t* d_assign, hipStream_t s, bool folded = false) {
     EvPair* p = ev_begin(e, 1, s);
-    HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
-                             e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
+    if (!folded)
+        HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
+                                 e->feas_words, e->topo, e->feas.as<uint64_t>(), s));
     ev_end(p, s);
     p = ev_begin(e, 2, s);
     if (e->recs.reserve(sizeof(jsp::AssignRec) * (size_t)std::max<uint32_t>(J, 1), grave(e)) != hipSuccess)
         return set_err(JSP_ENOMEM, "assignment records (%u jobs)", J);
+    if (level_walk_ok(e, n_runs)) {
+        const uint32_t nw = (e->D[e->cls_h[0].level] + 63) / 64;
+        HIP_TRY(jsp::launch_assign_level(e->feas.as<uint64_t>(), e->C, nw, d_run_class, d_run_len, n_runs, J, d_assign,
+                                         stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(),
+                                         e->expand_rpw, s));
+        ev_end(p, s);
+        return JSP_OK;
+    }
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
                                e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
                                d_assign,
@@ -664,9 +708,10 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     }
     e->last_shape = fused_ok(e) ? 1 : 0;
     if (e->last_shape == 0) {
-        if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s)) return rc;
+        const bool fold = fold_ok(e);
+        if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s, fold)) return rc;
         return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_run_class, d_run_len,
-                           n_runs, J, d_assign, s);
+                           n_runs, J, d_assign, s, fold);
     }
     jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
     jsp::FusedArgs f = fused_args(e, a, d_run_class, d_run_len, n_runs, J, d_assign, stats_ptr(e));
@@ -763,6 +808,7 @@ int svc_stop(jsp_engine* e) {
 int svc_suspend(jsp_engine* e) {
     e->svc.resume |= e->svc.running;
     e->svc.broken = false;  // new geometry: the service may fit again
+    e->svc.zero_key = ~0ull;  // and its lines are zeroed again at the next start
     return svc_stop(e);
 }
 
@@ -816,11 +862,21 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
     HIP_TRY(v.box.reserve(64));
     const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
-    HIP_TRY(v.granules.reserve(gpad + 3 * 128));  // granules, then bell, counter, n_runs on lines of their own
-    // after everything the engine enqueued on any stream (the last stream's
-    // event), without making later calls wait for the service
-    if (int rc = wait_prior(e, v.stream)) return rc;
-    HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
+    // granules, then bell, counter, n_runs on lines of their own. Zeroed only
+    // when allocated or the geometry changes: granule tags and request
+    // numbers never repeat across starts, a stop in the bell carries its
+    // service's generation, and the fused counter stays a multiple of the
+    // tile count -- so a restart after an idle exit (the recovery's cold
+    // start) costs the launch alone. Every write the service stages from
+    // (uploads) was synchronous, and rows are fenced per request
+    // (patch_wait), so the launch need not wait for the engine's streams.
+    if (gpad + 3 * 128 > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
+    HIP_TRY(v.granules.reserve(gpad + 3 * 128));
+    const unsigned long long key = ((unsigned long long)nb << 8) | ((unsigned long long)n_tiles << 40) | (unsigned)shape;
+    if (v.zero_key != key) {
+        HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
+        v.zero_key = key;
+    }
     __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)v.seq, __ATOMIC_RELEASE);
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
     v.gen = v.gen % 0x7FFFFFFFu + 1u;
@@ -890,11 +946,18 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
         grid = nb * f.groups + 1;
     }
     {
-        int per_cu = 0;
-        HIP_TRY(jsp::service_occupancy(ta0, shape, lds, &per_cu));
         // the API answer can be one workgroup per CU high at high SGPR counts
-        // (MI355X_MICROARCH.md, Residency): keep that margin
-        const int64_t fit = (int64_t)std::max(per_cu > 1 ? per_cu - 1 : per_cu, 0) * e->n_cu;
+        // (MI355X_MICROARCH.md, Residency): keep that margin. Asked once per
+        // (shape, W, R, LDS size).
+        const unsigned long long okey = ((unsigned long long)lds << 16) | ((unsigned long long)shape << 8) |
+                                        ((unsigned long long)e->W << 4) | e->R;
+        if (v.occ_key != okey) {
+            int per_cu = 0;
+            HIP_TRY(jsp::service_occupancy(ta0, shape, lds, &per_cu));
+            v.occ_fit = std::max(per_cu > 1 ? per_cu - 1 : per_cu, 0);
+            v.occ_key = okey;
+        }
+        const int64_t fit = (int64_t)v.occ_fit * e->n_cu;
         if ((int64_t)grid > fit)
             return set_err(JSP_ERANGE, "placement service needs %u co-resident workgroups; %d CUs hold %lld at %zu B "
                                        "of LDS each", grid, e->n_cu, (long long)fit, lds);
@@ -1702,6 +1765,8 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) 
     HIP_TRY(upload(e->cls, h.data(), h.size(), s));
     HIP_TRY(upload(e->word_off, woff.data(), woff.size(), s));
     HIP_TRY(e->feas.reserve((size_t)std::max<uint32_t>(woff[C], 1) * 8));
+    // the folded feasibility (fold_ok) never writes the bits past the last leaf
+    HIP_TRY(hipMemsetAsync(e->feas.p, 0, (size_t)std::max<uint32_t>(woff[C], 1) * 8, s));
     HIP_TRY(e->cap.reserve((size_t)std::max<uint32_t>(C, 1) * std::max<uint32_t>(e->L_total, 1) * 4));
     HIP_TRY(e->occ.reserve((size_t)std::max<uint32_t>(e->L_total, 1) * 4));
     HIP_TRY(hipStreamSynchronize(s));
@@ -1943,13 +2008,19 @@ int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const 
     if (!leader_rows || !levels || !domain_out) return set_err(JSP_EINVAL, "NULL buffer");
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
-    HIP_TRY(upload(e->tmp_a, leader_rows, n, s, grave(e)));
-    HIP_TRY(upload(e->tmp_b, levels, n, s, grave(e)));
-    HIP_TRY(e->tmp_c.reserve((size_t)n * 4, grave(e)));
-    HIP_TRY(jsp::launch_resolve(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), n, e->N, e->leaf_start.as<uint32_t>(),
-                                e->n_leaves, e->leaf_begin, e->topo, e->tmp_c.as<int32_t>(), s));
-    HIP_TRY(hipMemcpyAsync(domain_out, e->tmp_c.p, (size_t)n * 4, hipMemcpyDeviceToHost, s));
+    // inputs and output through pinned staging the kernel reads and writes in
+    // place: no copy launches (a pageable copy can stall behind the resident
+    // service, tools/block_probe.hip)
+    HIP_TRY(e->h_batch.reserve((size_t)n * 12, grave(e)));
+    int32_t* hr = e->h_batch.as<int32_t>();
+    uint32_t* hl = reinterpret_cast<uint32_t*>(hr + n);
+    int32_t* ho = hr + 2 * (size_t)n;
+    std::memcpy(hr, leader_rows, (size_t)n * 4);
+    std::memcpy(hl, levels, (size_t)n * 4);
+    HIP_TRY(jsp::launch_resolve(hr, hl, n, e->N, e->leaf_start.as<uint32_t>(), e->n_leaves, e->leaf_begin, e->topo, ho,
+                                s));
     HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(domain_out, ho, (size_t)n * 4);
     return JSP_OK;
 }
 
@@ -1969,17 +2040,22 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
     if (M > 0 && !follower_domains) return set_err(JSP_EINVAL, "follower_domains is NULL");
     hipStream_t s = e->stream;
     if (int rc = use_engine_stream(e)) return rc;
-    HIP_TRY(upload(e->tmp_a, leader_rows, n_jobs, s, grave(e)));
-    HIP_TRY(upload(e->tmp_b, levels, n_jobs, s, grave(e)));
-    HIP_TRY(upload(e->tmp_c, follower_off, (size_t)n_jobs + 1, s, grave(e)));
-    HIP_TRY(e->tmp_d.reserve((size_t)std::max<uint32_t>(M, 1) * 4, grave(e)));
-    if (M > 0) HIP_TRY(hipMemcpyAsync(e->tmp_d.p, follower_domains, (size_t)M * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(e->tmp_e.reserve((size_t)n_jobs * 4, grave(e)));
-    HIP_TRY(jsp::launch_audit(e->tmp_a.as<int32_t>(), e->tmp_b.as<uint32_t>(), e->tmp_c.as<uint32_t>(),
-                              e->tmp_d.as<int32_t>(), n_jobs, e->N, e->leaf_start.as<uint32_t>(), e->n_leaves,
-                              e->leaf_begin, e->topo, e->tmp_e.as<uint32_t>(), s));
-    HIP_TRY(hipMemcpyAsync(bad_out, e->tmp_e.p, (size_t)n_jobs * 4, hipMemcpyDeviceToHost, s));
+    // pinned staging read and written in place by the kernel (as the resolve)
+    const size_t n = n_jobs;
+    HIP_TRY(e->h_batch.reserve((n * 4 + 1 + (size_t)M) * 4, grave(e)));
+    int32_t* hr = e->h_batch.as<int32_t>();
+    uint32_t* hl = reinterpret_cast<uint32_t*>(hr + n);
+    uint32_t* hf = hl + n;
+    int32_t* hd = reinterpret_cast<int32_t*>(hf + n + 1);
+    uint32_t* ho = reinterpret_cast<uint32_t*>(hd + M);
+    std::memcpy(hr, leader_rows, n * 4);
+    std::memcpy(hl, levels, n * 4);
+    std::memcpy(hf, follower_off, (n + 1) * 4);
+    if (M > 0) std::memcpy(hd, follower_domains, (size_t)M * 4);
+    HIP_TRY(jsp::launch_audit(hr, hl, hf, hd, n_jobs, e->N, e->leaf_start.as<uint32_t>(), e->n_leaves, e->leaf_begin,
+                              e->topo, ho, s));
     HIP_TRY(hipStreamSynchronize(s));
+    std::memcpy(bad_out, ho, n * 4);
     return JSP_OK;
 }
 
@@ -1990,6 +2066,7 @@ int jsp_engine_set_fused(jsp_engine* e, int mode) {
     if (mode != JSP_FUSED_OFF && mode != JSP_FUSED_AUTO) return set_err(JSP_EINVAL, "fused mode %d", mode);
     if (mode != e->fused_mode) {
         if (int rc = svc_stop(e)) return rc;
+        e->svc.zero_key = ~0ull;
     }
     e->fused_mode = mode;
     return JSP_OK;
@@ -2005,6 +2082,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
         e->svc.resume = false;
         e->svc.armed = false;
         if (int rc = svc_stop(e)) return rc;
+        e->svc.zero_key = ~0ull;
     }
     e->svc_mode = mode;
     return JSP_OK;

@@ -72,6 +72,12 @@ struct TallyArgs {
     uint32_t ld, leaf_base;
     int W, R;
     int sc1_out;                // write cap/occ write-through (sc1): the fused kernel's hand-off to its tail
+    // Feasibility folded into the wave tally (every class of the pass at the
+    // leaf level, unsharded snapshot): each wave tile sets its leaves' bits of
+    // class c's words at feas_fold + c * fold_nw (an atomic AND of its bit
+    // range, then an OR of its bits), so no feasibility launch follows. Null: off.
+    uint64_t* feas_fold;
+    uint32_t fold_nw;
 };
 
 // Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks
@@ -266,6 +272,19 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                          uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
+// The level walker (assign_level_kernel): every class at one topology level
+// of nw <= kLevelMaxWords words and at most kLevelMaxRuns runs. One wave holds
+// the taken bits in registers (WPL consecutive words per lane) and walks the
+// runs in order; per run one wave scan of the free feasible counts hands the
+// run its lowest free feasible domains; one record per word that gives
+// domains away (expand_kernel writes assign[]). Returns hipErrorInvalidValue
+// when the shape does not fit (the caller runs assign_kernel).
+constexpr uint32_t kLevelMaxWords = 64 * 32;
+constexpr uint32_t kLevelMaxRuns = 32;
+size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
+hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
+                               const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
+                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

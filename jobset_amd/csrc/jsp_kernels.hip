@@ -775,6 +775,35 @@ __device__ __forceinline__ void wave_store(const TallyArgs& a, __amdgpu_buffer_r
     }
 }
 
+// The tile's leaves' feasibility bits (leaf-level classes: capacity >= pods
+// and no rows of other exclusive jobs), set in the class's words: the tile's
+// bit range is cleared and its bits or-ed in, in one word or two (every leaf
+// belongs to one tile, so after the launch each word is exact; bits past the
+// last leaf are never set). Agent-scope atomics: the next launch reads them.
+template <int NV>
+__device__ __forceinline__ void wave_fold(const TallyArgs& a, const JSP_CONST DevClass* k_cls, uint4 bt, int lane,
+                                          const uint32_t (&sums)[NV]) {
+    const uint32_t nl = bt.y - bt.x;
+    const bool free_leaf = (uint32_t)lane < nl && sums[NV - 1] == 0u;
+    const uint32_t gl0 = a.leaf_base + bt.x;
+    const uint32_t w0 = gl0 >> 6, sh = gl0 & 63u;
+    const uint64_t lmask = nl >= 64u ? ~0ull : ((1ull << nl) - 1ull);
+#pragma unroll
+    for (int c = 0; c < NV - 1; ++c) {
+        const uint32_t pods = k_cls[c].pods;
+        const uint64_t m = __ballot(free_leaf && sums[c] >= pods);
+        if (lane == 0) {
+            uint64_t* f = a.feas_fold + (size_t)(a.c0 + (uint32_t)c) * a.fold_nw + w0;
+            __hip_atomic_fetch_and(f, ~(lmask << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_or(f, m << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (sh != 0u && sh + nl > 64u) {
+                __hip_atomic_fetch_and(f + 1, ~(lmask >> (64u - sh)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_fetch_or(f + 1, m >> (64u - sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
 template <int W, int R, int NV>
 __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, const uint4* __restrict__ tiles,
                                                                    uint32_t n_tiles, uint32_t n_leaves) {
@@ -828,6 +857,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
         btA = desc(kA);
         wave_issue<W, R>(a, rs, btA.z & ~3u, btA.x, kA < nt, lane, A);
         wave_store<NV>(a, cap_r, occ_r, done_a, lane, sums);
+        if (a.feas_fold) wave_fold<NV>(a, k_cls, done_a, lane, sums);
         if (kB >= nt) break;
 #ifdef JSP_STAMPS
         if (first) {  // diagnostic only: the next tile's rows in registers, then time its evaluation alone
@@ -847,6 +877,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave_kernel(TallyArgs a, 
         btB = desc(kB);
         wave_issue<W, R>(a, rs, btB.z & ~3u, btB.x, kB < nt, lane, B);
         wave_store<NV>(a, cap_r, occ_r, done_b, lane, sums);
+        if (a.feas_fold) wave_fold<NV>(a, k_cls, done_b, lane, sums);
         if (kA >= nt) break;
     }
     JSP_WSTAMP(t0, 5);
@@ -888,6 +919,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave1_kernel(TallyArgs a,
     uint32_t sums[NV];
     wave_eval<W, R, NV>(a, k_cls, s_pre, bt, lane, A, sums);
     wave_store<NV>(a, cap_r, occ_r, bt, lane, sums);
+    if (a.feas_fold) wave_fold<NV>(a, k_cls, bt, lane, sums);
 }
 
 // ----------------------------------------------------------------- feasibility
@@ -2096,6 +2128,92 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
     }
 }
 
+// ---- level walker (jsp_internal.h launch_assign_level): every class at one
+// level, few runs. The workgroup stages the classes' feasibility words in LDS
+// (lane-major, WPL + 1 words per lane row: conflict-light 8-byte reads), then
+// wave 0 alone walks the runs with the taken bits in registers: lane l owns
+// words [l WPL, l WPL + WPL). Per run: the lane's free feasible count, one
+// wave scan, the run takes its `used` lowest (a lane takes the ranks
+// [excl, excl + cnt) that fall below used, in word order), a second scan over
+// the lanes' nonzero words gives each record its slot. No workgroup barrier
+// after the staging one.
+template <int WPL>
+__global__ __launch_bounds__(256) void assign_level_kernel(const uint64_t* __restrict__ feas, uint32_t C, uint32_t nw,
+                                                           const uint32_t* __restrict__ run_class,
+                                                           const uint32_t* __restrict__ run_len, uint32_t n_runs,
+                                                           int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
+                                                           uint32_t* __restrict__ rec_count,
+                                                           AssignRec* __restrict__ recs) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][64][WPL + 1]
+    JSP_LDS uint64_t* sf = lds_ptr(s_f);
+    constexpr uint32_t kPitch = WPL + 1;
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t i = tid; i < C * 64u * (uint32_t)WPL; i += 256u) {
+        const uint32_t c = i / (64u * WPL), r = i - c * 64u * WPL;  // r = word index within the class
+        sf[(c * 64u + r / WPL) * kPitch + r % WPL] = r < nw ? feas[(size_t)c * nw + r] : 0ull;
+    }
+    __syncthreads();
+    if (tid >= 64) return;
+    uint64_t T[WPL];
+#pragma unroll
+    for (int k = 0; k < WPL; ++k) T[k] = 0;
+    uint32_t jpos = 0, rec = 0, placed = 0;
+    for (uint32_t r = 0; r < n_runs; ++r) {
+        const uint32_t c = to_sgpr(run_class[r]), n = to_sgpr(run_len[r]);
+        uint64_t A[WPL];
+        uint32_t cnt = 0;
+        const JSP_LDS uint64_t* row = sf + (c * 64u + lane) * kPitch;
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            A[k] = row[k] & ~T[k];
+            cnt += (uint32_t)__popcll(A[k]);
+        }
+        const uint32_t incl = wave_incl_scan(cnt, (int)lane);
+        const uint32_t excl = incl - cnt;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        const uint32_t used = total < n ? total : n;
+        uint32_t rem = used > excl ? used - excl : 0u;
+        uint32_t nz = 0;
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            const uint32_t pc = (uint32_t)__popcll(A[k]);
+            if (rem == 0u) {
+                A[k] = 0;
+            } else if (pc > rem) {
+                A[k] &= (1ull << select_bit(A[k], rem)) - 1ull;
+                rem = 0;
+            } else {
+                rem -= pc;
+            }
+            T[k] |= A[k];
+            nz += A[k] != 0ull ? 1u : 0u;
+        }
+        const uint32_t nz_incl = wave_incl_scan(nz, (int)lane);
+        uint32_t slot = rec + nz_incl - nz;
+        rec += (uint32_t)__builtin_amdgcn_readlane((int)nz_incl, 63);
+        uint32_t base = jpos + excl;
+#pragma unroll
+        for (int k = 0; k < WPL; ++k) {
+            if (A[k] != 0ull) {
+                AssignRec x;
+                x.dom0 = (lane * (uint32_t)WPL + (uint32_t)k) * 64u;
+                x.base = base;
+                x.took = A[k];
+                recs[slot++] = x;
+                base += (uint32_t)__popcll(A[k]);
+            }
+        }
+        for (uint32_t j = jpos + used + lane; j < jpos + n; j += 64u) assign[j] = -1;
+        placed += used;
+        jpos += n;
+    }
+    if (lane == 0) {
+        *rec_count = rec;
+        stats[0] = n_runs;
+        stats[1] = placed;
+    }
+}
+
 // ---- fused tail: leaf pass of the feasibility build (see place_fused_kernel)
 struct TailFeasArgs {
     const uint32_t* cap;
@@ -2674,7 +2792,8 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
         const uint32_t q = s_p[0];
         if (q == 0) {  // stop or idle: every tile leaves too
             if (threadIdx.x == 0)
-                __hip_atomic_store(v.bell, (unsigned long long)kSvcStop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(v.bell, ((unsigned long long)v.gen << 32) | kSvcStop, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
         seq = q;
@@ -2729,8 +2848,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             while (true) {
                 const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t q = (uint32_t)m;
-                if (q == kSvcStop) break;
-                if (q != seq && q != 0) {
+                // a stop carries its service's generation: one left by an
+                // earlier service in this (unzeroed) bell is not for us
+                if (q == kSvcStop && (uint32_t)(m >> 32) == v.gen) break;
+                if (q != seq && q != 0 && q != kSvcStop) {
                     next = q;
                     J = (uint32_t)(m >> 32);  // bit 31: rows patched since the previous request
                     break;
@@ -2792,8 +2913,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
             while (true) {
                 const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t q = (uint32_t)m;
-                if (q == kSvcStop) break;
-                if (q != seq && q != 0) {
+                // a stop carries its service's generation: one left by an
+                // earlier service in this (unzeroed) bell is not for us
+                if (q == kSvcStop && (uint32_t)(m >> 32) == v.gen) break;
+                if (q != seq && q != 0 && q != kSvcStop) {
                     next = q;
                     J = (uint32_t)(m >> 32);
                     break;
@@ -2935,8 +3058,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
             while (true) {
                 const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint32_t q = (uint32_t)m;
-                if (q == kSvcStop) break;
-                if (q != seq && q != 0) {
+                // a stop carries its service's generation: one left by an
+                // earlier service in this (unzeroed) bell is not for us
+                if (q == kSvcStop && (uint32_t)(m >> 32) == v.gen) break;
+                if (q != seq && q != 0 && q != kSvcStop) {
                     next = q;
                     dirty = (uint32_t)(m >> 63);
                     break;
@@ -3338,6 +3463,40 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
     // record), nor the feasibility words plus one per run (a run's records are
     // distinct words of its class; the next run of the class may share one).
     const uint64_t wb = (uint64_t)feas_words + n_runs;
+    const uint32_t bound = wb < J ? (uint32_t)wb : J;
+    const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
+    const uint32_t waves = (bound + rpw - 1) / rpw;
+    jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
+    return hipGetLastError();
+}
+
+static uint32_t level_wpl(uint32_t nw) {
+    const uint32_t w = (nw + 63u) / 64u;
+    return w <= 4u ? 4u : w <= 8u ? 8u : w <= 16u ? 16u : w <= 32u ? 32u : 0u;
+}
+
+size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
+    const uint32_t wpl = level_wpl(nw);
+    return wpl ? (size_t)C * 64u * (wpl + 1u) * 8u : 0u;
+}
+
+hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
+                               const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
+                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s) {
+    const uint32_t wpl = level_wpl(nw);
+    const size_t lds = level_walk_lds_bytes(C, nw);
+    if (wpl == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
+        return hipErrorInvalidValue;
+    switch (wpl) {
+        case 4: jsp_launch(assign_level_kernel<4>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        case 8: jsp_launch(assign_level_kernel<8>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        case 16: jsp_launch(assign_level_kernel<16>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        default: jsp_launch(assign_level_kernel<32>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+    }
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0) return e;
+    // records: one per (run, word) that gives domains away; a class's runs
+    // take its words in order, so at most its words plus one per run
+    const uint64_t wb = (uint64_t)C * nw + n_runs;
     const uint32_t bound = wb < J ? (uint32_t)wb : J;
     const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
     const uint32_t waves = (bound + rpw - 1) / rpw;

@@ -744,3 +744,63 @@ def test_device_timed_entry_points(engine, cfg):
     with pytest.raises(JspError) as ei:
         engine.tally_device_timed(t.data_ptr(), t[-1].data_ptr(), L, 0)
     assert ei.value.code == JSP_EINVAL
+
+
+def _one_level(p: Problem, level: int, max_classes: int, runs_sorted: bool, seed: int) -> Problem:
+    import dataclasses
+    rng = np.random.default_rng(seed)
+    C = min(len(p.classes), max_classes)
+    classes = [dataclasses.replace(c, level=level) for c in p.classes[:C]]
+    jc = (p.job_class % C).astype(np.uint32)
+    if runs_sorted:  # a few long runs (replicated jobs of one template each)
+        jc = np.sort(jc, kind="stable")
+        if rng.random() < 0.5:
+            jc = jc[::-1].copy()
+    return dataclasses.replace(p, classes=classes, job_class=jc)
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_folded_feasibility_and_level_walk(engine, seed):
+    """The three-launch step with every class at one level: the wave tally
+    folds the leaf classes' feasibility into its tiles (no feasibility
+    launch) and the level walker assigns in one wave. Leaf level with <= 4
+    classes takes both, an upper level only the walker, more runs than the
+    walker takes the block walker: bit-exact with the oracle throughout."""
+    base = synth.random_problem(seed, max_nodes=30_000, max_leaves=3000, max_jobs=3000)
+    K = base.topology.n_levels
+    engine.set_fused(False)
+    try:
+        for level, maxc, sorted_runs in ((K - 1, 4, True), (K - 1, 4, False), (0, 6, True), (K - 1, 16, True)):
+            p = _one_level(base, level, maxc, sorted_runs, seed)
+            engine.load(p)
+            got = engine.place(p.job_class, want_tally=True)
+            a, cap, occ = O.place_c(p)
+            assert_same(got, a, cap, occ)
+            assert got.fused == 0
+            O.check_invariants(p, got.assign, got.cap, got.occ)
+    finally:
+        engine.set_fused(True)
+
+
+def test_folded_feasibility_after_patches(engine):
+    """cfg4 (1M nodes, 4 leaf classes, 4 runs) placed repeatedly while rows
+    change: every tally rewrites each leaf's bit exactly (no stale bit from
+    the previous step survives the fold)."""
+    p = synth.config4()
+    engine.set_fused(False)
+    try:
+        engine.load(p)
+        rng = np.random.default_rng(44)
+        for step in range(4):
+            got = engine.place(p.job_class)
+            np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+            rows = np.sort(rng.choice(p.nodes.n_nodes, size=20_000, replace=False)).astype(np.uint32)
+            if step % 2 == 0:
+                free = np.zeros((p.nodes.free.shape[0], rows.shape[0]), dtype=np.uint32)  # racks become infeasible
+            else:
+                free = rng.integers(0, 200_000, size=(p.nodes.free.shape[0], rows.shape[0])).astype(np.uint32)
+            engine.patch_rows(rows, free=free)
+            p.nodes.free[:, rows] = free
+        np.testing.assert_array_equal(engine.place(p.job_class).assign, O.place_c(p)[0])
+    finally:
+        engine.set_fused(True)
