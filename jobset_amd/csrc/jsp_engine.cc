@@ -824,6 +824,13 @@ void svc_resume(jsp_engine* e) {
     }
 }
 
+// The compaction service co-located on one XCD (ServiceArgs::spread;
+// JSP_SVC_XCD=0: off). Read at each service start (in-process A/B).
+bool svc_xcd() {
+    const char* c = std::getenv("JSP_SVC_XCD");
+    return !(c && c[0] == '0');
+}
+
 // Resident tiles keep their rows in LDS between requests (JSP_SVC_ROW_CACHE=0:
 // reload every request; read at each service start, so an A/B can switch it
 // inside one process).
@@ -870,8 +877,9 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     // start) costs the launch alone. Every write the service stages from
     // (uploads) was synchronous, and rows are fenced per request
     // (patch_wait), so the launch need not wait for the engine's streams.
-    if (gpad + 3 * 128 > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
-    HIP_TRY(v.granules.reserve(gpad + 3 * 128));
+    const size_t xbytes = ((size_t)4 * (nb + 1) + 127) & ~size_t(127);  // XCC vote words (co-located service)
+    if (gpad + 3 * 128 + xbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
+    HIP_TRY(v.granules.reserve(gpad + 3 * 128 + xbytes));
     const unsigned long long key = ((unsigned long long)nb << 8) | ((unsigned long long)n_tiles << 40) | (unsigned)shape;
     if (v.zero_key != key) {
         HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
@@ -889,6 +897,10 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.bell = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad);
     a.counter = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128);
     a.nruns = shape == 1 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 256) : nullptr;
+    a.xcc = reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 384);
+    // co-located compaction service: all its workgroups on one XCD when it
+    // fits one (32 CUs, one workgroup per CU); JSP_SVC_XCD=0 spreads it (A/B)
+    a.spread = shape == 2 && nb + 1 <= 32 && svc_xcd() ? 8u : 1u;
     a.pods = e->cls_h[0].pods;
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();

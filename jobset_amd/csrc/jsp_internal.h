@@ -170,6 +170,15 @@ struct ServiceArgs {
     uint32_t* nruns;                    // device word: the request's run count (fused shape), or null
     unsigned long long* counter;        // device: finished tiles over all requests (fused shape)
     uint32_t row_cache_words;           // compaction shape: LDS word offset of the tiles' row copy, 0 = none
+    // XCD co-location (compaction shape): the grid is spread x (tiles + 1)
+    // workgroups and only those with blockIdx % spread == 0 stay -- one XCD
+    // under the round-robin dealing of workgroups to XCDs. Each survivor
+    // publishes its XCC id in xcc[] (tagged with gen); when all agree, the
+    // bell and the look-back granules are written as plain stores that stay
+    // in that XCD's L2 (the sc1 loads that poll them are L2 hits); otherwise
+    // they stay write-through (correct on any placement). spread 1: off.
+    uint32_t spread;
+    uint32_t* xcc;                      // device [tiles + 1] vote words
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

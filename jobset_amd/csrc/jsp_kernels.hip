@@ -2611,9 +2611,14 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_kernel(TallyArgs a,
 constexpr uint32_t kAggregate = 1, kPrefix = 2;
 static_assert(kMaxBlkLeaves <= kTallyThreads, "compaction keeps one leaf per thread");
 
-__device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoch, uint32_t status, uint32_t v) {
+// `local`: every tile of the launch runs on one XCD (the service's XCC vote):
+// a plain store keeps the line in that XCD's L2, where the other tiles' sc1
+// loads find it; otherwise write-through (sc1), correct across XCDs.
+__device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoch, uint32_t status, uint32_t v,
+                                            bool local = false) {
     const unsigned long long x = ((unsigned long long)((epoch << 2) | status) << 32) | v;
-    __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (local) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // One compaction tile: tally its leaves, count the feasible ones, look back
@@ -2629,7 +2634,7 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
                                              uint32_t* s_x, JSP_LDS uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
-                                             bool use_cache = false, uint32_t tag = 0) {
+                                             bool use_cache = false, uint32_t tag = 0, bool local = false) {
     unsigned long long* assign64 = reinterpret_cast<unsigned long long*>(assign);
     const unsigned long long tag_hi = (unsigned long long)tag << 32;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -2645,7 +2650,7 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
     JSP_STAMP(tile, 3);
     svc_stamp(clk, 3);
-    if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total);
+    if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total, local);
     if (tid < 64) {  // wave 0: look back
         uint32_t prefix = 0, spins = 0;
         bool timeout = false;
@@ -2674,7 +2679,7 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
             // A tile that timed out knows no prefix: it publishes none (its
             // aggregate stays visible, so later tiles still sum correctly past
             // it), scatters nothing and reports the launch as failed.
-            if (tile != 0 && !timeout) put_granule(g + tile, epoch, kPrefix, prefix + total);
+            if (tile != 0 && !timeout) put_granule(g + tile, epoch, kPrefix, prefix + total, local);
             s_x[2] = prefix;
             s_x[3] = timeout ? 1u : 0u;
         }
@@ -2742,7 +2747,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
 // (one sc1 8-byte store, tag = seq), which the tiles poll close by. Only this
 // workgroup reads host memory: tiles polling it themselves see a request up
 // to a whole round trip apart and load the link with reads.
-__device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t* s_p) {
+__device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t* s_p, bool local = false) {
     const uint32_t w = threadIdx.x >> 6;
     uint32_t seq = v.seq0;
     if (threadIdx.x == 0) {
@@ -2778,7 +2783,8 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
                         __hip_atomic_store(v.nruns, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                     }
-                    __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
@@ -2805,13 +2811,62 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
     }
 }
 
+// The XCC vote of a co-located service (ServiceArgs::spread): workgroup
+// `slot` of n publishes its XCC id (tagged with the launch generation, so a
+// vote left by an earlier launch is not counted) and wave 0 reads all n:
+// true when every workgroup of the service runs on one XCD. Bounded: a vote
+// missing after idle_ticks counts as a disagreement (the write-through
+// protocol is correct on any placement).
+__device__ bool service_xcc_vote(const ServiceArgs& v, uint32_t slot, uint32_t n, uint32_t* s_flag) {
+    if (threadIdx.x == 0) {
+        uint32_t x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        __hip_atomic_store(v.xcc + slot, ((v.gen & 0x0FFFFFFFu) << 4) | (x & 15u), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x, tag = v.gen & 0x0FFFFFFFu;
+        uint32_t lo = 15u, hi = 0u;
+        bool ok = true;
+        const uint64_t t0 = wall_clock64();
+        for (uint32_t base = 0; base < n && ok; base += 64) {
+            const uint32_t i = base + lane;
+            uint32_t x = 0;
+            while (true) {
+                if (i < n) x = __hip_atomic_load(v.xcc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__all(i >= n || (x >> 4) == tag)) break;
+                if (wall_clock64() - t0 > v.idle_ticks) {
+                    ok = false;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (i < n) {
+                lo = min(lo, x & 15u);
+                hi = max(hi, x & 15u);
+            }
+        }
+        lo = wave_min_u32(lo);
+        hi = ~wave_min_u32(~hi);
+        if (lane == 0) s_flag[0] = ok && lo == hi ? 1u : 0u;
+    }
+    __syncthreads();
+    const bool local = s_flag[0] != 0u;
+    __syncthreads();
+    return local;
+}
+
 template <int W, int R>
 __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs a, ServiceArgs v) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     uint32_t* s_x = lds + tally_lds_words(a);  // compact_tile's words, then [16] request seq [17] J
-    const uint32_t tile = blockIdx.x;
+    // co-located launch: only every spread-th workgroup stays (one XCD under
+    // round-robin dealing), and the survivors vote on whether they share one
+    if (v.spread > 1 && blockIdx.x % v.spread != 0) return;
+    const uint32_t tile = blockIdx.x / (v.spread > 1 ? v.spread : 1u);
+    const bool local = v.spread > 1 ? service_xcc_vote(v, tile, a.n_blocks + 1, s_x + 18) : false;
     if (tile == a.n_blocks) {
-        service_dispatch(v, s_x + 16);
+        service_dispatch(v, s_x + 16, local);
         return;
     }
     uint32_t seq = v.seq0;
@@ -2871,7 +2926,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
         compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
-                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next);
+                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local);
         cached = row_cache != nullptr;
         signal_host_clk(v.done + tile, next, clk, clk_out);
         // The host may patch the snapshot before its next request (another
@@ -3324,7 +3379,7 @@ hipError_t launch_compact(const TallyArgs& a, const CompactArgs& f, hipStream_t 
 
 template <int W, int R>
 static hipError_t launch_service_wr(const TallyArgs& a, const ServiceArgs& v, hipStream_t s) {
-    jsp_launch((place_service_kernel<W, R>), dim3(a.n_blocks + 1), dim3(kTallyThreads),
+    jsp_launch((place_service_kernel<W, R>), dim3((a.n_blocks + 1) * (v.spread > 1 ? v.spread : 1u)), dim3(kTallyThreads),
                service_lds_bytes(a.la, a.W, a.R, v.row_cache_words != 0), s, a, v);
     return hipGetLastError();
 }

@@ -495,3 +495,27 @@ def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
         assert got.fused == 3
         np.testing.assert_array_equal(got.assign, a)
     assert svc_engine.timing(reset=True).svc_starts == 0
+
+
+@pytest.mark.parametrize("xcd", ["1", "0"])
+def test_service_colocated_and_spread(svc_engine, monkeypatch, xcd):
+    """The compaction service co-located on one XCD (plain bell and granule
+    stores when every workgroup votes the same XCC id) and spread over the
+    chip (write-through): the same answers, across requests, patches and J."""
+    monkeypatch.setenv("JSP_SVC_XCD", xcd)  # read at each service start
+    svc_engine.service_stop()
+    p = synth.config2()
+    svc_engine.load(p)
+    rng = np.random.default_rng(int(xcd) + 3)
+    for step in range(30):
+        J = [990, 1, 500, 1200][step % 4]
+        jc = np.zeros(J, dtype=np.uint32)
+        got = svc_engine.place(jc)
+        assert got.fused in (3,) or step == 0
+        np.testing.assert_array_equal(got.assign, O.place_c(dataclasses.replace(p, job_class=jc))[0])
+        if step % 5 == 4:
+            rows = np.sort(rng.choice(p.nodes.n_nodes, size=64, replace=False)).astype(np.uint32)
+            taints = rng.integers(0, 2, size=64).astype(np.uint32)
+            svc_engine.patch_rows(rows, taints=taints)
+            p.nodes.taints[rows] = taints
+    svc_engine.check()
