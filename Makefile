@@ -106,3 +106,13 @@ tools/bin/ab_clk/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine
 	@mkdir -p build/ab_clk tools/bin/ab_clk
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_CLKFREQ -c -o build/ab_clk/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_clk/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+# A/B build: service stamps 2-4 inside the row pass (loop start, class record, first scan)
+tools/bin/ab_fine/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_fine tools/bin/ab_fine
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_FINESTAMP -c -o build/ab_fine/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_fine/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+# diagnostic stamp build shipped to the GPU box (tools/bin is not gpurun-ignored)
+tools/bin/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/diag2 tools/bin/diag
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_STAMPS -c -o build/diag2/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag2/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

@@ -824,6 +824,13 @@ void svc_resume(jsp_engine* e) {
     }
 }
 
+// The compaction service's resident path (ServiceArgs::resident;
+// JSP_SVC_RESIDENT=0: the LDS row cache path). Read at each service start.
+bool svc_resident() {
+    const char* c = std::getenv("JSP_SVC_RESIDENT");
+    return !(c && c[0] == '0');
+}
+
 // The compaction service co-located on one XCD (ServiceArgs::spread;
 // JSP_SVC_XCD=0: off). Read at each service start (in-process A/B).
 bool svc_xcd() {
@@ -932,8 +939,11 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     jsp::TallyArgs ta{};
     jsp::SplitArgs sp{};
     if (shape == 2) {
-        // the tiles keep their rows in LDS between requests when each is one chunk
-        const bool rc = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
+        // the tiles keep their rows on chip between requests when each is one
+        // chunk: in registers (the resident path; JSP_SVC_RESIDENT=0: in LDS)
+        const bool one_chunk = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
+        a.resident = one_chunk && svc_resident() ? 1u : 0u;
+        const bool rc = one_chunk && !a.resident;
         a.row_cache_words = rc ? jsp::service_row_cache_words(e->blk_leaves) : 0u;
         lds = jsp::service_lds_bytes(e->blk_leaves, (int)e->W, (int)e->R, rc);
         grid = nb + 1;

@@ -179,6 +179,10 @@ struct ServiceArgs {
     // they stay write-through (correct on any placement). spread 1: off.
     uint32_t spread;
     uint32_t* xcc;                      // device [tiles + 1] vote words
+    // compaction shape, every tile one chunk: the tile's rows stay in
+    // registers between requests, its class in scalar registers and its
+    // leaves' row bounds in registers (place_service_kernel's resident path)
+    uint32_t resident;
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay
@@ -282,13 +286,13 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                          uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
 // The level walker (assign_level_kernel): every class at one topology level
-// of nw <= kLevelMaxWords words and at most kLevelMaxRuns runs. One wave holds
-// the taken bits in registers (WPL consecutive words per lane) and walks the
-// runs in order; per run one wave scan of the free feasible counts hands the
-// run its lowest free feasible domains; one record per word that gives
-// domains away (expand_kernel writes assign[]). Returns hipErrorInvalidValue
-// when the shape does not fit (the caller runs assign_kernel).
-constexpr uint32_t kLevelMaxWords = 64 * 32;
+// of nw <= kLevelMaxWords words and at most kLevelMaxRuns runs. 256 threads
+// hold the taken bits of their words in registers and walk the runs in
+// order; per run one block scan of the free feasible counts hands the run its
+// lowest free feasible domains; one record per word that gives domains away
+// (expand_kernel writes assign[]). Returns hipErrorInvalidValue when the
+// shape does not fit (the caller runs assign_kernel).
+constexpr uint32_t kLevelMaxWords = 256 * 8;
 constexpr uint32_t kLevelMaxRuns = 32;
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,

@@ -511,6 +511,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         for (int i = 0; i < 4; ++i) valid[i] = any && (row + i >= r0) && (row + i < r1);
         __syncthreads();  // s_cls / s_ls / s_acc ready (first chunk); previous leaf pass done (later ones)
         JSP_STAMP(blk, 1);
+#ifdef JSP_AB_FINESTAMP
+        svc_stamp(clk, 2);  // A/B build: slots 2-4 inside the row pass (compact_tile's are dropped)
+#endif
         const bool more = base + kChunkRows < r1;  // workgroup-uniform
         RowRegs<W, R> nxt;
         if (more) {
@@ -527,6 +530,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
             uint32_t v[4];
             if (c < nc) {
                 const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
+#ifdef JSP_AB_FINESTAMP
+                if (c == 0) svc_stamp(clk, 3);
+#endif
                 uint32_t cap[4];
                 row_caps<W, R>(k, fr, cap);
 #pragma unroll
@@ -542,6 +548,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
             }
             const uint32_t p0 = v[0], p1 = p0 + v[1], p2 = p1 + v[2], p3 = p2 + v[3];
             const uint32_t incl = wave_incl_scan(p3, lane);
+#ifdef JSP_AB_FINESTAMP
+            if (c == 0 && incl != 0xFFFFFFFFu) svc_stamp(clk, 4);
+#endif
             const uint32_t wex = incl - p3;
             reinterpret_cast<uint4*>(s_pre + c * kChunkRows)[tid] = make_uint4(wex + p0, wex + p1, wex + p2, incl);
             if (lane == 63) s_wsum[c * kTallyWaves + wid] = incl;
@@ -2129,89 +2138,116 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
 }
 
 // ---- level walker (jsp_internal.h launch_assign_level): every class at one
-// level, few runs. The workgroup stages the classes' feasibility words in LDS
-// (lane-major, WPL + 1 words per lane row: conflict-light 8-byte reads), then
-// wave 0 alone walks the runs with the taken bits in registers: lane l owns
-// words [l WPL, l WPL + WPL). Per run: the lane's free feasible count, one
-// wave scan, the run takes its `used` lowest (a lane takes the ranks
-// [excl, excl + cnt) that fall below used, in word order), a second scan over
-// the lanes' nonzero words gives each record its slot. No workgroup barrier
-// after the staging one.
-template <int WPL>
-__global__ __launch_bounds__(256) void assign_level_kernel(const uint64_t* __restrict__ feas, uint32_t C, uint32_t nw,
-                                                           const uint32_t* __restrict__ run_class,
-                                                           const uint32_t* __restrict__ run_len, uint32_t n_runs,
-                                                           int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
-                                                           uint32_t* __restrict__ rec_count,
-                                                           AssignRec* __restrict__ recs) {
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][64][WPL + 1]
+// level, few runs. The workgroup (256 threads) stages the classes'
+// feasibility words in LDS (word-major by thread: thread t owns words
+// [t WPT, t WPT + WPT), stored [class][k][t] so every read is conflict-free)
+// and keeps the taken bits of its words in registers. Per run, ONE block scan
+// (one barrier) of a packed (nonzero words << 18 | free feasible count) gives
+// each thread its first rank and its first record slot: the run takes its
+// `used` lowest free feasible domains, and the words that give domains away
+// are the first nonzero ones, so a word's record slot is its rank among the
+// nonzero words. The thread holding the run's last taking word publishes the
+// next run's record base (read after the next scan's barrier). A one-wave
+// version (all words in one wave's registers) was instruction-bound: a wave64
+// VALU op takes 4 cycles of its SIMD, ~3 us per run on cfg4.
+constexpr uint32_t kLevelThreads = 256;
+template <int WPT>
+__global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint64_t* __restrict__ feas, uint32_t C,
+                                                                     uint32_t nw, const uint32_t* __restrict__ run_class,
+                                                                     const uint32_t* __restrict__ run_len, uint32_t n_runs,
+                                                                     int32_t* __restrict__ assign,
+                                                                     uint32_t* __restrict__ stats,
+                                                                     uint32_t* __restrict__ rec_count,
+                                                                     AssignRec* __restrict__ recs) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][256]
     JSP_LDS uint64_t* sf = lds_ptr(s_f);
-    constexpr uint32_t kPitch = WPL + 1;
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    for (uint32_t i = tid; i < C * 64u * (uint32_t)WPL; i += 256u) {
-        const uint32_t c = i / (64u * WPL), r = i - c * 64u * WPL;  // r = word index within the class
-        sf[(c * 64u + r / WPL) * kPitch + r % WPL] = r < nw ? feas[(size_t)c * nw + r] : 0ull;
+    __shared__ uint32_t s_rc[kLevelMaxRuns], s_rl[kLevelMaxRuns];
+    __shared__ uint32_t s_scan[2 * kTallyWaves];
+    __shared__ uint32_t s_base[2];
+    const uint32_t tid = threadIdx.x;
+    JSP_STAMP(4050u, 0);
+    // the run table beside the words: one round trip, however far the runs
+    // live (pinned host memory on the host path)
+    if (tid < n_runs) {
+        s_rc[tid] = run_class[tid];
+        s_rl[tid] = run_len[tid];
+    }
+    if (tid == 0) s_base[0] = 0u;
+    // 16 loads per thread in flight before their LDS stores
+    constexpr uint32_t kBatch = 16;
+    const uint32_t total = C * kLevelThreads * (uint32_t)WPT;
+    for (uint32_t b0 = 0; b0 < total; b0 += kLevelThreads * kBatch) {
+        uint64_t f[kBatch];
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q) {
+            const uint32_t i = b0 + q * kLevelThreads + tid;  // i = c * (256 WPT) + word
+            const uint32_t c = i / (kLevelThreads * WPT), w = i - c * (kLevelThreads * WPT);
+            f[q] = (i < total && w < nw) ? feas[(size_t)c * nw + w] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kBatch; ++q) {
+            const uint32_t i = b0 + q * kLevelThreads + tid;
+            const uint32_t c = i / (kLevelThreads * WPT), w = i - c * (kLevelThreads * WPT);
+            if (i < total) sf[(c * WPT + w % WPT) * kLevelThreads + w / WPT] = f[q];
+        }
     }
     __syncthreads();
-    if (tid >= 64) return;
-    uint64_t T[WPL];
+    JSP_STAMP(4050u, 1);
+    uint64_t T[WPT];
 #pragma unroll
-    for (int k = 0; k < WPL; ++k) T[k] = 0;
-    uint32_t jpos = 0, rec = 0, placed = 0;
+    for (int k = 0; k < WPT; ++k) T[k] = 0;
+    uint32_t jpos = 0, placed = 0;
     for (uint32_t r = 0; r < n_runs; ++r) {
-        const uint32_t c = to_sgpr(run_class[r]), n = to_sgpr(run_len[r]);
-        uint64_t A[WPL];
-        uint32_t cnt = 0;
-        const JSP_LDS uint64_t* row = sf + (c * 64u + lane) * kPitch;
+        const uint32_t c = s_rc[r], n = s_rl[r];
+        uint64_t A[WPT];
+        uint32_t cnt = 0, nzw = 0;
 #pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            A[k] = row[k] & ~T[k];
+        for (int k = 0; k < WPT; ++k) {
+            A[k] = sf[(c * WPT + k) * kLevelThreads + tid] & ~T[k];
             cnt += (uint32_t)__popcll(A[k]);
+            nzw += A[k] != 0ull ? 1u : 0u;
         }
-        const uint32_t incl = wave_incl_scan(cnt, (int)lane);
-        const uint32_t excl = incl - cnt;
-        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        const uint32_t used = total < n ? total : n;
-        uint32_t rem = used > excl ? used - excl : 0u;
-        uint32_t nz = 0;
+        uint32_t tot_p;
+        const uint32_t pre_p = block_excl_scan<kLevelThreads>((nzw << 18) | cnt, s_scan, &tot_p, (int)(r & 1u));
+        const uint32_t pre = pre_p & 0x3FFFFu, total_free = tot_p & 0x3FFFFu;
+        const uint32_t used = total_free < n ? total_free : n;
+        const uint32_t rec_base = s_base[r & 1u];  // published by run r - 1 before this scan's barrier
+        uint32_t rem = used > pre ? used - pre : 0u;
+        uint32_t slot = rec_base + (pre_p >> 18);
+        uint32_t base = jpos + pre;
 #pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            const uint32_t pc = (uint32_t)__popcll(A[k]);
-            if (rem == 0u) {
-                A[k] = 0;
-            } else if (pc > rem) {
-                A[k] &= (1ull << select_bit(A[k], rem)) - 1ull;
-                rem = 0;
-            } else {
-                rem -= pc;
-            }
-            T[k] |= A[k];
-            nz += A[k] != 0ull ? 1u : 0u;
-        }
-        const uint32_t nz_incl = wave_incl_scan(nz, (int)lane);
-        uint32_t slot = rec + nz_incl - nz;
-        rec += (uint32_t)__builtin_amdgcn_readlane((int)nz_incl, 63);
-        uint32_t base = jpos + excl;
-#pragma unroll
-        for (int k = 0; k < WPL; ++k) {
-            if (A[k] != 0ull) {
+        for (int k = 0; k < WPT; ++k) {
+            if (rem != 0u && A[k] != 0ull) {
+                const uint32_t pc = (uint32_t)__popcll(A[k]);
+                uint64_t took = A[k];
+                if (pc > rem) took &= (1ull << select_bit(took, rem)) - 1ull;
+                const uint32_t tk = pc > rem ? rem : pc;
+                rem -= tk;
+                T[k] |= took;
                 AssignRec x;
-                x.dom0 = (lane * (uint32_t)WPL + (uint32_t)k) * 64u;
+                x.dom0 = (tid * (uint32_t)WPT + (uint32_t)k) * 64u;
                 x.base = base;
-                x.took = A[k];
-                recs[slot++] = x;
-                base += (uint32_t)__popcll(A[k]);
+                x.took = took;
+                recs[slot] = x;
+                ++slot;
+                base += tk;
+                // the run's last taking word: the next run's records start after it
+                if (rem == 0u) s_base[(r + 1) & 1u] = slot;
             }
         }
-        for (uint32_t j = jpos + used + lane; j < jpos + n; j += 64u) assign[j] = -1;
+        if (used == 0u && tid == 0) s_base[(r + 1) & 1u] = rec_base;
+        for (uint32_t j = jpos + used + tid; j < jpos + n; j += kLevelThreads) assign[j] = -1;
         placed += used;
         jpos += n;
+        if (r < 5) JSP_STAMP(4050u, 2 + r);
     }
-    if (lane == 0) {
-        *rec_count = rec;
+    __syncthreads();  // the last run's record base
+    if (tid == 0) {
+        *rec_count = s_base[n_runs & 1u];
         stats[0] = n_runs;
         stats[1] = placed;
     }
+    JSP_STAMP(4050u, 7);
 }
 
 // ---- fused tail: leaf pass of the feasibility build (see place_fused_kernel)
@@ -2621,35 +2657,28 @@ __device__ __forceinline__ void put_granule(unsigned long long* g, uint32_t epoc
     else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// One compaction tile: tally its leaves, count the feasible ones, look back
-// for the feasible leaves before it, scatter its jobs' domains. `sys`: assign[]
-// and stats are in pinned host memory (system-scope stores). s_x: the small
-// LDS words after the tally carve ([2] prefix [3] timeout [4..16] scan).
-// tag != 0 (the resident service): assign is a u64 array and entry j is
-// written as (tag << 32) | domain in ONE system-scope store, so the host knows
-// each entry has arrived from the entry itself and returns without waiting for
-// the tiles' done words (which then only gate the next request).
-template <int W, int R, bool STAGED = false>
-__device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
-                                             uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
-                                             int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
-                                             uint32_t* s_x, JSP_LDS uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
-                                             bool use_cache = false, uint32_t tag = 0, bool local = false) {
+// The compaction after the tally: `ok` = this thread's leaf (l0 + tid) is
+// feasible. Scan of the feasible count, look back for the feasible leaves
+// before the tile, scatter its jobs' domains. `sys`: assign[] and stats are in
+// pinned host memory (system-scope stores). s_x: the small LDS words after
+// the tally carve ([2] prefix [3] timeout [4..16] scan). tag != 0 (the
+// resident service): assign is a u64 array and entry j is written as
+// (tag << 32) | domain in ONE system-scope store, so the host knows each entry
+// has arrived from the entry itself and returns without waiting for the
+// tiles' done words (which then only gate the next request).
+__device__ __forceinline__ void compact_finish(const TallyArgs& a, uint32_t tile, uint32_t l0, bool ok, uint32_t epoch,
+                                               uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
+                                               int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* s_x,
+                                               JSP_LDS uint32_t* clk, uint32_t tag, bool local) {
     unsigned long long* assign64 = reinterpret_cast<unsigned long long*>(assign);
     const unsigned long long tag_hi = (unsigned long long)tag << 32;
     const int tid = threadIdx.x, lane = tid & 63;
-    // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
-    tally_block<W, R, STAGED>(a, tile, lds, bt, clk, row_cache, use_cache);
-    JSP_STAMP(tile, 2);
-    svc_stamp(clk, 2);
-
-    const uint32_t* s_acc = lds + tally_acc_off(1);
-    const uint32_t l0 = bt.x, nl = bt.y - bt.x;
-    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
     uint32_t total;
     const uint32_t rank = block_excl_scan<kTallyThreads>(ok ? 1u : 0u, s_x + 4, &total);
     JSP_STAMP(tile, 3);
+#ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 3);
+#endif
     if (tid == 0) put_granule(g + tile, epoch, tile == 0 ? kPrefix : kAggregate, total, local);
     if (tid < 64) {  // wave 0: look back
         uint32_t prefix = 0, spins = 0;
@@ -2686,7 +2715,9 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     }
     __syncthreads();
     JSP_STAMP(tile, 4);
+#ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 4);
+#endif
     const uint32_t prefix = s_x[2];
     const bool failed = s_x[3] != 0;
     if (!failed) {
@@ -2709,6 +2740,26 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     } else if (tid == 0) {
         __hip_atomic_store(err, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+}
+
+// One compaction tile: tally its leaves (sums in LDS), then compact_finish.
+template <int W, int R, bool STAGED = false>
+__device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
+                                             uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
+                                             int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
+                                             uint32_t* s_x, JSP_LDS uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
+                                             bool use_cache = false, uint32_t tag = 0, bool local = false) {
+    const int tid = threadIdx.x;
+    // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
+    tally_block<W, R, STAGED>(a, tile, lds, bt, clk, row_cache, use_cache);
+    JSP_STAMP(tile, 2);
+#ifndef JSP_AB_FINESTAMP
+    svc_stamp(clk, 2);
+#endif
+    const uint32_t* s_acc = lds + tally_acc_off(1);
+    const uint32_t nl = bt.y - bt.x;
+    const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
+    compact_finish(a, tile, bt.x, ok, epoch, J, n_runs, g, spin_limit, assign, stats, err, sys, s_x, clk, tag, local);
 }
 
 template <int W, int R>
@@ -2811,6 +2862,81 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
     }
 }
 
+// ---- resident compaction tile (ServiceArgs::resident): every tile is one
+// chunk, so thread t's 4 rows and leaf t never change while the service
+// lives. The rows stay in registers (reloaded with sc1 loads when a patch
+// marked them dirty), the class in scalar registers, and each leaf's
+// chunk-local row bounds in registers: a request evaluates the rows, scans
+// them (two independent DPP chains), stores the row prefixes, crosses ONE
+// barrier and forms each leaf's capacity and occupancy from two prefix
+// differences -- no class-record or leaf-start LDS round trips, no
+// accumulation buffer, no second barrier before the feasible-count scan.
+struct ResidentLeaf {
+    uint32_t xh, xb;  // chunk-local last row of the leaf, row before its first
+    uint32_t wh, wb;  // their waves (256 rows per wave)
+    bool live, has_lo;
+};
+
+__device__ __forceinline__ ResidentLeaf resident_leaf(const TallyArgs& a, uint4 bt) {
+    ResidentLeaf f{0u, 0u, 0u, 0u, false, false};
+    const uint32_t nl = bt.y - bt.x, li = threadIdx.x;
+    if (li < nl) {
+        const uint32_t base = bt.z & ~3u;
+        const uint32_t s = a.leaf_start[bt.x + li], e = a.leaf_start[bt.x + li + 1];
+        f.live = s < e;
+        f.xh = f.live ? e - 1 - base : 0u;
+        f.has_lo = f.live && s > base;
+        f.xb = f.has_lo ? s - 1 - base : 0u;
+        f.wh = f.xh >> 8;
+        f.wb = f.xb >> 8;
+    }
+    return f;
+}
+
+__device__ __forceinline__ uint32_t wave_off(uint4 ws, uint32_t w) {
+    const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
+    return w == 0 ? 0u : w == 1 ? e1 : w == 2 ? e2 : e3;
+}
+
+template <int W, int R>
+__device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const RowRegs<W, R>& x, const bool (&valid)[4],
+                                              const ResidentLeaf& lf, JSP_LDS uint32_t* s_pre,
+                                              JSP_LDS uint32_t* s_wsum) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+    uint32_t cap[4];
+    row_caps<W, R>(k, x.fr, cap);
+    uint32_t v0[4], v1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        bool ok = valid[i] & ((x.tn[i] & k.tol_inv) == 0);
+#pragma unroll
+        for (int w = 0; w < W; ++w) ok = ok & ((x.lab[w][i] & k.mask[w]) == k.req[w]);
+        v0[i] = ok ? cap[i] : 0u;
+        v1[i] = (valid[i] && x.ex[i] != -1) ? 1u : 0u;
+    }
+    const uint32_t a0 = v0[0], a1 = a0 + v0[1], a2 = a1 + v0[2], a3 = a2 + v0[3];
+    const uint32_t b0 = v1[0], b1 = b0 + v1[1], b2 = b1 + v1[2], b3 = b2 + v1[3];
+    const uint32_t ia = wave_incl_scan(a3, lane), ib = wave_incl_scan(b3, lane);
+    const uint32_t wa = ia - a3, wb = ib - b3;
+    reinterpret_cast<JSP_LDS u32x4*>(s_pre)[tid] = u32x4{wa + a0, wa + a1, wa + a2, ia};
+    reinterpret_cast<JSP_LDS u32x4*>(s_pre + kChunkRows)[tid] = u32x4{wb + b0, wb + b1, wb + b2, ib};
+    if (lane == 63) {
+        s_wsum[wid] = ia;
+        s_wsum[kTallyWaves + wid] = ib;
+    }
+    __syncthreads();
+    if (!lf.live) return false;
+    const u32x4 va = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum);
+    const u32x4 vb = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum + kTallyWaves);
+    const uint4 wsa = make_uint4(va[0], va[1], va[2], va[3]), wsb = make_uint4(vb[0], vb[1], vb[2], vb[3]);
+    const uint32_t ha = s_pre[lf.xh], hb = s_pre[kChunkRows + lf.xh];
+    const uint32_t la = lf.has_lo ? s_pre[lf.xb] : 0u, lb = lf.has_lo ? s_pre[kChunkRows + lf.xb] : 0u;
+    const uint32_t capsum = (ha + wave_off(wsa, lf.wh)) - (lf.has_lo ? la + wave_off(wsa, lf.wb) : 0u);
+    const uint32_t occsum = (hb + wave_off(wsb, lf.wh)) - (lf.has_lo ? lb + wave_off(wsb, lf.wb) : 0u);
+    return capsum >= k.pods && occsum == 0u;
+}
+
 // The XCC vote of a co-located service (ServiceArgs::spread): workgroup
 // `slot` of n publishes its XCC id (tagged with the launch generation, so a
 // vote left by an earlier launch is not counted) and wave 0 reads all n:
@@ -2883,6 +3009,19 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
     // request) reloads them
     JSP_LDS u32x4* row_cache = v.row_cache_words ? lds_ptr(reinterpret_cast<u32x4*>(lds + v.row_cache_words)) : nullptr;
     bool cached = false;
+    // resident path: the tile's rows, class and leaf bounds held across requests
+    const bool resident = v.resident != 0u;
+    RowRegs<W, R> rows;
+    bool valid[4] = {false, false, false, false};
+    ResidentLeaf lf{0u, 0u, 0u, 0u, false, false};
+    ClassRegs<W, R> kreg{};
+    if (resident) {
+        lf = resident_leaf(a, bt);
+        kreg = class_regs_k<W, R>(*(const JSP_CONST DevClass*)a.cls);
+        const uint32_t row = (bt.z & ~3u) + 4u * threadIdx.x;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) valid[i] = row + i >= bt.z && row + i < bt.w;
+    }
     {
         constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
         const int tid = threadIdx.x;
@@ -2925,9 +3064,22 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         const bool use_cache = cached && (Jw >> 31) == 0u;
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
-        compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
-                                 v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local);
-        cached = row_cache != nullptr;
+        if (resident) {
+            if (!use_cache) {  // first request, or rows patched since the last one: from memory (sc1, no stale L1)
+                const uint32_t row = (bt.z & ~3u) + 4u * threadIdx.x;
+                load_rows<W, R, true>(a, row, row < bt.w && row + 3 >= bt.z, rows);
+            }
+            const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
+                                                lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
+            svc_stamp(clk, 2);
+            compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
+                           v.stats, v.err, true, s_x, clk, next, local);
+            cached = true;
+        } else {
+            compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
+                                     v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local);
+            cached = row_cache != nullptr;
+        }
         signal_host_clk(v.done + tile, next, clk, clk_out);
         // The host may patch the snapshot before its next request (another
         // launch): drop this CU's L1 lines now, off the request path -- no
@@ -3135,9 +3287,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         svc_stamp(clk, 1);
         tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), clk, row_cache, use_cache);
         cached = row_cache != nullptr;
-        svc_stamp(clk, 2);
+#ifndef JSP_AB_FINESTAMP
+    svc_stamp(clk, 2);
+#endif
         split_emit(ag, sp, bt, out, lds, s_x);
-        svc_stamp(clk, 4);
+#ifndef JSP_AB_FINESTAMP
+    svc_stamp(clk, 4);
+#endif
         signal_host_clk(v.done + tile, next, clk, clk_out);
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
@@ -3525,28 +3681,29 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
     return hipGetLastError();
 }
 
-static uint32_t level_wpl(uint32_t nw) {
-    const uint32_t w = (nw + 63u) / 64u;
-    return w <= 4u ? 4u : w <= 8u ? 8u : w <= 16u ? 16u : w <= 32u ? 32u : 0u;
+static uint32_t level_wpt(uint32_t nw) {
+    const uint32_t w = (nw + kLevelThreads - 1) / kLevelThreads;
+    return w <= 1u ? 1u : w <= 2u ? 2u : w <= 4u ? 4u : w <= 8u ? 8u : 0u;
 }
 
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
-    const uint32_t wpl = level_wpl(nw);
-    return wpl ? (size_t)C * 64u * (wpl + 1u) * 8u : 0u;
+    const uint32_t wpt = level_wpt(nw);
+    return wpt ? (size_t)C * kLevelThreads * wpt * 8u : 0u;
 }
 
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s) {
-    const uint32_t wpl = level_wpl(nw);
+    const uint32_t wpt = level_wpt(nw);
     const size_t lds = level_walk_lds_bytes(C, nw);
-    if (wpl == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
+    if (wpt == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
         return hipErrorInvalidValue;
-    switch (wpl) {
-        case 4: jsp_launch(assign_level_kernel<4>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        case 8: jsp_launch(assign_level_kernel<8>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        case 16: jsp_launch(assign_level_kernel<16>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        default: jsp_launch(assign_level_kernel<32>, dim3(1), dim3(256), (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+    const dim3 g(1), b(kLevelThreads);
+    switch (wpt) {
+        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
+        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
     }
     if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0) return e;
     // records: one per (run, word) that gives domains away; a class's runs

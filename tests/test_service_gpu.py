@@ -497,12 +497,15 @@ def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
     assert svc_engine.timing(reset=True).svc_starts == 0
 
 
+@pytest.mark.parametrize("resident", ["1", "0"])
 @pytest.mark.parametrize("xcd", ["1", "0"])
-def test_service_colocated_and_spread(svc_engine, monkeypatch, xcd):
+def test_service_colocated_and_spread(svc_engine, monkeypatch, xcd, resident):
     """The compaction service co-located on one XCD (plain bell and granule
     stores when every workgroup votes the same XCC id) and spread over the
-    chip (write-through): the same answers, across requests, patches and J."""
+    chip (write-through), with the tiles' rows held in registers (resident
+    path) or in LDS: the same answers, across requests, patches and J."""
     monkeypatch.setenv("JSP_SVC_XCD", xcd)  # read at each service start
+    monkeypatch.setenv("JSP_SVC_RESIDENT", resident)
     svc_engine.service_stop()
     p = synth.config2()
     svc_engine.load(p)

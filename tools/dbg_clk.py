@@ -20,8 +20,9 @@ for cfg in (1, 2):
     e.load(p)
     e.set_timing(True)
     call = e.host_placer(*job_runs(p.job_class))
-    for gap, xcd in ((0.0, "1"), (0.0, "0"), (0.001, "1"), (0.001, "0")):
+    for gap, xcd, res in ((0.0, "1", "1"), (0.0, "1", "0"), (0.0, "0", "1"), (0.0, "0", "0"), (0.001, "1", "1")):
         os.environ["JSP_SVC_XCD"] = xcd  # read at the service's start
+        os.environ["JSP_SVC_RESIDENT"] = res
         e.service_stop()
         rows = []
         for i in range(300):
@@ -44,13 +45,11 @@ for cfg in (1, 2):
         walls = []
         for i in range(300):
             t0 = time.perf_counter()
-            if gap:
-                pass
             e.set_timing(False) if i == 0 else None
             call()
             walls.append((time.perf_counter() - t0) * 1e6)
         e.set_timing(True)
-        line = f"cfg{cfg} xcd={xcd} gap {gap * 1e3:g} ms: wall(timing off) p50 {np.median(walls[20:]):.2f} us | bcast {m[0]:.2f} tallied {m[1]:.2f} scanned {m[2]:.2f} lookback {m[3]:.2f} drained {m[4]:.2f} us"
+        line = f"cfg{cfg} xcd={xcd} resident={res} gap {gap * 1e3:g} ms: wall(timing off) p50 {np.median(walls[20:]):.2f} us | bcast {m[0]:.2f} tallied {m[1]:.2f} scanned {m[2]:.2f} lookback {m[3]:.2f} drained {m[4]:.2f} us"
         if fq:
             line += f" | row+leaf pass clock {np.median(fq):.0f} MHz"
         print(line, flush=True)
