@@ -641,6 +641,28 @@ def main() -> None:
                                  "note": "device path (launch, device-resident runs and assign[]), HIP events "
                                          "around 200 back-to-back placements"},
                     "host_api_resident": host_api_latency(eng, pc, 200)}
+            if r.fused in (3, 5):
+                # the shipped shape's device time: the resident service's own
+                # per-request stamps (first tile saw the request -> last tile
+                # drained), its algorithmic bytes (the rows evaluated, the
+                # leaf offsets, what it hands back)
+                eng.set_timing(True)
+                cl = eng.host_placer(*job_runs(pc.job_class))
+                for _ in range(20):
+                    cl()
+                eng.timing(reset=True)
+                for _ in range(200):
+                    cl()
+                tsv = eng.timing(reset=True)
+                eng.set_timing(False)
+                dev_us = tsv.svc_us / max(tsv.svc_calls, 1)
+                sb = compact_bytes(pc) if r.fused == 3 else tally_bytes(pc)
+                line["service_roofline"] = {
+                    "bound": "hbm", "shape": SHAPES[r.fused], "request_us_device": round(dev_us, 3),
+                    "bytes_per_request": sb, "achieved": round(sb / (dev_us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(sb / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5), "requests": int(tsv.svc_calls),
+                    "note": "the host API's shape: in-kernel stamps per request (timing on), rows held on chip between "
+                            "requests; algorithmic bytes = the rows evaluated + leaf offsets + the outputs"}
             if cfg in (3, 5):
                 line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
                 line["host_api_cold_recovery"] = cold_recovery_latency(eng, pc, args.cold_trials // 2)

@@ -152,6 +152,10 @@ typedef struct jsp_timing {
                                   launch path instead. When its grid cannot be co-resident the service stays
                                   off until the next upload; otherwise the next call starts it again */
     double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
+    /* jsp_snapshot_patch (ABI v5), host wall clock, always accumulated */
+    uint64_t patches;          /* patch calls with at least one row */
+    double patch_us;           /* their host time, the service (re)start of svc_wake included */
+    double wake_us;            /* of which (re)starting the service for a coming recovery */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */

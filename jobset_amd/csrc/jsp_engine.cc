@@ -238,6 +238,7 @@ struct jsp_engine {
         bool start_failed = false;  // the last start never saw its dispatcher poll (-> broken)
         bool armed = false;   // the host API was answered by the service: a patch (re)starts it (svc_wake)
         unsigned long long zero_key = ~0ull;  // geometry the granule / bell lines were last zeroed for
+        unsigned long long layout_key = ~0ull;  // geometry the host-side slots / words were laid out for
         unsigned long long occ_key = ~0ull;   // (shape, LDS, grid) whose co-residency was last checked
         int occ_fit = 0;
         std::chrono::steady_clock::time_point last{};
@@ -809,6 +810,7 @@ int svc_suspend(jsp_engine* e) {
     e->svc.resume |= e->svc.running;
     e->svc.broken = false;  // new geometry: the service may fit again
     e->svc.zero_key = ~0ull;  // and its lines are zeroed again at the next start
+    e->svc.layout_key = ~0ull;
     return svc_stop(e);
 }
 
@@ -862,18 +864,31 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
         v.cap_runs = cr;
     }
     uint32_t n_tiles = nb;  // workgroups that answer (and write a done word), dispatcher excluded
+    // The host-side layout (split slots, the host walk's tile table, the done
+    // and stamp words) is rebuilt only when the geometry changes: every
+    // request rewrites the slots the walk reads, done words are compared with
+    // request numbers that never repeat, and the error word is acknowledged at
+    // its current value -- so a restart after an idle exit (a recovery's cold
+    // start) costs the launch alone.
     if (shape == 3) {
         v.groups = split_groups(e);
         v.cpg = (e->C + v.groups - 1) / v.groups;
         n_tiles = nb * v.groups;
-        const size_t sb = (size_t)n_tiles * (v.cpg + 1) * jsp::kSplitSlot * 8;
-        HIP_TRY(v.split.reserve(sb));
-        std::memset(v.split.p, 0, sb);
-        e->walk.set_tiles(e->blk_l0, e->blk_l1, v.groups, v.cpg);
     }
+    const unsigned long long lkey = ((unsigned long long)nb << 40) | ((unsigned long long)v.groups << 32) |
+                                    ((unsigned long long)v.cpg << 8) | (unsigned)shape;
     const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3;
-    HIP_TRY(v.words.reserve(nw * 4));
-    std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
+    if (v.layout_key != lkey || !v.words.p || nw * 4 > v.words.bytes) {
+        if (shape == 3) {
+            const size_t sb = (size_t)n_tiles * (v.cpg + 1) * jsp::kSplitSlot * 8;
+            HIP_TRY(v.split.reserve(sb));
+            std::memset(v.split.p, 0, sb);
+            e->walk.set_tiles(e->blk_l0, e->blk_l1, v.groups, v.cpg);
+        }
+        HIP_TRY(v.words.reserve(nw * 4));
+        std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
+        v.layout_key = lkey;
+    }
     HIP_TRY(v.box.reserve(64));
     const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
     // granules, then bell, counter, n_runs on lines of their own. Zeroed only
@@ -919,7 +934,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
     a.ready = ready;
     a.gen = v.gen;
-    v.err_ack = 0;
+    v.err_ack = __atomic_load_n(w + n_tiles + 2, __ATOMIC_ACQUIRE);  // an earlier instance's error is not ours
     {
         const char* c = std::getenv("JSP_SVC_EARLY");  // read per service start (in-process A/B)
         v.early = !(c && c[0] == '0');
@@ -1168,9 +1183,33 @@ void svc_wake(jsp_engine* e) {
     if (!on || !v.armed || !svc_ok(e)) return;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
     if (v.running && since <= 0.5 * svc_idle_ms()) return;  // up, and not about to idle out
+    // long idle (a recovery after hours): the service has left by itself and
+    // its stream is done -- a query, not a synchronize, tells; otherwise stop it
+    if (v.running && since > svc_idle_ms() + 5.0 && hipStreamQuery(v.stream) == hipSuccess) {
+        v.running = false;
+        v.pending = 0;
+        e->grave.flush();
+    }
     if (svc_stop(e) != JSP_OK || svc_start(e, 0, 0, false) != JSP_OK) {
         (void)svc_stop(e);  // the next jsp_place starts it (or answers on the launch path)
         g_err.clear();
+        return;
+    }
+    // A warm-up request (no jobs, rows marked patched): the fresh tiles load
+    // their rows, run every phase once and pull the kernel's code into the
+    // instruction caches while the deletions finish, so the recreate's
+    // request runs warm. Posted without waiting (the dispatcher finds it when
+    // it starts polling); the next request settles it first (svc_settle).
+    if (v.shape == 2 || v.shape == 3) {
+        const uint32_t seq = next_seq(v.seq);
+        v.seq = seq;
+        v.last = std::chrono::steady_clock::now();
+        __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)seq, __ATOMIC_RELEASE);
+        // rows marked patched, and they stay marked: the patch kernel may not
+        // have landed when the warm-up loads them, so the next request (which
+        // waits for the patch's completion word) loads them again
+        __atomic_store_n(v.box.as<unsigned long long>(), (0x80000000ull << 32) | seq, __ATOMIC_RELEASE);
+        v.pending = seq;
     }
 }
 
@@ -1692,6 +1731,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
                        const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner);
+    const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
     if (n == 0) return JSP_OK;
@@ -1745,7 +1785,13 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     // No wait here: later work is ordered after the patch -- launches by the
     // stream, service requests by the patch's completion word (patch_wait).
     svc_resume(e);
+    const auto t1 = std::chrono::steady_clock::now();
     svc_wake(e);
+    const auto t2 = std::chrono::steady_clock::now();
+    using us = std::chrono::duration<double, std::micro>;
+    e->acc.patches += 1;
+    e->acc.patch_us += us(t2 - t0).count();
+    e->acc.wake_us += us(t2 - t1).count();
     return JSP_OK;
 }
 

@@ -160,6 +160,23 @@ int main(int argc, char** argv) {
         std::fflush(stdout);
         k.halt();
     }
+    // 3. the launch call alone (host wall of hipLaunchKernel, no wait) after an idle gap
+    {
+        std::printf("{\"launch_call_only\": {");
+        for (int gi = 0; gi < 6; ++gi) {
+            std::vector<double> v;
+            for (int t = 0; t < trials; ++t) {
+                std::this_thread::sleep_for(std::chrono::microseconds((long)(gaps_ms[gi] * 1000)));
+                const auto t0 = clk::now();
+                hipLaunchKernelGGL(tiny, dim3(1), dim3(64), 0, s, d);
+                v.push_back(us_since(t0));
+                CK(hipStreamSynchronize(s));
+            }
+            std::printf("\"%gms\": %s%s", gaps_ms[gi], pct(v).c_str(), gi == 5 ? "" : ", ");
+            std::fflush(stdout);
+        }
+        std::printf("}}\n");
+    }
     CK(hipFree(d));
     return 0;
 }

@@ -22,7 +22,7 @@ call = e.host_placer(*job_runs(p.job_class))
 call()
 wake = os.environ.get("JSP_SVC_WAKE", "1")
 for gap in (0.0, 0.001, 0.01, 0.0):
-    pa, pl, starts = [], [], []
+    pa, pl, starts, wk = [], [], [], []
     for t in range(trials):
         row = np.array([(t * 7919) % p.nodes.n_nodes], dtype=np.uint32)
         patch = e.host_patcher(row, taints=p.nodes.taints[row])
@@ -38,9 +38,12 @@ for gap in (0.0, 0.001, 0.01, 0.0):
         t3 = time.perf_counter()
         pa.append((t1 - t0) * 1e6)
         pl.append((t3 - t2) * 1e6)
-        starts.append(e.timing(reset=True).svc_starts)
+        tm = e.timing(reset=True)
+        starts.append(tm.svc_starts)
+        wk.append(tm.wake_us)
     pa, pl = np.array(pa), np.array(pl)
     print(f"wake={wake} gap {gap * 1e3:g} ms: patch p50 {np.median(pa):.1f} p99 {np.percentile(pa, 99):.1f} | "
-          f"place p50 {np.median(pl):.1f} p99 {np.percentile(pl, 99):.1f} | starts/trial {np.mean(starts):.2f}",
+          f"place p50 {np.median(pl):.1f} p99 {np.percentile(pl, 99):.1f} | wake (in patch) p50 {np.median(wk):.1f} | "
+          f"starts/trial {np.mean(starts):.2f}",
           flush=True)
 e.service_stop()
