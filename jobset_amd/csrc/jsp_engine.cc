@@ -185,6 +185,9 @@ struct jsp_engine {
     unsigned long long patch_target = 0;
     uint32_t patch_seq = 0;
     bool patch_pending = false;
+    bool patch_svc = false;             // the pending patch goes to the service's dispatcher
+    bool patch_deferred = false;        // ... and is held back for the next request (not posted yet)
+    jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
     int fused_mode = JSP_FUSED_AUTO;
@@ -222,6 +225,7 @@ struct jsp_engine {
         DevBuf granules; // compaction granules | bell | counter | n_runs, one 128-B line each after the granules
         DevBuf tally;    // fused shape: the service's own cap[C][L] | occ[L] (device-path launches use e->cap)
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
+        HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
         uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
         uint32_t blocks = 0;           // row blocks the running service was started for
         uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
@@ -343,7 +347,10 @@ int wait_prior(jsp_engine* e, hipStream_t s) {
 // Order work on stream s after everything the engine enqueued before on
 // another stream (uploads and jsp_place use the engine stream, the device
 // entry points the caller's). Calls on one stream cost nothing here.
+int patch_fence(jsp_engine* e);
 int enter_stream(jsp_engine* e, hipStream_t s) {
+    // a patch the service applies is not stream-ordered: wait for its word
+    if (int rc = patch_fence(e)) return rc;
     if (e->have_last && e->last_stream != s)
         if (int rc = wait_prior(e, s)) return rc;
     if (s != e->stream && stream_mark_mode() == 0) jsp::set_launch_stop(e->ev_last);
@@ -792,8 +799,13 @@ int svc_shape(jsp_engine* e) {
 }
 bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
+int patch_wait(jsp_engine* e);
 int svc_stop(jsp_engine* e) {
     auto& v = e->svc;
+    // a patch posted to the dispatcher lands first (the stop word would
+    // replace its request; a later upload must not be patched over)
+    if (e->patch_pending && e->patch_svc)
+        if (int rc = patch_wait(e)) return rc;
     v.pending = 0;  // the stop waits for the kernel to leave, i.e. for every tile to finish
     if (!v.running) return JSP_OK;
     v.running = false;
@@ -920,6 +932,13 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.counter = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128);
     a.nruns = shape == 1 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 256) : nullptr;
     a.xcc = reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 384);
+    if (!v.pdesc.p) HIP_TRY(v.pdesc.reserve(sizeof(jsp::PatchDesc)));
+    if (!e->h_patch_done.p) {
+        HIP_TRY(e->h_patch_done.reserve(64));
+        std::memset(e->h_patch_done.p, 0, 64);
+    }
+    a.pdesc = v.pdesc.as<jsp::PatchDesc>();
+    a.pdone = e->h_patch_done.as<uint32_t>();
     // co-located compaction service: all its workgroups on one XCD when it
     // fits one (32 CUs, one workgroup per CU); JSP_SVC_XCD=0 spreads it (A/B)
     a.spread = shape == 2 && nb + 1 <= 32 && svc_xcd() ? 8u : 1u;
@@ -1150,12 +1169,48 @@ uint32_t next_seq(uint32_t q) {
     return s;
 }
 
+// Post a request word (second half first: the dispatcher reads both in one
+// 16-byte load and takes a torn read for none).
+void svc_post(jsp_engine* e, uint32_t seq, uint32_t jw, uint32_t n_runs) {
+    auto& v = e->svc;
+    __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq, __ATOMIC_RELEASE);
+    __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
+}
+
 // Wait for the last snapshot patch's completion word (the rows are then in
 // memory for every later reader, the resident tiles' `sc1` loads included).
+// A patch held back for the next request, posted on its own now (a service
+// that has left meanwhile is caught by patch_wait, and the patch kernel
+// applies it).
+void patch_post_deferred(jsp_engine* e) {
+    if (!e->patch_deferred) return;
+    e->patch_deferred = false;
+    auto& v = e->svc;
+    const uint32_t seq = next_seq(v.seq);
+    v.seq = seq;
+    v.last = std::chrono::steady_clock::now();
+    svc_post(e, seq, jsp::kReqPatch | jsp::kReqPatchOnly, 0);
+}
+
 int patch_wait(jsp_engine* e) {
     if (!e->patch_pending) return JSP_OK;
+    patch_post_deferred(e);
     const uint32_t* w = e->h_patch_done.as<uint32_t>();
     for (uint64_t spins = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) != e->patch_seq; ++spins) {
+        if ((spins & 255) == 0 && e->patch_svc) {
+            // posted to the dispatcher: if the service left without taking it
+            // (an idle exit racing the post), apply it with the patch kernel
+            const hipError_t q = hipStreamQuery(e->svc.stream);
+            if (q == hipErrorNotReady) continue;
+            if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == e->patch_seq) break;
+            e->svc.running = false;
+            e->patch_svc = false;
+            if (int rc = use_engine_stream(e)) return rc;
+            e->patch_target += (e->last_patch.n + 255) / 256;
+            e->last_patch.target = e->patch_target;
+            HIP_TRY(jsp::launch_patch(e->last_patch, e->stream));
+            continue;
+        }
         if ((spins & 255) == 0) {
             const hipError_t q = hipStreamQuery(e->stream);
             if (q == hipErrorNotReady) continue;
@@ -1166,8 +1221,23 @@ int patch_wait(jsp_engine* e) {
         }
     }
     e->patch_pending = false;
+    e->patch_svc = false;
     return JSP_OK;
 }
+
+// Launches that read the rows are stream-ordered after a patch kernel, but
+// not after a patch the service applies: they wait for its word first.
+int patch_fence(jsp_engine* e) { return e->patch_pending && e->patch_svc ? patch_wait(e) : JSP_OK; }
+
+// Whether patches go to the resident service's dispatcher (A/B:
+// JSP_SVC_PATCH=0 always the patch kernel; =2 posted at once rather than
+// carried by the next request). Read per call (in-process A/B).
+int svc_patch_mode() {
+    const char* v = std::getenv("JSP_SVC_PATCH");
+    return v && v[0] == '0' ? 0 : v && v[0] == '2' ? 2 : 1;
+}
+bool svc_patch_on() { return svc_patch_mode() != 0; }
+
 
 // A snapshot patch is the first sign of a recovery: the watch events of the
 // deleted Jobs' pods arrive while the reconciler deletes them in the
@@ -1177,24 +1247,41 @@ int patch_wait(jsp_engine* e) {
 // here without waiting: the GPU wakes from idle and the grid comes up while
 // the deletions finish, and the recreate's jsp_place finds it polling.
 // JSP_SVC_WAKE=0 turns this off (A/B).
-void svc_wake(jsp_engine* e) {
+// Whether a patch should (re)start the service: the host API has been
+// answered by it and it is not up (or about to idle out).
+bool svc_wake_wanted(jsp_engine* e) {
     static const bool on = [] { const char* v = std::getenv("JSP_SVC_WAKE"); return !(v && v[0] == '0'); }();
     auto& v = e->svc;
-    if (!on || !v.armed || !svc_ok(e)) return;
+    if (!on || !v.armed || !svc_ok(e)) return false;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
-    if (v.running && since <= 0.5 * svc_idle_ms()) return;  // up, and not about to idle out
-    // long idle (a recovery after hours): the service has left by itself and
-    // its stream is done -- a query, not a synchronize, tells; otherwise stop it
+    return !(v.running && since <= 0.5 * svc_idle_ms());
+}
+
+// (Re)start the service without waiting for its dispatcher to poll. Long
+// idle (a recovery after hours): the service has left by itself and its
+// stream is done -- a query, not a synchronize, tells; otherwise it is
+// stopped. On failure it stays stopped (the next jsp_place starts it, or
+// answers on the launch path) and the error is dropped.
+int svc_restart_quiet(jsp_engine* e) {
+    auto& v = e->svc;
+    const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
     if (v.running && since > svc_idle_ms() + 5.0 && hipStreamQuery(v.stream) == hipSuccess) {
         v.running = false;
         v.pending = 0;
         e->grave.flush();
     }
     if (svc_stop(e) != JSP_OK || svc_start(e, 0, 0, false) != JSP_OK) {
-        (void)svc_stop(e);  // the next jsp_place starts it (or answers on the launch path)
+        (void)svc_stop(e);
         g_err.clear();
-        return;
+        return JSP_EHIP;
     }
+    v.resume = false;
+    return JSP_OK;
+}
+
+void svc_wake(jsp_engine* e) {
+    auto& v = e->svc;
+    if (!svc_wake_wanted(e) || svc_restart_quiet(e) != JSP_OK) return;
     // A warm-up request (no jobs, rows marked patched): the fresh tiles load
     // their rows, run every phase once and pull the kernel's code into the
     // instruction caches while the deletions finish, so the recreate's
@@ -1217,12 +1304,17 @@ void svc_wake(jsp_engine* e) {
 int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
               int32_t* assign_out, uint32_t* placed) {
     auto& v = e->svc;
-    if (int rc = patch_wait(e)) return rc;  // the request's tiles must read the patched rows
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
                    (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
+    // the request's tiles must read the patched rows: a patch held back for
+    // the running service rides on this request (its dispatcher applies it
+    // before ringing the tiles); any other is waited for
+    bool carry = !restart && e->patch_deferred;
+    if (carry) e->patch_deferred = false;
+    else if (int rc = patch_wait(e)) return rc;
     // A cold start -- the first request after an idle exit (recoveries are
     // hours apart), an upload or a geometry change -- launches the service,
     // waits for its dispatcher to poll and posts to it. Measured after 60 ms
@@ -1265,7 +1357,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
                          __ATOMIC_RELEASE);
         // the compaction and split tiles keep their rows in LDS: bit 31 of J tells
         // them the snapshot was patched since their previous request (J < 2^30)
-        const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? 0x80000000u : 0u);
+        const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? jsp::kReqDirty : 0u) |
+                            (carry ? jsp::kReqPatch : 0u);
+        carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
         v.rows_dirty = false;
         __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
         const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
@@ -1742,8 +1836,8 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
-    if (int rc = use_engine_stream(e)) return rc;
-    // the delta into pinned staging, which the patch kernel reads in place
+    // the delta into pinned staging, which the patch kernel (or the service's
+    // dispatcher) reads in place
     const uint32_t W = e->W, R = e->R;
     const size_t off_lab = ((size_t)n * 4 + 7) & ~size_t(7), off_t = off_lab + (size_t)W * n * 8,
                  off_f = off_t + (size_t)n * 4, off_x = off_f + (size_t)R * n * 4, bytes = off_x + (size_t)n * 4;
@@ -1755,8 +1849,11 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (free_res) std::memcpy(hp + off_f, free_res, (size_t)R * n * 4);
     if (excl_owner) std::memcpy(hp + off_x, excl_owner, (size_t)n * 4);
     if (!e->patch_ctr.p) {
+        if (int rc = use_engine_stream(e)) return rc;
         HIP_TRY(e->patch_ctr.reserve(64));
         HIP_TRY(hipMemsetAsync(e->patch_ctr.p, 0, 64, s));
+    }
+    if (!e->h_patch_done.p) {
         HIP_TRY(e->h_patch_done.reserve(64));
         std::memset(e->h_patch_done.p, 0, 64);
     }
@@ -1775,18 +1872,57 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     a.freer = e->freer.as<uint32_t>();
     a.excl = e->excl.as<int32_t>();
     a.counter = e->patch_ctr.as<unsigned long long>();
-    e->patch_target += (n + 255) / 256;
-    a.target = e->patch_target;
     a.done = e->h_patch_done.as<uint32_t>();
     e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
     a.seq = e->patch_seq;
-    HIP_TRY(jsp::launch_patch(a, s));
-    e->patch_pending = true;
-    // No wait here: later work is ordered after the patch -- launches by the
-    // stream, service requests by the patch's completion word (patch_wait).
-    svc_resume(e);
+    e->last_patch = a;
+    // No wait here: later work is ordered after the patch -- service requests
+    // and (for a patch the service applies) launches by its completion word
+    // (patch_wait / patch_fence), other launches by the stream.
     const auto t1 = std::chrono::steady_clock::now();
-    svc_wake(e);
+    auto& v = e->svc;
+    const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
+    const bool up = v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    if (svc_patch_on() && up) {
+        // the service is up: its dispatcher applies the patch, no launch. It
+        // is held back for the next request, which carries it (no host-link
+        // round trip of its own); anything else that reads the rows first
+        // posts it alone and waits (patch_wait)
+        jsp::PatchDesc* d = v.pdesc.as<jsp::PatchDesc>();
+        *d = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
+        e->patch_pending = e->patch_svc = e->patch_deferred = true;
+        if (svc_patch_mode() == 2) patch_post_deferred(e);  // A/B: posted now, not carried
+    } else if (svc_patch_on() && svc_wake_wanted(e)) {
+        // a recovery's first patch after the service left: start it and let
+        // its dispatcher apply the patch, then run a warm-up request (no jobs)
+        // on the patched rows -- one launch; the recreate's request runs warm
+        if (svc_restart_quiet(e) == JSP_OK) {
+            jsp::PatchDesc* d = v.pdesc.as<jsp::PatchDesc>();
+            *d = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
+            const uint32_t seq = next_seq(v.seq);
+            v.seq = seq;
+            v.last = std::chrono::steady_clock::now();
+            const bool warm = v.shape == 2 || v.shape == 3;
+            svc_post(e, seq, jsp::kReqPatch | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly), 0);
+            if (warm) {
+                v.pending = seq;
+                v.rows_dirty = false;  // the warm-up loaded the patched rows
+            }
+            e->patch_pending = e->patch_svc = true;
+        }
+    }
+    if (!e->patch_pending) {
+        if (int rc = use_engine_stream(e)) return rc;
+        // the patch kernel's workgroups count up to the target (patches the
+        // service applied do not touch the counter)
+        e->patch_target += (n + 255) / 256;
+        a.target = e->patch_target;
+        HIP_TRY(jsp::launch_patch(a, s));
+        e->patch_pending = true;
+        e->patch_svc = false;
+        svc_resume(e);
+        svc_wake(e);
+    }
     const auto t2 = std::chrono::steady_clock::now();
     using us = std::chrono::duration<double, std::micro>;
     e->acc.patches += 1;
@@ -1944,7 +2080,7 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     const bool want_tally = (tally_out && e->C > 0) || occ_out;
     bool svc_after = false;  // a cold start: the service is launched after the launch path answers
-    if (!want_tally && svc_ok(e)) {
+    if (!want_tally && J < jsp::kReqPatchOnly && svc_ok(e)) {  // J and the request bits share a word
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
         const int src = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed);

@@ -152,6 +152,21 @@ struct CompactArgs {
 // word instead of a launch.
 constexpr uint32_t kSvcStop = 0xFFFFFFFFu;  // request word's low half: every workgroup leaves
 constexpr uint32_t kSvcClkSlots = 8;        // per tile: seen, acquired, tallied, scanned, looked back, drained
+// A snapshot patch the service's dispatcher applies (request bit kReqPatch):
+// host-mapped, written by the host before the request is posted.
+struct PatchDesc {
+    const uint32_t* rows;     // [n] row ids
+    const uint64_t* dlab;     // [W][n] or null
+    const uint32_t* dtaint;   // [n] or null
+    const uint32_t* dfree;    // [R][n] or null
+    const int32_t* dexcl;     // [n] or null
+    uint32_t n;
+    uint32_t seq;             // written to ServiceArgs::pdone once every row is in memory
+};
+// Request word bits above J (J < 2^29): 31 rows patched since the tiles'
+// previous request, 30 apply the staged patch first, 29 nothing behind it.
+constexpr uint32_t kReqDirty = 1u << 31, kReqPatch = 1u << 30, kReqPatchOnly = 1u << 29;
+
 struct ServiceArgs {
     const unsigned long long* mailbox;  // host-mapped 16 B: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; [1] first
     unsigned long long* granules;       // [n_blocks] the service's own look-back granules (tag = seq)
@@ -183,6 +198,8 @@ struct ServiceArgs {
     // registers between requests, its class in scalar registers and its
     // leaves' row bounds in registers (place_service_kernel's resident path)
     uint32_t resident;
+    const PatchDesc* pdesc;             // host-mapped patch descriptor (kReqPatch)
+    uint32_t* pdone;                    // host-mapped: the applied patch's seq
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

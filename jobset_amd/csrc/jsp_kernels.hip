@@ -2798,7 +2798,42 @@ __global__ __launch_bounds__(kTallyThreads) void place_compact_kernel(TallyArgs 
 // (one sc1 8-byte store, tag = seq), which the tiles poll close by. Only this
 // workgroup reads host memory: tiles polling it themselves see a request up
 // to a whole round trip apart and load the link with reads.
-__device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t* s_p, bool local = false) {
+// A snapshot patch the dispatcher applies itself (ServiceArgs::pdesc,
+// request bit kReqPatch): the whole workgroup overwrites the rows from the
+// staged delta in pinned memory with write-through stores, every wave
+// drains, and lane 0 publishes the patch's number in the host word -- no
+// launch per patch while the service is up, and none besides the service's
+// own when a patch wakes it.
+__device__ void service_apply_patch(const ServiceArgs& v, const TallyArgs& a) {
+    // the descriptor and the staged delta are rewritten by the host for every
+    // patch: drop what this CU's caches hold of the last one
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const PatchDesc* d = v.pdesc;
+    const uint32_t n = d->n;
+    for (uint32_t i = threadIdx.x; i < n; i += kTallyThreads) {
+        const uint32_t row = d->rows[i];
+        if (d->dlab)
+            for (int w = 0; w < a.W; ++w)
+                __hip_atomic_store(const_cast<uint64_t*>(a.labels) + (size_t)w * a.npad + row, d->dlab[(size_t)w * n + i],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d->dtaint)
+            __hip_atomic_store(const_cast<uint32_t*>(a.taints) + row, d->dtaint[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (d->dfree)
+            for (int r = 0; r < a.R; ++r)
+                __hip_atomic_store(const_cast<uint32_t*>(a.freer) + (size_t)r * a.npad + row, d->dfree[(size_t)r * n + i],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (d->dexcl)
+            __hip_atomic_store(const_cast<int32_t*>(a.excl) + row, d->dexcl[i], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(v.pdone, d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const TallyArgs& a, uint32_t* s_p,
+                                                 bool local = false) {
     const uint32_t w = threadIdx.x >> 6;
     uint32_t seq = v.seq0;
     if (threadIdx.x == 0) {
@@ -2827,15 +2862,20 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
                     break;
                 }
                 if (q != seq && q != 0 && x.z == q) {
-                    const unsigned long long m = ((unsigned long long)x.y << 32) | q;
-                    // n_runs first (the tail reads it after the bell), then ring at
-                    // once (the first wave to see it; a second ringer writes the same words)
-                    if (v.nruns) {
-                        __hip_atomic_store(v.nruns, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    if ((x.y & kReqPatch) == 0u) {
+                        const unsigned long long m = ((unsigned long long)x.y << 32) | q;
+                        // n_runs first (the tail reads it after the bell), then ring at
+                        // once (the first wave to see it; a second ringer writes the same words)
+                        if (v.nruns) {
+                            __hip_atomic_store(v.nruns, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        }
+                        if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    // a patch first: the whole workgroup applies it below, then rings
+                    __hip_atomic_store(s_p + 1, x.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_store(s_p + 3, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
@@ -2846,12 +2886,24 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, uint32_t*
             }
         }
         __syncthreads();
-        const uint32_t q = s_p[0];
+        const uint32_t q = s_p[0], jw = s_p[1], nr = s_p[3];
         if (q == 0) {  // stop or idle: every tile leaves too
             if (threadIdx.x == 0)
                 __hip_atomic_store(v.bell, ((unsigned long long)v.gen << 32) | kSvcStop, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             return;
+        }
+        if (jw & kReqPatch) {
+            service_apply_patch(v, a);  // ends with a barrier and the completion word
+            if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
+                const unsigned long long m = ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly)) << 32) | q;
+                if (v.nruns) {
+                    __hip_atomic_store(v.nruns, nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                }
+                if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         seq = q;
         // the next request comes only after every tile has answered this one
@@ -2992,7 +3044,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
     const uint32_t tile = blockIdx.x / (v.spread > 1 ? v.spread : 1u);
     const bool local = v.spread > 1 ? service_xcc_vote(v, tile, a.n_blocks + 1, s_x + 18) : false;
     if (tile == a.n_blocks) {
-        service_dispatch(v, s_x + 16, local);
+        service_dispatch(v, a, s_x + 16, local);
         return;
     }
     uint32_t seq = v.seq0;
@@ -3103,7 +3155,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(Tall
     const uint32_t tile = blockIdx.x;
     const uint32_t n_tiles = a.n_blocks * f.groups;
     if (tile == n_tiles) {
-        service_dispatch(v, lds);
+        service_dispatch(v, a, lds);
         return;
     }
     uint32_t* s_x = fused_flags(lds, a, f);  // [0] request seq [1] J [2] last-arriver flag
@@ -3236,7 +3288,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     const uint32_t n_tiles = a.n_blocks * sp.groups;
     uint32_t* s_x = lds + tally_lds_words((int)sp.cpg, (int)sp.cpg + 1, (int)a.la);  // [0] seq [4..16) scan [16..) prefixes
     if (tile == n_tiles) {
-        service_dispatch(v, s_x);
+        service_dispatch(v, a, s_x);
         return;
     }
     const FusedTile ft = fused_tile(tile, sp.groups, sp.cpg, sp.C);

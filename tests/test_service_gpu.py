@@ -476,6 +476,56 @@ def test_async_patch_sizes_then_place(svc_engine, n):
     np.testing.assert_array_equal(full.occ, occ)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("then", ["place", "tally_launch", "stop", "patch_again", "shared_rows"])
+def test_patch_applied_by_the_dispatcher(svc_engine, monkeypatch, mode, then):
+    """A patch while the service is up is applied by its dispatcher: held
+    back and carried by the next request (JSP_SVC_PATCH=1), posted at once
+    (=2), or the patch kernel (=0). Whatever reads the rows next -- the
+    service's next request, a launch (tallies out), a service stop, another
+    patch (of the same rows) -- sees every patched column, bit-exact."""
+    monkeypatch.setenv("JSP_SVC_PATCH", mode)
+    p = synth.config2()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused == 3
+    rng = np.random.default_rng(int(mode) * 10 + len(then))
+    R = p.nodes.free.shape[0]
+    rows0 = None
+    for k in range(3):
+        n = int(rng.integers(1, 3000))
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=n, replace=False)).astype(np.uint32)
+        if then == "shared_rows" and rows0 is not None:
+            rows = rows0
+            n = rows.shape[0]
+        rows0 = rows
+        taints = rng.integers(0, 2, size=n).astype(np.uint32)
+        free = rng.integers(0, 200_000, size=(R, n)).astype(np.uint32)
+        svc_engine.patch_rows(rows, taints=taints, free=free)
+        p.nodes.taints[rows] = taints
+        p.nodes.free[:, rows] = free
+        if then in ("patch_again", "shared_rows"):
+            excl = np.where(rng.random(n) < 0.05, 3, -1).astype(np.int32)
+            svc_engine.patch_rows(rows, excl=excl)
+            p.nodes.excl[rows] = excl
+        a, cap, occ = O.place_c(p)
+        if then == "tally_launch":
+            got = svc_engine.place(p.job_class, want_tally=True)
+            np.testing.assert_array_equal(got.cap, cap)
+            np.testing.assert_array_equal(got.occ, occ)
+        elif then == "stop":
+            svc_engine.service_stop()
+            got = svc_engine.place(p.job_class)
+        else:
+            got = svc_engine.place(p.job_class)
+            assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, a)
+    got = svc_engine.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+
+
 def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
     """Batched follower resolution / audits whose scratch outgrows its
     buffers while the service is resident: the old buffers wait for the

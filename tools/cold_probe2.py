@@ -21,12 +21,14 @@ e.load(p)
 call = e.host_placer(*job_runs(p.job_class))
 call()
 wake = os.environ.get("JSP_SVC_WAKE", "1")
-for gap in (0.0, 0.001, 0.01, 0.0):
+series = [(m, 0.06, g) for m in ("1", "0") for g in (0.0, 0.001, 0.01)] + [(m, 0.002, 0.0) for m in ("1", "2", "0")] * 2
+for mode, idle, gap in series:
+    os.environ["JSP_SVC_PATCH"] = mode  # read per call (in-process A/B: 1 carried, 2 posted, 0 patch kernel)
     pa, pl, starts, wk = [], [], [], []
     for t in range(trials):
         row = np.array([(t * 7919) % p.nodes.n_nodes], dtype=np.uint32)
         patch = e.host_patcher(row, taints=p.nodes.taints[row])
-        time.sleep(0.06)
+        time.sleep(idle)
         e.timing(reset=True)
         t0 = time.perf_counter()
         patch()
@@ -42,7 +44,7 @@ for gap in (0.0, 0.001, 0.01, 0.0):
         starts.append(tm.svc_starts)
         wk.append(tm.wake_us)
     pa, pl = np.array(pa), np.array(pl)
-    print(f"wake={wake} gap {gap * 1e3:g} ms: patch p50 {np.median(pa):.1f} p99 {np.percentile(pa, 99):.1f} | "
+    print(f"wake={wake} svc_patch={mode} idle {idle * 1e3:g} ms gap {gap * 1e3:g} ms: patch p50 {np.median(pa):.1f} p99 {np.percentile(pa, 99):.1f} | "
           f"place p50 {np.median(pl):.1f} p99 {np.percentile(pl, 99):.1f} | wake (in patch) p50 {np.median(wk):.1f} | "
           f"starts/trial {np.mean(starts):.2f}",
           flush=True)

@@ -24,12 +24,15 @@ def main():
         p = synth.CONFIGS[cfg]()
         eng.load(p)
         call = eng.host_placer(*job_runs(p.job_class))
-        for timed in (False, True):
+        for timed, patched in ((False, False), (True, False), (False, True), (True, True)):
             eng.set_timing(timed)
             for _ in range(100):
                 call()
             walls, phases = [], []
-            for _ in range(reps):
+            for r in range(reps):
+                if patched:  # one row rewritten with its own values: the tiles reload their rows
+                    row = np.array([(r * 7919) % p.nodes.n_nodes], dtype=np.uint32)
+                    eng.patch_rows(row, taints=p.nodes.taints[row])
                 t0 = time.perf_counter()
                 call()
                 walls.append((time.perf_counter() - t0) * 1e6)
@@ -38,7 +41,7 @@ def main():
                     ref = c[:, 0].min()
                     phases.append([(c[:, k].max() - ref) * 10 for k in (0, 1, 6, 7, 2, 3, 4, 5)])
             w = np.array(walls)
-            line = f"cfg{cfg} timing={'on ' if timed else 'off'}: wall p50 {np.median(w):.2f} us p99 {np.percentile(w, 99):.2f}"
+            line = f"cfg{cfg} timing={'on ' if timed else 'off'} patched={int(patched)}: wall p50 {np.median(w):.2f} us p99 {np.percentile(w, 99):.2f}"
             if timed:
                 ph = np.median(np.array(phases), axis=0)
                 line += " | device (ns from first tile seeing the request, slowest tile): " + " ".join(
