@@ -187,6 +187,9 @@ struct jsp_engine {
     bool patch_pending = false;
     bool patch_svc = false;             // the pending patch goes to the service's dispatcher
     bool patch_deferred = false;        // ... and is held back for the next request (not posted yet)
+    uint32_t patch_bits = 0;            // its request bits (kReqPatch, kReqPatchInline)
+    uint32_t patch_nf = 0;              // inline: n | column flags << 16 (the request's n_runs word)
+    uint32_t patch_req = 0;             // the request that posted it alone (0: none)
     jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
@@ -226,6 +229,7 @@ struct jsp_engine {
         DevBuf tally;    // fused shape: the service's own cap[C][L] | occ[L] (device-path launches use e->cap)
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
         HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
+        HostBuf pstage;  // inline patch staging (kReqPatchInline, jsp_internal.h)
         uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
         uint32_t blocks = 0;           // row blocks the running service was started for
         uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
@@ -934,11 +938,17 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.xcc = reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 384);
     if (!v.pdesc.p) HIP_TRY(v.pdesc.reserve(sizeof(jsp::PatchDesc)));
     if (!e->h_patch_done.p) {
-        HIP_TRY(e->h_patch_done.reserve(64));
-        std::memset(e->h_patch_done.p, 0, 64);
+        HIP_TRY(e->h_patch_done.reserve(128));
+        std::memset(e->h_patch_done.p, 0, 128);
     }
+    {
+        const size_t pb = jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, e->W, e->R).bytes;
+        if (pb > v.pstage.bytes) HIP_TRY(v.pstage.reserve(pb));  // not resident now: a free does not wait
+    }
+    a.pstage = v.pstage.as<const char>();
     a.pdesc = v.pdesc.as<jsp::PatchDesc>();
     a.pdone = e->h_patch_done.as<uint32_t>();
+    a.taken = e->h_patch_done.as<uint32_t>() + 16;  // its own line
     // co-located compaction service: all its workgroups on one XCD when it
     // fits one (32 CUs, one workgroup per CU); JSP_SVC_XCD=0 spreads it (A/B)
     a.spread = shape == 2 && nb + 1 <= 32 && svc_xcd() ? 8u : 1u;
@@ -1189,7 +1199,8 @@ void patch_post_deferred(jsp_engine* e) {
     const uint32_t seq = next_seq(v.seq);
     v.seq = seq;
     v.last = std::chrono::steady_clock::now();
-    svc_post(e, seq, jsp::kReqPatch | jsp::kReqPatchOnly, 0);
+    svc_post(e, seq, e->patch_bits | jsp::kReqPatchOnly, e->patch_nf);
+    e->patch_req = seq;
 }
 
 int patch_wait(jsp_engine* e) {
@@ -1229,12 +1240,17 @@ int patch_wait(jsp_engine* e) {
 // not after a patch the service applies: they wait for its word first.
 int patch_fence(jsp_engine* e) { return e->patch_pending && e->patch_svc ? patch_wait(e) : JSP_OK; }
 
-// Whether patches go to the resident service's dispatcher (A/B:
-// JSP_SVC_PATCH=0 always the patch kernel; =2 posted at once rather than
-// carried by the next request). Read per call (in-process A/B).
+// How patches reach the resident service's dispatcher. 2 (default): posted
+// at once, so the dispatcher applies them during the gap before the next
+// request (a recovery's deletions take milliseconds), and a request posted
+// before the patch's completion word came back carries it again (applying a
+// staged patch twice writes the same values; the request may have replaced
+// the patch's own in the mailbox). 1: held back and carried by the next
+// request only. 0: always the patch kernel. JSP_SVC_PATCH, read per call
+// (in-process A/B).
 int svc_patch_mode() {
     const char* v = std::getenv("JSP_SVC_PATCH");
-    return v && v[0] == '0' ? 0 : v && v[0] == '2' ? 2 : 1;
+    return v && v[0] == '0' ? 0 : v && v[0] == '1' ? 1 : 2;
 }
 bool svc_patch_on() { return svc_patch_mode() != 0; }
 
@@ -1312,9 +1328,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     // the request's tiles must read the patched rows: a patch held back for
     // the running service rides on this request (its dispatcher applies it
     // before ringing the tiles); any other is waited for
-    bool carry = !restart && e->patch_deferred;
-    if (carry) e->patch_deferred = false;
-    else if (int rc = patch_wait(e)) return rc;
+    bool carry = !restart && e->patch_pending && e->patch_svc;
+    if (!carry)
+        if (int rc = patch_wait(e)) return rc;
     // A cold start -- the first request after an idle exit (recoveries are
     // hours apart), an upload or a geometry change -- launches the service,
     // waits for its dispatcher to poll and posts to it. Measured after 60 ms
@@ -1336,6 +1352,14 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         if (int rc = svc_wait_ready(e)) return rc;
         if (int rc = svc_settle(e)) return rc;
     }
+    if (carry) {  // held back, or posted and its completion word not back yet
+        // (a posted patch the dispatcher has taken is applied before it takes
+        // this request: no need to carry it again)
+        const uint32_t* pw = e->h_patch_done.as<uint32_t>();
+        carry = e->patch_deferred || (__atomic_load_n(pw, __ATOMIC_ACQUIRE) != e->patch_seq &&
+                                      __atomic_load_n(pw + 16, __ATOMIC_ACQUIRE) != e->patch_req);
+        e->patch_deferred = false;
+    }
     // the compaction answer is read from its tagged entries (timing on: the
     // done words, which carry the per-tile stamps)
     const bool early = shape == 2 && J > 0 && !e->timing && v.early;
@@ -1352,13 +1376,16 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         seq = next_seq(v.seq);
         v.seq = seq;
         v.last = std::chrono::steady_clock::now();
-        // second half first: the dispatcher reads both halves in one 16-byte load
-        __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq,
+        // second half first: the dispatcher reads both halves in one 16-byte
+        // load (an inline patch carried here: its n | flags in place of n_runs,
+        // which only the fused shape reads and which never carries one inline)
+        const uint32_t w2 = carry && (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : n_runs;
+        __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)w2 << 32) | seq,
                          __ATOMIC_RELEASE);
         // the compaction and split tiles keep their rows in LDS: bit 31 of J tells
         // them the snapshot was patched since their previous request (J < 2^30)
         const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? jsp::kReqDirty : 0u) |
-                            (carry ? jsp::kReqPatch : 0u);
+                            (carry ? e->patch_bits : 0u);
         carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
         v.rows_dirty = false;
         __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
@@ -1836,82 +1863,98 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
-    // the delta into pinned staging, which the patch kernel (or the service's
-    // dispatcher) reads in place
+    auto& v = e->svc;
+    // Who applies it: the running service's dispatcher (held back for the next
+    // request, which carries it -- no host-link round trip of its own; whatever
+    // else reads the rows first posts it alone and waits, patch_wait); after
+    // the service left, a recovery's first patch restarts it at once (its grid
+    // comes up while the delta is staged) and the dispatcher applies it
+    // followed by a warm-up request; otherwise the patch kernel.
+    const auto t1 = std::chrono::steady_clock::now();
+    const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
+    const bool up = svc_patch_on() && v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    const bool wake = !up && svc_patch_on() && svc_wake_wanted(e) && svc_restart_quiet(e) == JSP_OK;
+    const auto t1w = std::chrono::steady_clock::now();
+    // The delta into pinned staging, read in place. Patches for the service
+    // of up to kPatchInlineRows rows go to its fixed inline buffer (layout
+    // from n and the column flags, which ride in the request); larger ones,
+    // and the patch kernel's, to the engine's staging through a descriptor.
     const uint32_t W = e->W, R = e->R;
-    const size_t off_lab = ((size_t)n * 4 + 7) & ~size_t(7), off_t = off_lab + (size_t)W * n * 8,
-                 off_f = off_t + (size_t)n * 4, off_x = off_f + (size_t)R * n * 4, bytes = off_x + (size_t)n * 4;
-    HIP_TRY(e->h_patch.reserve(bytes, grave(e)));
-    char* hp = static_cast<char*>(e->h_patch.p);
-    std::memcpy(hp, rows, (size_t)n * 4);
-    if (labels) std::memcpy(hp + off_lab, labels, (size_t)W * n * 8);
-    if (taints) std::memcpy(hp + off_t, taints, (size_t)n * 4);
-    if (free_res) std::memcpy(hp + off_f, free_res, (size_t)R * n * 4);
-    if (excl_owner) std::memcpy(hp + off_x, excl_owner, (size_t)n * 4);
+    const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
+                        (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
+    const bool inl = (up || wake) && n <= jsp::kPatchInlineRows && v.shape != 1 && v.pstage.p;
+    const jsp::PatchInlineLayout L = jsp::patch_inline_layout(n, inl ? fl : 15u, W, R);
+    char* hp;
+    size_t base = 0;
+    if (inl) {
+        hp = static_cast<char*>(v.pstage.p);
+    } else {
+        base = 64;  // the same layout without its header
+        HIP_TRY(e->h_patch.reserve(L.bytes, grave(e)));
+        hp = static_cast<char*>(e->h_patch.p) - base;
+    }
+    std::memcpy(hp + L.rows, rows, (size_t)n * 4);
+    if (labels) std::memcpy(hp + L.lab, labels, (size_t)W * n * 8);
+    if (taints) std::memcpy(hp + L.taint, taints, (size_t)n * 4);
+    if (free_res) std::memcpy(hp + L.free, free_res, (size_t)R * n * 4);
+    if (excl_owner) std::memcpy(hp + L.excl, excl_owner, (size_t)n * 4);
     if (!e->patch_ctr.p) {
         if (int rc = use_engine_stream(e)) return rc;
         HIP_TRY(e->patch_ctr.reserve(64));
         HIP_TRY(hipMemsetAsync(e->patch_ctr.p, 0, 64, s));
     }
     if (!e->h_patch_done.p) {
-        HIP_TRY(e->h_patch_done.reserve(64));
-        std::memset(e->h_patch_done.p, 0, 64);
+        HIP_TRY(e->h_patch_done.reserve(128));
+        std::memset(e->h_patch_done.p, 0, 128);
     }
+    e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
+    if (inl) __atomic_store_n(reinterpret_cast<uint32_t*>(hp), e->patch_seq, __ATOMIC_RELAXED);  // header
     jsp::PatchArgs a{};
-    a.rows = reinterpret_cast<const uint32_t*>(hp);
+    a.rows = reinterpret_cast<const uint32_t*>(hp + L.rows);
     a.n = n;
     a.npad = e->npad;
     a.W = W;
     a.R = R;
-    a.dlab = labels ? reinterpret_cast<const uint64_t*>(hp + off_lab) : nullptr;
-    a.dtaint = taints ? reinterpret_cast<const uint32_t*>(hp + off_t) : nullptr;
-    a.dfree = free_res ? reinterpret_cast<const uint32_t*>(hp + off_f) : nullptr;
-    a.dexcl = excl_owner ? reinterpret_cast<const int32_t*>(hp + off_x) : nullptr;
+    a.dlab = labels ? reinterpret_cast<const uint64_t*>(hp + L.lab) : nullptr;
+    a.dtaint = taints ? reinterpret_cast<const uint32_t*>(hp + L.taint) : nullptr;
+    a.dfree = free_res ? reinterpret_cast<const uint32_t*>(hp + L.free) : nullptr;
+    a.dexcl = excl_owner ? reinterpret_cast<const int32_t*>(hp + L.excl) : nullptr;
     a.labels = e->labels.as<uint64_t>();
     a.taints = e->taints.as<uint32_t>();
     a.freer = e->freer.as<uint32_t>();
     a.excl = e->excl.as<int32_t>();
     a.counter = e->patch_ctr.as<unsigned long long>();
     a.done = e->h_patch_done.as<uint32_t>();
-    e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
     a.seq = e->patch_seq;
     e->last_patch = a;
-    // No wait here: later work is ordered after the patch -- service requests
-    // and (for a patch the service applies) launches by its completion word
-    // (patch_wait / patch_fence), other launches by the stream.
-    const auto t1 = std::chrono::steady_clock::now();
-    auto& v = e->svc;
-    const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
-    const bool up = v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
-    if (svc_patch_on() && up) {
-        // the service is up: its dispatcher applies the patch, no launch. It
-        // is held back for the next request, which carries it (no host-link
-        // round trip of its own); anything else that reads the rows first
-        // posts it alone and waits (patch_wait)
-        jsp::PatchDesc* d = v.pdesc.as<jsp::PatchDesc>();
-        *d = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
-        e->patch_pending = e->patch_svc = e->patch_deferred = true;
-        if (svc_patch_mode() == 2) patch_post_deferred(e);  // A/B: posted now, not carried
-    } else if (svc_patch_on() && svc_wake_wanted(e)) {
-        // a recovery's first patch after the service left: start it and let
-        // its dispatcher apply the patch, then run a warm-up request (no jobs)
-        // on the patched rows -- one launch; the recreate's request runs warm
-        if (svc_restart_quiet(e) == JSP_OK) {
-            jsp::PatchDesc* d = v.pdesc.as<jsp::PatchDesc>();
-            *d = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
-            const uint32_t seq = next_seq(v.seq);
-            v.seq = seq;
-            v.last = std::chrono::steady_clock::now();
-            const bool warm = v.shape == 2 || v.shape == 3;
-            svc_post(e, seq, jsp::kReqPatch | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly), 0);
-            if (warm) {
-                v.pending = seq;
-                v.rows_dirty = false;  // the warm-up loaded the patched rows
-            }
-            e->patch_pending = e->patch_svc = true;
-        }
+    e->patch_bits = jsp::kReqPatch | (inl ? jsp::kReqPatchInline : 0u);
+    e->patch_req = 0;
+    e->patch_nf = inl ? (n | fl << 16) : 0u;
+    if (up || wake) {
+        if (!inl) *v.pdesc.as<jsp::PatchDesc>() = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
+        e->patch_pending = e->patch_svc = true;
     }
-    if (!e->patch_pending) {
+    // No wait here: later work is ordered after the patch -- service requests
+    // and launches by its completion word (patch_wait / patch_fence), or by
+    // the stream for the patch kernel.
+    if (up) {
+        e->patch_deferred = true;
+        if (svc_patch_mode() == 2) patch_post_deferred(e);  // posted now (svc_patch_mode)
+    } else if (wake) {
+        // the patch, then a warm-up request (no jobs) on the patched rows: the
+        // fresh tiles load them and pull the code into the instruction caches
+        // while the deletions finish, so the recreate's request runs warm
+        const uint32_t seq = next_seq(v.seq);
+        v.seq = seq;
+        v.last = std::chrono::steady_clock::now();
+        const bool warm = v.shape == 2 || v.shape == 3;
+        svc_post(e, seq, e->patch_bits | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly), e->patch_nf);
+        e->patch_req = seq;
+        if (warm) {
+            v.pending = seq;
+            v.rows_dirty = false;  // the warm-up loaded the patched rows
+        }
+    } else {
         if (int rc = use_engine_stream(e)) return rc;
         // the patch kernel's workgroups count up to the target (patches the
         // service applied do not touch the counter)
@@ -1927,7 +1970,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     using us = std::chrono::duration<double, std::micro>;
     e->acc.patches += 1;
     e->acc.patch_us += us(t2 - t0).count();
-    e->acc.wake_us += us(t2 - t1).count();
+    e->acc.wake_us += us(wake ? t1w - t1 : t2 - t1).count();
     return JSP_OK;
 }
 
@@ -2080,7 +2123,7 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     const bool want_tally = (tally_out && e->C > 0) || occ_out;
     bool svc_after = false;  // a cold start: the service is launched after the launch path answers
-    if (!want_tally && J < jsp::kReqPatchOnly && svc_ok(e)) {  // J and the request bits share a word
+    if (!want_tally && J < jsp::kReqPatchInline && svc_ok(e)) {  // J and the request bits share a word
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
         const int src = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed);

@@ -163,9 +163,37 @@ struct PatchDesc {
     uint32_t n;
     uint32_t seq;             // written to ServiceArgs::pdone once every row is in memory
 };
-// Request word bits above J (J < 2^29): 31 rows patched since the tiles'
-// previous request, 30 apply the staged patch first, 29 nothing behind it.
-constexpr uint32_t kReqDirty = 1u << 31, kReqPatch = 1u << 30, kReqPatchOnly = 1u << 29;
+// Request word bits above J (J < 2^28): 31 rows patched since the tiles'
+// previous request, 30 apply the staged patch first, 29 nothing behind it,
+// 28 the patch is inline (below) and the request's n_runs word is
+// n | column flags << 16.
+constexpr uint32_t kReqDirty = 1u << 31, kReqPatch = 1u << 30, kReqPatchOnly = 1u << 29,
+                   kReqPatchInline = 1u << 28;
+// Inline patch staging (ServiceArgs::pstage, host-mapped, one fixed buffer per
+// service): a 64-B header {seq}, then rows[n], then (8-B aligned) the present
+// columns in the order labels [W][n] u64, taints [n], free [R][n], excl [n].
+// Its layout follows from n and the flags alone, so the dispatcher issues
+// every load of a patch at once -- one host-link round trip, no pointer chase.
+constexpr uint32_t kPatchInlineRows = 4096;
+constexpr uint32_t kPatchLab = 1, kPatchTaint = 2, kPatchFree = 4, kPatchExcl = 8;
+struct PatchInlineLayout {
+    size_t rows, lab, taint, free, excl, bytes;
+};
+__host__ __device__ inline PatchInlineLayout patch_inline_layout(uint32_t n, uint32_t flags, uint32_t W, uint32_t R) {
+    PatchInlineLayout L{};
+    L.rows = 64;
+    size_t o = (64 + (size_t)n * 4 + 7) & ~size_t(7);
+    L.lab = o;
+    if (flags & kPatchLab) o += (size_t)W * n * 8;
+    L.taint = o;
+    if (flags & kPatchTaint) o += (size_t)n * 4;
+    L.free = o;
+    if (flags & kPatchFree) o += (size_t)R * n * 4;
+    L.excl = o;
+    if (flags & kPatchExcl) o += (size_t)n * 4;
+    L.bytes = o;
+    return L;
+}
 
 struct ServiceArgs {
     const unsigned long long* mailbox;  // host-mapped 16 B: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; [1] first
@@ -199,7 +227,9 @@ struct ServiceArgs {
     // leaves' row bounds in registers (place_service_kernel's resident path)
     uint32_t resident;
     const PatchDesc* pdesc;             // host-mapped patch descriptor (kReqPatch)
+    const char* pstage;                 // host-mapped inline patch staging (kReqPatchInline)
     uint32_t* pdone;                    // host-mapped: the applied patch's seq
+    uint32_t* taken;                    // host-mapped: the seq of the request the dispatcher took last
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

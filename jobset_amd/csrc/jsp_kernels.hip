@@ -2832,6 +2832,50 @@ __device__ void service_apply_patch(const ServiceArgs& v, const TallyArgs& a) {
     if (threadIdx.x == 0) __hip_atomic_store(v.pdone, d->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The inline form: n and the column flags come with the request, the layout
+// follows from them, so each thread issues every load of its rows (and lane 0
+// the header) before the first store -- one round trip over the host link.
+__device__ void service_apply_inline(const ServiceArgs& v, const TallyArgs& a, uint32_t nf) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const uint32_t n = nf & 0xFFFFu, fl = nf >> 16;
+    const PatchInlineLayout L = patch_inline_layout(n, fl, (uint32_t)a.W, (uint32_t)a.R);
+    const char* b = v.pstage;
+    uint32_t seq = 0;
+    if (threadIdx.x == 0) seq = *reinterpret_cast<const uint32_t*>(b);
+    for (uint32_t i = threadIdx.x; i < n; i += kTallyThreads) {
+        const uint32_t row = reinterpret_cast<const uint32_t*>(b + L.rows)[i];
+        uint64_t lab[4];
+        uint32_t fr[4];
+        uint32_t tn = 0;
+        int32_t ex = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if ((fl & kPatchLab) && w < a.W) lab[w] = reinterpret_cast<const uint64_t*>(b + L.lab)[(size_t)w * n + i];
+        if (fl & kPatchTaint) tn = reinterpret_cast<const uint32_t*>(b + L.taint)[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if ((fl & kPatchFree) && r < a.R) fr[r] = reinterpret_cast<const uint32_t*>(b + L.free)[(size_t)r * n + i];
+        if (fl & kPatchExcl) ex = reinterpret_cast<const int32_t*>(b + L.excl)[i];
+#pragma unroll
+        for (int w = 0; w < 4; ++w)
+            if ((fl & kPatchLab) && w < a.W)
+                __hip_atomic_store(const_cast<uint64_t*>(a.labels) + (size_t)w * a.npad + row, lab[w], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (fl & kPatchTaint)
+            __hip_atomic_store(const_cast<uint32_t*>(a.taints) + row, tn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if ((fl & kPatchFree) && r < a.R)
+                __hip_atomic_store(const_cast<uint32_t*>(a.freer) + (size_t)r * a.npad + row, fr[r], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (fl & kPatchExcl)
+            __hip_atomic_store(const_cast<int32_t*>(a.excl) + row, ex, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(v.pdone, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const TallyArgs& a, uint32_t* s_p,
                                                  bool local = false) {
     const uint32_t w = threadIdx.x >> 6;
@@ -2873,7 +2917,10 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                         if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    // a patch first: the whole workgroup applies it below, then rings
+                    // a patch first: the whole workgroup applies it below, then
+                    // rings. The host learns that the request was taken (a later
+                    // request then need not carry the patch again).
+                    if (x.y & kReqPatch) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     __hip_atomic_store(s_p + 1, x.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(s_p + 3, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -2894,9 +2941,12 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             return;
         }
         if (jw & kReqPatch) {
-            service_apply_patch(v, a);  // ends with a barrier and the completion word
+            // each ends with a barrier and the completion word
+            if (jw & kReqPatchInline) service_apply_inline(v, a, nr);
+            else service_apply_patch(v, a);
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
-                const unsigned long long m = ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly)) << 32) | q;
+                const unsigned long long m =
+                    ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
                 if (v.nruns) {
                     __hip_atomic_store(v.nruns, nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -439,7 +439,7 @@ def test_patch_wakes_the_service(svc_engine):
     np.testing.assert_array_equal(got.assign, a)
 
 
-@pytest.mark.parametrize("n", [1, 255, 256, 257, 5000, 14999])
+@pytest.mark.parametrize("n", [1, 255, 256, 257, 4095, 4096, 4097, 5000, 14999])
 def test_async_patch_sizes_then_place(svc_engine, n):
     """The patch kernel reads the delta from pinned memory and its last
     workgroup publishes the completion word the next service request waits
@@ -480,9 +480,10 @@ def test_async_patch_sizes_then_place(svc_engine, n):
 @pytest.mark.parametrize("mode", ["1", "2", "0"])
 @pytest.mark.parametrize("then", ["place", "tally_launch", "stop", "patch_again", "shared_rows"])
 def test_patch_applied_by_the_dispatcher(svc_engine, monkeypatch, mode, then):
-    """A patch while the service is up is applied by its dispatcher: held
-    back and carried by the next request (JSP_SVC_PATCH=1), posted at once
-    (=2), or the patch kernel (=0). Whatever reads the rows next -- the
+    """A patch while the service is up is applied by its dispatcher: posted
+    at once and carried again by a request that finds it not yet applied
+    (JSP_SVC_PATCH=2, the default), held back and carried by the next request
+    (=1), or the patch kernel (=0). Whatever reads the rows next -- the
     service's next request, a launch (tallies out), a service stop, another
     patch (of the same rows) -- sees every patched column, bit-exact."""
     monkeypatch.setenv("JSP_SVC_PATCH", mode)

@@ -21,7 +21,7 @@ e.load(p)
 call = e.host_placer(*job_runs(p.job_class))
 call()
 wake = os.environ.get("JSP_SVC_WAKE", "1")
-series = [(m, 0.06, g) for m in ("1", "0") for g in (0.0, 0.001, 0.01)] + [(m, 0.002, 0.0) for m in ("1", "2", "0")] * 2
+series = [(m, 0.06, g) for m in ("1", "0") for g in (0.0, 0.001, 0.01)] + [(m, 0.002, g) for g in (0.0, 0.001) for m in ("1", "2", "0")] * 2
 for mode, idle, gap in series:
     os.environ["JSP_SVC_PATCH"] = mode  # read per call (in-process A/B: 1 carried, 2 posted, 0 patch kernel)
     pa, pl, starts, wk = [], [], [], []
