@@ -9,8 +9,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <condition_variable>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/jsplace.h"
@@ -190,6 +192,15 @@ struct jsp_engine {
     uint32_t patch_bits = 0;            // its request bits (kReqPatch, kReqPatchInline)
     uint32_t patch_nf = 0;              // inline: n | column flags << 16 (the request's n_runs word)
     uint32_t patch_req = 0;             // the request that posted it alone (0: none)
+    // The waker: a host thread that restarts the service for a recovery's
+    // first patch off the caller's thread (the launch after an idle period
+    // costs ~10 us of host time). wake_job is guarded by mu; the thread
+    // sleeps on wake_cv (wake_ring / wake_quit under wake_mu).
+    bool wake_job = false;
+    std::thread waker;
+    std::mutex wake_mu;
+    std::condition_variable wake_cv;
+    bool wake_ring = false, wake_quit = false;
     jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
@@ -807,8 +818,8 @@ int patch_wait(jsp_engine* e);
 int svc_stop(jsp_engine* e) {
     auto& v = e->svc;
     // a patch posted to the dispatcher lands first (the stop word would
-    // replace its request; a later upload must not be patched over)
-    if (e->patch_pending && e->patch_svc)
+    // replace its request); one held back stays so (patch_wait applies it)
+    if (e->patch_pending && e->patch_svc && !e->patch_deferred)
         if (int rc = patch_wait(e)) return rc;
     v.pending = 0;  // the stop waits for the kernel to leave, i.e. for every tile to finish
     if (!v.running) return JSP_OK;
@@ -823,6 +834,8 @@ int svc_stop(jsp_engine* e) {
 // it again at their end when it was running, so the next jsp_place -- the
 // recovery path: post-delete snapshot uploaded, then placed -- finds it ready.
 int svc_suspend(jsp_engine* e) {
+    // every patch lands before an upload replaces what it patched
+    if (int rc = patch_wait(e)) return rc;
     e->svc.resume |= e->svc.running;
     e->svc.broken = false;  // new geometry: the service may fit again
     e->svc.zero_key = ~0ull;  // and its lines are zeroed again at the next start
@@ -1205,6 +1218,16 @@ void patch_post_deferred(jsp_engine* e) {
 
 int patch_wait(jsp_engine* e) {
     if (!e->patch_pending) return JSP_OK;
+    e->wake_job = false;  // a reader other than a placement: no wake, the patch lands now
+    if (e->patch_deferred && !e->svc.running) {
+        // held back for a service that is not up: the patch kernel applies it
+        e->patch_deferred = false;
+        e->patch_svc = false;
+        if (int rc = use_engine_stream(e)) return rc;
+        e->patch_target += (e->last_patch.n + 255) / 256;
+        e->last_patch.target = e->patch_target;
+        HIP_TRY(jsp::launch_patch(e->last_patch, e->stream));
+    }
     patch_post_deferred(e);
     const uint32_t* w = e->h_patch_done.as<uint32_t>();
     for (uint64_t spins = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) != e->patch_seq; ++spins) {
@@ -1316,10 +1339,78 @@ void svc_wake(jsp_engine* e) {
     }
 }
 
+// The waker's job (or the next caller's, whichever takes the engine lock
+// first): restart the service, post the held-back patch and, for the tile
+// shapes, a warm-up request (no jobs) behind it -- the fresh tiles load the
+// patched rows and pull the code into the instruction caches while the
+// deletions finish, so the recreate's request runs warm. A patch already
+// taken care of (patch_wait) leaves nothing to do; a start that fails
+// leaves the patch held back, and patch_wait hands it to the patch kernel.
+void run_wake(jsp_engine* e) {
+    if (!e->wake_job) return;
+    e->wake_job = false;
+    if (!(e->patch_pending && e->patch_svc && e->patch_deferred)) return;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (svc_restart_quiet(e) != JSP_OK) return;
+    auto& v = e->svc;
+    const uint32_t seq = next_seq(v.seq);
+    v.seq = seq;
+    v.last = std::chrono::steady_clock::now();
+    const bool warm = v.shape == 2 || v.shape == 3;
+    const bool inl = (e->patch_bits & jsp::kReqPatchInline) != 0;
+    if (inl && v.shape == 1) {  // staged inline for a tile shape; the fused shape's n_runs word is taken
+        e->patch_bits &= ~jsp::kReqPatchInline;
+        const jsp::PatchArgs& a = e->last_patch;
+        *v.pdesc.as<jsp::PatchDesc>() = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, a.n, a.seq};
+    }
+    svc_post(e, seq, e->patch_bits | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly),
+             (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : 0u);
+    e->patch_req = seq;
+    e->patch_deferred = false;
+    if (warm) {
+        v.pending = seq;
+        v.rows_dirty = false;  // the warm-up loads the patched rows
+    }
+    e->acc.wake_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void waker_main(jsp_engine* e) {
+    (void)hipSetDevice(e->device);
+    for (;;) {
+        {
+            std::unique_lock<std::mutex> l(e->wake_mu);
+            e->wake_cv.wait(l, [e] { return e->wake_ring || e->wake_quit; });
+            if (e->wake_quit) return;
+            e->wake_ring = false;
+        }
+        std::lock_guard<std::mutex> g(e->mu);
+        run_wake(e);
+    }
+}
+
+// Hand the wake to the waker thread (started on first use; JSP_SVC_WAKER=0:
+// the caller runs it inline, A/B). Called with mu held.
+void ring_waker(jsp_engine* e) {
+    const char* w = std::getenv("JSP_SVC_WAKER");  // read per call (in-process A/B)
+    const bool on = !(w && w[0] == '0');
+    e->wake_job = true;
+    if (!on) {
+        run_wake(e);
+        return;
+    }
+    if (!e->waker.joinable()) e->waker = std::thread(waker_main, e);
+    {
+        std::lock_guard<std::mutex> l(e->wake_mu);
+        e->wake_ring = true;
+    }
+    e->wake_cv.notify_one();
+}
+
 // One placement through the service: J jobs of the engine's one class.
 int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
               int32_t* assign_out, uint32_t* placed) {
     auto& v = e->svc;
+    run_wake(e);  // a recovery's wake the waker has not run yet: run it here
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
@@ -1624,9 +1715,18 @@ void jsp_engine_destroy(jsp_engine* e) {
         delete e;  // the destructor tears the device set down
         return;
     }
+    if (e->waker.joinable()) {  // not under mu: the waker may be waiting for it
+        {
+            std::lock_guard<std::mutex> l(e->wake_mu);
+            e->wake_quit = true;
+        }
+        e->wake_cv.notify_one();
+        e->waker.join();
+    }
     {
         std::lock_guard<std::mutex> g(e->mu);
         (void)hipSetDevice(e->device);
+        e->wake_job = false;
         (void)svc_stop(e);
         if (e->stream) (void)hipStreamSynchronize(e->stream);
     }
@@ -1859,6 +1959,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
+    run_wake(e);  // an earlier patch's wake still queued: run it (that patch then goes to the service)
     if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
     if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
@@ -1873,8 +1974,9 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     const auto t1 = std::chrono::steady_clock::now();
     const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
     const bool up = svc_patch_on() && v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
-    const bool wake = !up && svc_patch_on() && svc_wake_wanted(e) && svc_restart_quiet(e) == JSP_OK;
-    const auto t1w = std::chrono::steady_clock::now();
+    // a wake stages for the tile shapes' inline buffer once a service has run
+    // (run_wake moves it to the descriptor if the fused shape starts instead)
+    const bool wake = !up && svc_patch_on() && svc_wake_wanted(e);
     // The delta into pinned staging, read in place. Patches for the service
     // of up to kPatchInlineRows rows go to its fixed inline buffer (layout
     // from n and the column flags, which ride in the request); larger ones,
@@ -1882,7 +1984,8 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     const uint32_t W = e->W, R = e->R;
     const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
                         (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
-    const bool inl = (up || wake) && n <= jsp::kPatchInlineRows && v.shape != 1 && v.pstage.p;
+    const bool inl = (up || wake) && n <= jsp::kPatchInlineRows && v.pstage.p &&
+                     jsp::patch_inline_layout(n, 15u, W, R).bytes <= v.pstage.bytes && (wake || v.shape != 1);
     const jsp::PatchInlineLayout L = jsp::patch_inline_layout(n, inl ? fl : 15u, W, R);
     char* hp;
     size_t base = 0;
@@ -1931,7 +2034,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     e->patch_req = 0;
     e->patch_nf = inl ? (n | fl << 16) : 0u;
     if (up || wake) {
-        if (!inl) *v.pdesc.as<jsp::PatchDesc>() = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
+        if (!inl && v.pdesc.p) *v.pdesc.as<jsp::PatchDesc>() = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, n, a.seq};
         e->patch_pending = e->patch_svc = true;
     }
     // No wait here: later work is ordered after the patch -- service requests
@@ -1941,19 +2044,9 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
         e->patch_deferred = true;
         if (svc_patch_mode() == 2) patch_post_deferred(e);  // posted now (svc_patch_mode)
     } else if (wake) {
-        // the patch, then a warm-up request (no jobs) on the patched rows: the
-        // fresh tiles load them and pull the code into the instruction caches
-        // while the deletions finish, so the recreate's request runs warm
-        const uint32_t seq = next_seq(v.seq);
-        v.seq = seq;
-        v.last = std::chrono::steady_clock::now();
-        const bool warm = v.shape == 2 || v.shape == 3;
-        svc_post(e, seq, e->patch_bits | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly), e->patch_nf);
-        e->patch_req = seq;
-        if (warm) {
-            v.pending = seq;
-            v.rows_dirty = false;  // the warm-up loaded the patched rows
-        }
+        // held back; the waker restarts the service and posts it (run_wake)
+        e->patch_deferred = true;
+        ring_waker(e);
     } else {
         if (int rc = use_engine_stream(e)) return rc;
         // the patch kernel's workgroups count up to the target (patches the
@@ -1970,7 +2063,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     using us = std::chrono::duration<double, std::micro>;
     e->acc.patches += 1;
     e->acc.patch_us += us(t2 - t0).count();
-    e->acc.wake_us += us(wake ? t1w - t1 : t2 - t1).count();
+    if (!wake) e->acc.wake_us += us(t2 - t1).count();  // a wake's own time is counted where it runs
     return JSP_OK;
 }
 
@@ -2356,6 +2449,7 @@ int jsp_engine_service_stop(jsp_engine* e) {
     std::lock_guard<std::mutex> g(e->mu);
     e->svc.resume = false;
     e->svc.armed = false;  // no patch restarts it until a jsp_place is answered by it again
+    e->wake_job = false;   // nor a wake still queued (its patch lands through patch_wait)
     return svc_stop(e);
 }
 
@@ -2387,6 +2481,7 @@ int jsp_engine_sync(jsp_engine* e) {
     if (e->multi) return jspm::sync(e->multi);
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_settle(e)) return rc;  // the service's last request finished on every tile
+    if (int rc = patch_wait(e)) return rc;  // and every patch landed
     HIP_TRY(hipStreamSynchronize(e->stream));
     if (e->have_last && e->last_foreign) {
         if (int rc = wait_last_foreign(e)) return rc;

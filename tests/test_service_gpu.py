@@ -424,7 +424,12 @@ def test_patch_wakes_the_service(svc_engine):
         svc_engine.timing(reset=True)
         time.sleep(0.08)  # past JSP_SERVICE_IDLE_MS: the service has left
         patch()
-        assert svc_engine.timing(reset=False).svc_starts == 1  # woken by the patch
+        # woken by the patch: the waker thread restarts it (poll briefly)
+        for _ in range(200):
+            if svc_engine.timing(reset=False).svc_starts == 1:
+                break
+            time.sleep(0.0005)
+        assert svc_engine.timing(reset=False).svc_starts == 1
         time.sleep(gap)
         got = svc_engine.place(p.job_class)
         t = svc_engine.timing(reset=True)
@@ -437,6 +442,52 @@ def test_patch_wakes_the_service(svc_engine):
     got = svc_engine.place(p.job_class)
     assert got.fused == 3 and svc_engine.timing(reset=True).svc_starts == 1
     np.testing.assert_array_equal(got.assign, a)
+
+
+@pytest.mark.parametrize("waker", ["1", "0"])
+@pytest.mark.parametrize("then", ["place", "patch_again", "upload", "tally_launch", "stop", "sync"])
+def test_wake_then_any_reader(svc_engine, monkeypatch, waker, then):
+    """A recovery's first patch after the service left is held back and the
+    waker thread restarts the service and posts it (JSP_SVC_WAKER=0: the
+    patch call does it inline). Whatever comes next -- the placement, a
+    second patch right behind it, a re-upload, a launch with tallies, an
+    explicit stop, a sync -- finds the patched rows, bit-exact, at once or
+    after the sleep the waker may still be in."""
+    monkeypatch.setenv("JSP_SVC_WAKER", waker)
+    p = synth.config2()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused == 3
+    rng = np.random.default_rng(len(then) + int(waker))
+    R = p.nodes.free.shape[0]
+    for gap in (0.0, 0.003):
+        time.sleep(0.08)  # past JSP_SERVICE_IDLE_MS: the service has left
+        n = int(rng.integers(1, 40))
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=n, replace=False)).astype(np.uint32)
+        free = rng.integers(0, 200_000, size=(R, n)).astype(np.uint32)
+        excl = np.where(rng.random(n) < 0.2, 5, -1).astype(np.int32)
+        svc_engine.patch_rows(rows, free=free, excl=excl)
+        p.nodes.free[:, rows] = free
+        p.nodes.excl[rows] = excl
+        time.sleep(gap)
+        if then == "patch_again":
+            taints = rng.integers(0, 2, size=n).astype(np.uint32)
+            svc_engine.patch_rows(rows, taints=taints)
+            p.nodes.taints[rows] = taints
+        elif then == "upload":
+            svc_engine.load(p)
+        elif then == "stop":
+            svc_engine.service_stop()
+        elif then == "sync":
+            svc_engine.sync()
+        a, cap, occ = O.place_c(p)
+        if then == "tally_launch":
+            got = svc_engine.place(p.job_class, want_tally=True)
+            np.testing.assert_array_equal(got.cap, cap)
+            np.testing.assert_array_equal(got.occ, occ)
+        else:
+            got = svc_engine.place(p.job_class)
+            assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, a)
 
 
 @pytest.mark.parametrize("n", [1, 255, 256, 257, 4095, 4096, 4097, 5000, 14999])

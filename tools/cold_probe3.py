@@ -34,8 +34,11 @@ p = synth.config2()
 e.load(p)
 call = e.host_placer(*job_runs(p.job_class))
 call()
-for idle_spin, gap_spin in ((False, False), (True, True), (False, True), (True, False)):
-    for gap in (0.0, 0.001, 0.01):
+series = [(w, False, False, g) for w in ("1", "0") for g in (0.0, 0.001, 0.01)] + \
+    [(w, True, True, g) for w in ("1", "0") for g in (0.0, 0.001)]
+for waker, idle_spin, gap_spin, gap in series:
+    os.environ["JSP_SVC_WAKER"] = waker  # read per call (in-process A/B: 0 = the patch call restarts the service)
+    if True:
         pa, p1, p2, prep, wt = [], [], [], [], []
         for t in range(trials):
             row = np.array([(t * 7919) % p.nodes.n_nodes], dtype=np.uint32)
@@ -59,7 +62,7 @@ for idle_spin, gap_spin in ((False, False), (True, True), (False, True), (True, 
             prep.append(tm.host_prep_us)
             wt.append(tm.host_wait_us)
         f = lambda v: f"p50 {np.median(v):.1f} p99 {np.percentile(v, 99):.1f}"  # noqa: E731
-        print(f"idle {'spin ' if idle_spin else 'sleep'} gap {gap * 1e3:g} ms {'spin ' if gap_spin else 'sleep'}: "
+        print(f"waker={os.environ['JSP_SVC_WAKER']} idle {'spin ' if idle_spin else 'sleep'} gap {gap * 1e3:g} ms {'spin ' if gap_spin else 'sleep'}: "
               f"patch {f(pa)} | place1 {f(p1)} (prep p50 {np.median(prep):.1f}, wait p50 {np.median(wt):.1f}) | "
               f"place2 {f(p2)}", flush=True)
 e.service_stop()
