@@ -96,8 +96,8 @@ def evidence_dirs():
     every profiles/r*/<run>/ by round (descending) and file time."""
     out = []
     latest = os.path.join(ROOT, "profiles", "LATEST")
-    if os.path.exists(latest):
-        d = os.path.join(ROOT, open(latest).read().strip())
+    if os.path.exists(latest):  # a path under profiles/ (scripts/collect_profiles.sh writes it)
+        d = os.path.join(ROOT, "profiles", open(latest).read().strip())
         if os.path.isdir(d):
             out.append(d)
     for r in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*")), reverse=True):
@@ -111,7 +111,7 @@ def evidence_dirs():
 def latest_dir():
     """The evidence directory profiles/LATEST names (None when absent)."""
     f = os.path.join(ROOT, "profiles", "LATEST")
-    return os.path.join(ROOT, open(f).read().strip()) if os.path.exists(f) else None
+    return os.path.join(ROOT, "profiles", open(f).read().strip()) if os.path.exists(f) else None
 
 
 def pmc_traffic(kernel, cfg: int):

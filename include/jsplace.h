@@ -154,8 +154,8 @@ typedef struct jsp_timing {
     double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
     /* jsp_snapshot_patch (ABI v5), host wall clock, always accumulated */
     uint64_t patches;          /* patch calls with at least one row */
-    double patch_us;           /* their host time, the service (re)start of svc_wake included */
-    double wake_us;            /* of which (re)starting the service for a coming recovery */
+    double patch_us;           /* their host time (a waker-thread restart is not in it) */
+    double wake_us;            /* host time (re)starting the service for a coming recovery, wherever it ran */
 } jsp_timing;
 
 /* jsp_engine_set_fused modes */
@@ -215,11 +215,23 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nodes);
 /* Overwrite n rows (ids in `rows`, local to this shard) of the resident
  * snapshot. delta columns are [W][n], [n], [R][n], [n] (NULL: column
  * unchanged); structure (leaf ranges) is unchanged. The call copies the delta
- * and returns without waiting for the device: every later call sees the
- * patched rows (launches are stream-ordered after it, service requests wait
- * for its completion word). A patch is the first sign of a recovery, so while
- * the resident service is armed (the last jsp_place was answered by it) a
- * patch also (re)starts the service without waiting for it (ABI v5). */
+ * into pinned staging and returns without waiting for the device (ABI v5);
+ * every later call sees the patched rows. Who applies it:
+ *  - the resident service, when it is up: its dispatcher workgroup reads the
+ *    staged delta (up to 4096 rows in one host-link round trip) and writes the
+ *    rows; no launch. The patch is posted at once, so it lands during the gap
+ *    before the next request, and a request that finds it not yet taken
+ *    carries it again (writing a staged delta twice writes the same values);
+ *  - after the service left, while it is armed (the last jsp_place was
+ *    answered by it): a patch is the first sign of a recovery, so the engine's
+ *    waker thread restarts the service and posts the patch, followed by a
+ *    warm-up request without jobs, off the caller's thread;
+ *  - otherwise a patch kernel on the engine stream.
+ * Later launches wait for its completion word (or are stream-ordered after
+ * the patch kernel); uploads and jsp_engine_sync apply pending patches first.
+ * JSP_SVC_PATCH=0 (always the kernel), =1 (held back for the next request),
+ * JSP_SVC_WAKER=0 (the patch call restarts the service itself) and
+ * JSP_SVC_WAKE=0 (no restart on a patch) are A/B switches. */
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n,
                        const uint64_t* labels, const uint32_t* taints,
                        const uint32_t* free_res, const int32_t* excl_owner);

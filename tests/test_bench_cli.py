@@ -34,3 +34,19 @@ def test_world_size_disagreeing_with_gpus_fails():
 def test_gpus_must_be_positive():
     r = _run(["--gpus", "0"])
     assert r.returncode != 0 and '"metric"' not in r.stdout
+
+
+def test_evidence_lookup_follows_latest():
+    """The roofline's traffic and trace figures come from the evidence
+    directory profiles/LATEST names (a path under profiles/), and the line
+    says so (`latest`: true) -- for the compaction and the cfg4 tally kernel."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    b = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(b)
+    latest = b.latest_dir()
+    assert latest is not None and os.path.isdir(latest)
+    assert b.evidence_dirs()[0] == latest
+    for kernel, cfg in (("place_compact_kernel", 2), ("tally_wave1_kernel", 4)):
+        t = b.pmc_traffic(kernel, cfg)
+        assert t is not None and t["latest"], (kernel, t)
