@@ -187,6 +187,8 @@ struct jsp_engine {
     unsigned long long patch_target = 0;
     uint32_t patch_seq = 0;
     bool patch_pending = false;
+    DevBuf lvl_ready;                   // the one-launch level walk's published record count
+    uint32_t lvl_epoch = 0;
     bool patch_svc = false;             // the pending patch goes to the service's dispatcher
     bool patch_deferred = false;        // ... and is held back for the next request (not posted yet)
     uint32_t patch_bits = 0;            // its request bits (kReqPatch, kReqPatchInline)
@@ -617,9 +619,20 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
         return set_err(JSP_ENOMEM, "assignment records (%u jobs)", J);
     if (level_walk_ok(e, n_runs)) {
         const uint32_t nw = (e->D[e->cls_h[0].level] + 63) / 64;
+        // the expansion rides in the walker's launch (JSP_LEVEL_ONE_LAUNCH=0: a second launch, A/B)
+        static const bool one = [] { const char* v = std::getenv("JSP_LEVEL_ONE_LAUNCH"); return !(v && v[0] == '0'); }();
+        unsigned long long* ready = nullptr;
+        if (one) {
+            if (!e->lvl_ready.p) {
+                HIP_TRY(e->lvl_ready.reserve(64));
+                HIP_TRY(hipMemsetAsync(e->lvl_ready.p, 0, 64, s));
+            }
+            ready = e->lvl_ready.as<unsigned long long>();
+            e->lvl_epoch = e->lvl_epoch % 0x7FFFFFFFu + 1u;
+        }
         HIP_TRY(jsp::launch_assign_level(e->feas.as<uint64_t>(), e->C, nw, d_run_class, d_run_len, n_runs, J, d_assign,
                                          stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(),
-                                         e->expand_rpw, s));
+                                         e->expand_rpw, s, ready, e->lvl_epoch));
         ev_end(p, s);
         return JSP_OK;
     }

@@ -342,9 +342,13 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
 constexpr uint32_t kLevelMaxWords = 256 * 8;
 constexpr uint32_t kLevelMaxRuns = 32;
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
+// ready (device u64, or null: a second launch expands): the walker publishes
+// (epoch << 32 | 1 << 31 | record count) there once its records are written,
+// and the launch's other workgroups expand them (epoch: new per launch, != 0).
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
+                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s,
+                               unsigned long long* ready = nullptr, uint32_t epoch = 0);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

@@ -2137,6 +2137,48 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
     }
 }
 
+// The expanders of the one-launch level walk: wave g owns records
+// [g rpw, g rpw + rpw). It waits (bounded) for the walker's published count
+// of this launch (epoch-tagged), reads its records write-through and writes
+// their jobs' domains as expand_kernel does.
+__device__ void level_expand(const AssignRec* recs, const unsigned long long* ready, uint32_t epoch, uint32_t bound,
+                             uint32_t rpw, int32_t* assign) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t r0 = ((blockIdx.x - 1) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rpw;
+    if (r0 >= bound) return;  // wave-uniform
+    const uint64_t t0 = wall_clock64();
+    uint32_t n = 0;
+    while (true) {
+        const unsigned long long x = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == epoch && (x & 0x80000000ull)) {
+            n = (uint32_t)x & 0x7FFFFFFFu;
+            break;
+        }
+        if (wall_clock64() - t0 > 100000000ull) return;  // 1 s: the walker never published (its error shows in stats)
+        __builtin_amdgcn_s_sleep(2);
+    }
+    if (r0 >= n) return;
+    const uint32_t m = n - r0 < rpw ? n - r0 : rpw;
+    uint32_t dom0 = 0, base = 0, t_lo = 0, t_hi = 0;
+    if (lane < m) {
+        const unsigned long long* rp = reinterpret_cast<const unsigned long long*>(recs + r0 + lane);
+        const unsigned long long a = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long b = __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dom0 = (uint32_t)a;
+        base = (uint32_t)(a >> 32);
+        t_lo = (uint32_t)b;
+        t_hi = (uint32_t)(b >> 32);
+    }
+    const uint64_t below = (1ull << lane) - 1ull;
+    for (uint32_t i = 0; i < m; ++i) {
+        const uint64_t t = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)t_hi, (int)i) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)t_lo, (int)i);
+        const uint32_t bs = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)i);
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readlane((int)dom0, (int)i);
+        if ((t >> lane) & 1ull) assign[bs + (uint32_t)__popcll(t & below)] = (int32_t)(d0 + lane);
+    }
+}
+
 // ---- level walker (jsp_internal.h launch_assign_level): every class at one
 // level, few runs. The workgroup (256 threads) stages the classes'
 // feasibility words in LDS (word-major by thread: thread t owns words
@@ -2158,7 +2200,17 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
                                                                      int32_t* __restrict__ assign,
                                                                      uint32_t* __restrict__ stats,
                                                                      uint32_t* __restrict__ rec_count,
-                                                                     AssignRec* __restrict__ recs) {
+                                                                     AssignRec* __restrict__ recs,
+                                                                     unsigned long long* __restrict__ ready,
+                                                                     uint32_t epoch, uint32_t bound, uint32_t rpw) {
+    // Expansion in the same launch (ready != null): workgroups 1.. wait for
+    // the walker (workgroup 0, dispatched first, never waits for them) to
+    // publish its record count, then expand the records as expand_kernel
+    // does -- no second launch and no launch gap between walk and expansion.
+    if (ready != nullptr && blockIdx.x > 0) {
+        level_expand(recs, ready, epoch, bound, rpw, assign);
+        return;
+    }
     extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][256]
     JSP_LDS uint64_t* sf = lds_ptr(s_f);
     __shared__ uint32_t s_rc[kLevelMaxRuns], s_rl[kLevelMaxRuns];
@@ -2224,11 +2276,19 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
                 const uint32_t tk = pc > rem ? rem : pc;
                 rem -= tk;
                 T[k] |= took;
-                AssignRec x;
-                x.dom0 = (tid * (uint32_t)WPT + (uint32_t)k) * 64u;
-                x.base = base;
-                x.took = took;
-                recs[slot] = x;
+                const uint32_t dom0 = (tid * (uint32_t)WPT + (uint32_t)k) * 64u;
+                if (ready != nullptr) {  // read by other workgroups of this launch: write-through
+                    unsigned long long* rp = reinterpret_cast<unsigned long long*>(recs + slot);
+                    __hip_atomic_store(rp, ((unsigned long long)base << 32) | dom0, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(rp + 1, (unsigned long long)took, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    AssignRec x;
+                    x.dom0 = dom0;
+                    x.base = base;
+                    x.took = took;
+                    recs[slot] = x;
+                }
                 ++slot;
                 base += tk;
                 // the run's last taking word: the next run's records start after it
@@ -2241,11 +2301,15 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         jpos += n;
         if (r < 5) JSP_STAMP(4050u, 2 + r);
     }
+    if (ready != nullptr) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this thread's records are out
     __syncthreads();  // the last run's record base
     if (tid == 0) {
         *rec_count = s_base[n_runs & 1u];
         stats[0] = n_runs;
         stats[1] = placed;
+        if (ready != nullptr)
+            __hip_atomic_store(ready, ((unsigned long long)epoch << 32) | 0x80000000ull | s_base[n_runs & 1u],
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     JSP_STAMP(4050u, 7);
 }
@@ -3795,25 +3859,28 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
 
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s) {
+                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s,
+                               unsigned long long* ready, uint32_t epoch) {
     const uint32_t wpt = level_wpt(nw);
     const size_t lds = level_walk_lds_bytes(C, nw);
     if (wpt == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
         return hipErrorInvalidValue;
-    const dim3 g(1), b(kLevelThreads);
-    switch (wpt) {
-        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs); break;
-    }
-    if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0) return e;
     // records: one per (run, word) that gives domains away; a class's runs
     // take its words in order, so at most its words plus one per run
     const uint64_t wb = (uint64_t)C * nw + n_runs;
     const uint32_t bound = wb < J ? (uint32_t)wb : J;
     const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
     const uint32_t waves = (bound + rpw - 1) / rpw;
+    // one launch (ready != null): the walker plus the expanders behind it
+    unsigned long long* rd = J > 0 ? ready : nullptr;
+    const dim3 g(rd ? 1u + (waves + 3) / 4 : 1u), b(kLevelThreads);
+    switch (wpt) {
+        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
+        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
+        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
+        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
+    }
+    if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0 || rd) return e;
     jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
     return hipGetLastError();
 }
