@@ -36,6 +36,8 @@ call = e.host_placer(*job_runs(p.job_class))
 call()
 series = [(w, False, False, g) for w in ("1", "0") for g in (0.0, 0.001, 0.01)] + \
     [(w, True, True, g) for w in ("1", "0") for g in (0.0, 0.001)]
+if len(sys.argv) > 2:  # only the slept series (A/B of the waker's spin across processes)
+    series = [(w, False, False, g) for w in ("1",) for g in (0.001, 0.01)]
 for waker, idle_spin, gap_spin, gap in series:
     os.environ["JSP_SVC_WAKER"] = waker  # read per call (in-process A/B: 0 = the patch call restarts the service)
     if True:
