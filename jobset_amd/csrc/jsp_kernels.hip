@@ -2137,6 +2137,7 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
     }
 }
 
+constexpr uint32_t kLevelEarly = 1u << 30;  // rpw flag: publish the record count after every run
 // The expanders of the one-launch level walk: wave g owns records
 // [g rpw, g rpw + rpw). It waits (bounded) for the walker's published count
 // of this launch (epoch-tagged), reads its records write-through and writes
@@ -2150,7 +2151,9 @@ __device__ void level_expand(const AssignRec* recs, const unsigned long long* re
     uint32_t n = 0;
     while (true) {
         const unsigned long long x = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((uint32_t)(x >> 32) == epoch && (x & 0x80000000ull)) {
+        // the final count (done bit), or a partial one (early expansion) that
+        // already covers this wave's records
+        if ((uint32_t)(x >> 32) == epoch && ((x & 0x80000000ull) || ((uint32_t)x & 0x7FFFFFFFu) >= r0 + rpw)) {
             n = (uint32_t)x & 0x7FFFFFFFu;
             break;
         }
@@ -2207,6 +2210,8 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
     // the walker (workgroup 0, dispatched first, never waits for them) to
     // publish its record count, then expand the records as expand_kernel
     // does -- no second launch and no launch gap between walk and expansion.
+    const bool early = ready != nullptr && (rpw & kLevelEarly) != 0u;
+    rpw &= ~kLevelEarly;
     if (ready != nullptr && blockIdx.x > 0) {
         level_expand(recs, ready, epoch, bound, rpw, assign);
         return;
@@ -2264,6 +2269,12 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         const uint32_t pre = pre_p & 0x3FFFFu, total_free = tot_p & 0x3FFFFu;
         const uint32_t used = total_free < n ? total_free : n;
         const uint32_t rec_base = s_base[r & 1u];  // published by run r - 1 before this scan's barrier
+        // early expansion (rpw & kLevelEarly): the records of runs < r are out
+        // (every thread waited for its stores before this scan's barrier), so
+        // the expanders may start on them while this run is walked
+        if (early && r > 0 && tid == 0)
+            __hip_atomic_store(ready, ((unsigned long long)epoch << 32) | rec_base, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
         uint32_t rem = used > pre ? used - pre : 0u;
         uint32_t slot = rec_base + (pre_p >> 18);
         uint32_t base = jpos + pre;
@@ -2296,6 +2307,7 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
             }
         }
         if (used == 0u && tid == 0) s_base[(r + 1) & 1u] = rec_base;
+        if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this run's records are out
         for (uint32_t j = jpos + used + tid; j < jpos + n; j += kLevelThreads) assign[j] = -1;
         placed += used;
         jpos += n;
@@ -3874,11 +3886,14 @@ hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, co
     // one launch (ready != null): the walker plus the expanders behind it
     unsigned long long* rd = J > 0 ? ready : nullptr;
     const dim3 g(rd ? 1u + (waves + 3) / 4 : 1u), b(kLevelThreads);
+    // early expansion (JSP_LEVEL_EARLY=1, A/B): the walker publishes after every run
+    static const bool early = [] { const char* v = std::getenv("JSP_LEVEL_EARLY"); return v && v[0] == '1'; }();
+    const uint32_t rpw_k = rpw | (rd && early ? kLevelEarly : 0u);
     switch (wpt) {
-        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
-        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
-        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
-        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw); break;
+        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
+        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
+        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
+        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
     }
     if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0 || rd) return e;
     jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
