@@ -620,7 +620,8 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
     if (level_walk_ok(e, n_runs)) {
         const uint32_t nw = (e->D[e->cls_h[0].level] + 63) / 64;
         // the expansion rides in the walker's launch (JSP_LEVEL_ONE_LAUNCH=0: a second launch, A/B)
-        static const bool one = [] { const char* v = std::getenv("JSP_LEVEL_ONE_LAUNCH"); return !(v && v[0] == '0'); }();
+        const char* ov = std::getenv("JSP_LEVEL_ONE_LAUNCH");  // read per call (in-process A/B)
+        const bool one = !(ov && ov[0] == '0');
         unsigned long long* ready = nullptr;
         if (one) {
             if (!e->lvl_ready.p) {

@@ -781,6 +781,35 @@ def test_folded_feasibility_and_level_walk(engine, seed):
         engine.set_fused(True)
 
 
+@pytest.mark.parametrize("one", ["1", "0"])
+@pytest.mark.parametrize("seed", range(8))
+def test_level_walk_one_launch_job_counts(engine, monkeypatch, one, seed):
+    """The level walk with its expansion in the same launch (expander
+    workgroups wait for the walker's record count; JSP_LEVEL_ONE_LAUNCH=0:
+    a second launch): J = 0, 1, a few, about the domain count and well past
+    it (every run's tail unplaceable), empty leading runs, bit-exact."""
+    import dataclasses
+    monkeypatch.setenv("JSP_LEVEL_ONE_LAUNCH", one)
+    base = _one_level(synth.random_problem(seed, max_nodes=30_000, max_leaves=3000, max_jobs=3000),
+                      0, 4, True, seed)
+    K = base.topology.n_levels
+    base = dataclasses.replace(base, classes=[dataclasses.replace(c, level=K - 1) for c in base.classes])
+    engine.set_fused(False)
+    try:
+        engine.load(base)
+        D = base.topology.n_domains[K - 1]
+        C = len(base.classes)
+        for J in (0, 1, 7, D, 3 * D + 5):
+            jc = np.sort(np.arange(J, dtype=np.uint32) % C, kind="stable")
+            p = dataclasses.replace(base, job_class=jc)
+            got = engine.place(p.job_class, want_tally=True)
+            a, cap, occ = O.place_c(p)
+            assert_same(got, a, cap, occ)
+            assert got.fused == 0
+    finally:
+        engine.set_fused(True)
+
+
 def test_folded_feasibility_after_patches(engine):
     """cfg4 (1M nodes, 4 leaf classes, 4 runs) placed repeatedly while rows
     change: every tally rewrites each leaf's bit exactly (no stale bit from
