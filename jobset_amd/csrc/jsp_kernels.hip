@@ -2221,6 +2221,7 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
     __shared__ uint32_t s_rc[kLevelMaxRuns], s_rl[kLevelMaxRuns];
     __shared__ uint32_t s_scan[2 * kTallyWaves];
     __shared__ uint32_t s_base[2];
+    __shared__ uint32_t s_u0[kLevelMaxRuns], s_u1[kLevelMaxRuns];
     const uint32_t tid = threadIdx.x;
     JSP_STAMP(4050u, 0);
     // the run table beside the words: one round trip, however far the runs
@@ -2268,6 +2269,7 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         const uint32_t pre_p = block_excl_scan<kLevelThreads>((nzw << 18) | cnt, s_scan, &tot_p, (int)(r & 1u));
         const uint32_t pre = pre_p & 0x3FFFFu, total_free = tot_p & 0x3FFFFu;
         const uint32_t used = total_free < n ? total_free : n;
+        if (r < 4) JSP_STAMP(4051u, r);  // diagnostic: this run's scan is done
         const uint32_t rec_base = s_base[r & 1u];  // published by run r - 1 before this scan's barrier
         // early expansion (rpw & kLevelEarly): the records of runs < r are out
         // (every thread waited for its stores before this scan's barrier), so
@@ -2307,8 +2309,12 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
             }
         }
         if (used == 0u && tid == 0) s_base[(r + 1) & 1u] = rec_base;
+        if (r < 4) JSP_STAMP(4051u, 4 + r);  // diagnostic: this run's records issued
         if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this run's records are out
-        for (uint32_t j = jpos + used + tid; j < jpos + n; j += kLevelThreads) assign[j] = -1;
+        if (tid == 0) {  // the run's unplaceable tail, written after the walk (off the runs' chain)
+            s_u0[r] = jpos + used;
+            s_u1[r] = jpos + n;
+        }
         placed += used;
         jpos += n;
         if (r < 5) JSP_STAMP(4050u, 2 + r);
@@ -2322,6 +2328,23 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         if (ready != nullptr)
             __hip_atomic_store(ready, ((unsigned long long)epoch << 32) | 0x80000000ull | s_base[n_runs & 1u],
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // the unplaceable tails (-1), while the expanders work: 16-byte stores
+    // between the 4-aligned bounds when assign[] is 16-byte aligned
+    const bool vec = (reinterpret_cast<uintptr_t>(assign) & 15u) == 0u;
+    for (uint32_t r = 0; r < n_runs; ++r) {
+        const uint32_t j0 = s_u0[r], j1 = s_u1[r];
+        if (j0 >= j1) continue;
+        uint32_t a0 = j1, a1 = j1;
+        if (vec) {
+            a0 = (j0 + 3u) & ~3u;
+            a1 = j1 & ~3u;
+            if (a0 > a1) a0 = a1 = j1;
+        }
+        for (uint32_t j = j0 + tid; j < a0; j += kLevelThreads) assign[j] = -1;
+        for (uint32_t q = a0 / 4u + tid; q < a1 / 4u; q += kLevelThreads)
+            reinterpret_cast<int4*>(assign)[q] = make_int4(-1, -1, -1, -1);
+        for (uint32_t j = a1 + tid; j < j1; j += kLevelThreads) assign[j] = -1;
     }
     JSP_STAMP(4050u, 7);
 }

@@ -36,11 +36,15 @@ def main():
         eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 0)
         torch.cuda.synchronize()
         lib.jsp_debug_stamps(buf.ctypes.data, buf.shape[0])
-        st = buf.reshape(4096, 8)[4050].astype(np.int64)
-        rows.append((st - st[0]) * 10)
+        b = buf.reshape(4096, 8)
+        st = b[4050].astype(np.int64)
+        sub = b[4051].astype(np.int64)
+        rows.append(np.concatenate([(st - st[0]) * 10, (sub - st[0]) * 10]))
     med = np.median(np.stack(rows[3:]), axis=0)
     print("assign_level_kernel cfg4 (ns from entry): staged {:.0f} | runs {} | end {:.0f}".format(
         med[1], " ".join(f"{x:.0f}" for x in med[2:6]), med[7]), flush=True)
+    print("  per run: scan done {} | records issued {}".format(
+        " ".join(f"{x:.0f}" for x in med[8:12]), " ".join(f"{x:.0f}" for x in med[12:16])), flush=True)
 
 
 if __name__ == "__main__":
