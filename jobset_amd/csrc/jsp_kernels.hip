@@ -2195,9 +2195,10 @@ __device__ void level_expand(const AssignRec* recs, const unsigned long long* re
 // next run's record base (read after the next scan's barrier). A one-wave
 // version (all words in one wave's registers) was instruction-bound: a wave64
 // VALU op takes 4 cycles of its SIMD, ~3 us per run on cfg4.
-constexpr uint32_t kLevelThreads = 256;
-template <int WPT>
-__global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint64_t* __restrict__ feas, uint32_t C,
+// NT threads (256, or 1024 for more than 256 words: one or two words per
+// thread, 4 waves per SIMD to hide each other's latency in the per-run chain)
+template <int WPT, int NT>
+__global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __restrict__ feas, uint32_t C,
                                                                      uint32_t nw, const uint32_t* __restrict__ run_class,
                                                                      const uint32_t* __restrict__ run_len, uint32_t n_runs,
                                                                      int32_t* __restrict__ assign,
@@ -2216,10 +2217,10 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         level_expand(recs, ready, epoch, bound, rpw, assign);
         return;
     }
-    extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][256]
+    extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][NT]
     JSP_LDS uint64_t* sf = lds_ptr(s_f);
     __shared__ uint32_t s_rc[kLevelMaxRuns], s_rl[kLevelMaxRuns];
-    __shared__ uint32_t s_scan[2 * kTallyWaves];
+    __shared__ uint32_t s_scan[2 * (NT / 64)];
     __shared__ uint32_t s_base[2];
     __shared__ uint32_t s_u0[kLevelMaxRuns], s_u1[kLevelMaxRuns];
     const uint32_t tid = threadIdx.x;
@@ -2233,20 +2234,20 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
     if (tid == 0) s_base[0] = 0u;
     // 16 loads per thread in flight before their LDS stores
     constexpr uint32_t kBatch = 16;
-    const uint32_t total = C * kLevelThreads * (uint32_t)WPT;
-    for (uint32_t b0 = 0; b0 < total; b0 += kLevelThreads * kBatch) {
+    const uint32_t total = C * (uint32_t)NT * (uint32_t)WPT;
+    for (uint32_t b0 = 0; b0 < total; b0 += (uint32_t)NT * kBatch) {
         uint64_t f[kBatch];
 #pragma unroll
         for (uint32_t q = 0; q < kBatch; ++q) {
-            const uint32_t i = b0 + q * kLevelThreads + tid;  // i = c * (256 WPT) + word
-            const uint32_t c = i / (kLevelThreads * WPT), w = i - c * (kLevelThreads * WPT);
+            const uint32_t i = b0 + q * (uint32_t)NT + tid;  // i = c * (256 WPT) + word
+            const uint32_t c = i / ((uint32_t)NT * WPT), w = i - c * ((uint32_t)NT * WPT);
             f[q] = (i < total && w < nw) ? feas[(size_t)c * nw + w] : 0ull;
         }
 #pragma unroll
         for (uint32_t q = 0; q < kBatch; ++q) {
-            const uint32_t i = b0 + q * kLevelThreads + tid;
-            const uint32_t c = i / (kLevelThreads * WPT), w = i - c * (kLevelThreads * WPT);
-            if (i < total) sf[(c * WPT + w % WPT) * kLevelThreads + w / WPT] = f[q];
+            const uint32_t i = b0 + q * (uint32_t)NT + tid;
+            const uint32_t c = i / ((uint32_t)NT * WPT), w = i - c * ((uint32_t)NT * WPT);
+            if (i < total) sf[(c * WPT + w % WPT) * (uint32_t)NT + w / WPT] = f[q];
         }
     }
     __syncthreads();
@@ -2261,12 +2262,12 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
         uint32_t cnt = 0, nzw = 0;
 #pragma unroll
         for (int k = 0; k < WPT; ++k) {
-            A[k] = sf[(c * WPT + k) * kLevelThreads + tid] & ~T[k];
+            A[k] = sf[(c * WPT + k) * (uint32_t)NT + tid] & ~T[k];
             cnt += (uint32_t)__popcll(A[k]);
             nzw += A[k] != 0ull ? 1u : 0u;
         }
         uint32_t tot_p;
-        const uint32_t pre_p = block_excl_scan<kLevelThreads>((nzw << 18) | cnt, s_scan, &tot_p, (int)(r & 1u));
+        const uint32_t pre_p = block_excl_scan<NT>((nzw << 18) | cnt, s_scan, &tot_p, (int)(r & 1u));
         const uint32_t pre = pre_p & 0x3FFFFu, total_free = tot_p & 0x3FFFFu;
         const uint32_t used = total_free < n ? total_free : n;
         if (r < 4) JSP_STAMP(4051u, r);  // diagnostic: this run's scan is done
@@ -2341,10 +2342,10 @@ __global__ __launch_bounds__(kLevelThreads) void assign_level_kernel(const uint6
             a1 = j1 & ~3u;
             if (a0 > a1) a0 = a1 = j1;
         }
-        for (uint32_t j = j0 + tid; j < a0; j += kLevelThreads) assign[j] = -1;
-        for (uint32_t q = a0 / 4u + tid; q < a1 / 4u; q += kLevelThreads)
+        for (uint32_t j = j0 + tid; j < a0; j += (uint32_t)NT) assign[j] = -1;
+        for (uint32_t q = a0 / 4u + tid; q < a1 / 4u; q += (uint32_t)NT)
             reinterpret_cast<int4*>(assign)[q] = make_int4(-1, -1, -1, -1);
-        for (uint32_t j = a1 + tid; j < j1; j += kLevelThreads) assign[j] = -1;
+        for (uint32_t j = a1 + tid; j < j1; j += (uint32_t)NT) assign[j] = -1;
     }
     JSP_STAMP(4050u, 7);
 }
@@ -3882,21 +3883,30 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
     return hipGetLastError();
 }
 
-static uint32_t level_wpt(uint32_t nw) {
-    const uint32_t w = (nw + kLevelThreads - 1) / kLevelThreads;
-    return w <= 1u ? 1u : w <= 2u ? 2u : w <= 4u ? 4u : w <= 8u ? 8u : 0u;
+// the level walker's shape for nw words: (words per thread, threads);
+// JSP_LEVEL_NT=256 keeps 256 threads up to 2048 words (A/B)
+static void level_shape(uint32_t nw, uint32_t* wpt, uint32_t* nt) {
+    static const bool narrow = [] { const char* v = std::getenv("JSP_LEVEL_NT"); return v && std::atoi(v) == 256; }();
+    *wpt = 0;
+    *nt = 256;
+    if (nw <= 256) *wpt = 1;
+    else if (!narrow && nw <= 1024) { *wpt = 1; *nt = 1024; }
+    else if (!narrow && nw <= 2048) { *wpt = 2; *nt = 1024; }
+    else if (narrow && nw <= 2048) *wpt = nw <= 512 ? 2u : nw <= 1024 ? 4u : 8u;
 }
 
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
-    const uint32_t wpt = level_wpt(nw);
-    return wpt ? (size_t)C * kLevelThreads * wpt * 8u : 0u;
+    uint32_t wpt, nt;
+    level_shape(nw, &wpt, &nt);
+    return wpt ? (size_t)C * nt * wpt * 8u : 0u;
 }
 
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s,
                                unsigned long long* ready, uint32_t epoch) {
-    const uint32_t wpt = level_wpt(nw);
+    uint32_t wpt, nt;
+    level_shape(nw, &wpt, &nt);
     const size_t lds = level_walk_lds_bytes(C, nw);
     if (wpt == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
         return hipErrorInvalidValue;
@@ -3908,16 +3918,26 @@ hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, co
     const uint32_t waves = (bound + rpw - 1) / rpw;
     // one launch (ready != null): the walker plus the expanders behind it
     unsigned long long* rd = J > 0 ? ready : nullptr;
-    const dim3 g(rd ? 1u + (waves + 3) / 4 : 1u), b(kLevelThreads);
+    const uint32_t wpb = nt / 64;  // expander waves per workgroup
+    const dim3 g(rd ? 1u + (waves + wpb - 1) / wpb : 1u), b(nt);
     // early expansion (JSP_LEVEL_EARLY=1, A/B): the walker publishes after every run
     static const bool early = [] { const char* v = std::getenv("JSP_LEVEL_EARLY"); return v && v[0] == '1'; }();
     const uint32_t rpw_k = rpw | (rd && early ? kLevelEarly : 0u);
-    switch (wpt) {
-        case 1: jsp_launch(assign_level_kernel<1>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
-        case 2: jsp_launch(assign_level_kernel<2>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
-        case 4: jsp_launch(assign_level_kernel<4>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
-        default: jsp_launch(assign_level_kernel<8>, g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, stats, rec_count, recs, rd, epoch, bound, rpw_k); break;
+#define JSP_LEVEL_LAUNCH(W_, N_) \
+    jsp_launch((assign_level_kernel<W_, N_>), g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, \
+               stats, rec_count, recs, rd, epoch, bound, rpw_k)
+    if (nt == 1024) {
+        if (wpt == 1) JSP_LEVEL_LAUNCH(1, 1024);
+        else JSP_LEVEL_LAUNCH(2, 1024);
+    } else {
+        switch (wpt) {
+            case 1: JSP_LEVEL_LAUNCH(1, 256); break;
+            case 2: JSP_LEVEL_LAUNCH(2, 256); break;
+            case 4: JSP_LEVEL_LAUNCH(4, 256); break;
+            default: JSP_LEVEL_LAUNCH(8, 256); break;
+        }
     }
+#undef JSP_LEVEL_LAUNCH
     if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0 || rd) return e;
     jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
     return hipGetLastError();
