@@ -276,6 +276,14 @@ struct jsp_engine {
     jsp_timing acc{};
 
     ~jsp_engine() {
+        if (waker.joinable()) {  // jsp_engine_destroy joins it; any other delete too
+            {
+                std::lock_guard<std::mutex> l(wake_mu);
+                wake_quit = true;
+            }
+            wake_cv.notify_one();
+            waker.join();
+        }
         if (multi) jspm::destroy(multi);
         (void)hipSetDevice(device);
         for (auto* v : {&ev, &tev})
