@@ -806,6 +806,7 @@ def main() -> None:
         barrier(world)
         if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
             cfg4["device_set"] = device_set_leg(p4, sp.assign(), max(20, args.steps))
+            torch.cuda.set_device(local)  # the rank's own device for the barrier (the library restores it too)
         barrier(world)
 
     if rank == 0:

@@ -60,6 +60,18 @@ struct Grave {
 
 // Grow-only device buffer. `g`: where the old buffer goes when it must grow
 // while a kernel that never ends by itself runs (nullptr: freed at once).
+// The calling thread's current device, restored when an entry point that
+// switches devices returns (the device-set engine walks its devices; a
+// caller -- a torch rank, a Go thread -- keeps the device it had).
+struct DeviceGuard {
+    int prev = -1;
+    DeviceGuard() { (void)hipGetDevice(&prev); }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
@@ -1659,6 +1671,7 @@ int jsp_device_count(int* out) {
 }
 
 int jsp_engine_create(int device_id, jsp_engine** out) {
+    DeviceGuard dg;
     if (!out) return set_err(JSP_EINVAL, "out is NULL");
     *out = nullptr;
     int n = 0;
@@ -1709,6 +1722,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
 }
 
 int jsp_engine_create_multi(const int* device_ids, int n_devices, jsp_engine** out) {
+    DeviceGuard dg;
     if (!out) return set_err(JSP_EINVAL, "out is NULL");
     *out = nullptr;
     jspm::Multi* m = nullptr;
@@ -1733,6 +1747,7 @@ int jsp_engine_shards(jsp_engine* e, int* shards, int* devices) {
 
 void jsp_engine_destroy(jsp_engine* e) {
     if (!e) return;
+    DeviceGuard dg;
     if (e->multi) {
         delete e;  // the destructor tears the device set down
         return;
@@ -1757,7 +1772,7 @@ void jsp_engine_destroy(jsp_engine* e) {
 
 int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::topology_upload(e->multi, t);
+    if (e->multi) { DeviceGuard dg; return jspm::topology_upload(e->multi, t); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!t) return set_err(JSP_EINVAL, "topology is NULL");
@@ -1835,7 +1850,7 @@ int jsp_topology_upload(jsp_engine* e, const jsp_topology* t) {
 
 int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::snapshot_upload(e->multi, nd);
+    if (e->multi) { DeviceGuard dg; return jspm::snapshot_upload(e->multi, nd); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
@@ -1973,7 +1988,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
                        const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner);
+    if (e->multi) { DeviceGuard dg; return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner); }
     const auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
@@ -2091,7 +2106,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
 
 int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t C) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::classes_upload(e->multi, classes, C);
+    if (e->multi) { DeviceGuard dg; return jspm::classes_upload(e->multi, classes, C); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_suspend(e)) return rc;  // it holds the old buffers and geometry
     if (!e->have_topo) return set_err(JSP_ESTATE, "upload the topology first");
@@ -2225,7 +2240,7 @@ int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uin
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::place(e->multi, run_class, run_len, n_runs, assign_out, tally_out, occ_out, stats);
+    if (e->multi) { DeviceGuard dg; return jspm::place(e->multi, run_class, run_len, n_runs, assign_out, tally_out, occ_out, stats); }
     auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
@@ -2363,7 +2378,7 @@ int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs, in
 int jsp_resolve_leader_domains(jsp_engine* e, const int32_t* leader_rows, const uint32_t* levels, uint32_t n,
                                int32_t* domain_out) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::resolve(e->multi, leader_rows, levels, n, domain_out);
+    if (e->multi) { DeviceGuard dg; return jspm::resolve(e->multi, leader_rows, levels, n, domain_out); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, false)) return rc;
     if (n == 0) return JSP_OK;
@@ -2390,7 +2405,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
                          const uint32_t* follower_off, const int32_t* follower_domains, uint32_t n_jobs,
                          uint32_t* bad_out) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::audit(e->multi, leader_rows, levels, follower_off, follower_domains, n_jobs, bad_out);
+    if (e->multi) { DeviceGuard dg; return jspm::audit(e->multi, leader_rows, levels, follower_off, follower_domains, n_jobs, bad_out); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, false)) return rc;
     if (n_jobs == 0) return JSP_OK;
@@ -2423,7 +2438,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
 
 int jsp_engine_set_fused(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::forward(e->multi, 0, mode);
+    if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 0, mode); }
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_FUSED_OFF && mode != JSP_FUSED_AUTO) return set_err(JSP_EINVAL, "fused mode %d", mode);
     if (mode != e->fused_mode) {
@@ -2436,7 +2451,7 @@ int jsp_engine_set_fused(jsp_engine* e, int mode) {
 
 int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::forward(e->multi, 1, mode);
+    if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 1, mode); }
     std::lock_guard<std::mutex> g(e->mu);
     if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO && mode != JSP_SERVICE_DEVICE_WALK)
         return set_err(JSP_EINVAL, "service mode %d", mode);
@@ -2477,7 +2492,7 @@ int jsp_engine_service_stop(jsp_engine* e) {
 
 int jsp_engine_set_timing(jsp_engine* e, int enable) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::forward(e->multi, 2, enable);
+    if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 2, enable); }
     std::lock_guard<std::mutex> g(e->mu);
     e->timing = enable != 0;
     return JSP_OK;
@@ -2485,7 +2500,7 @@ int jsp_engine_set_timing(jsp_engine* e, int enable) {
 
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::get_timing(e->multi, out, reset);
+    if (e->multi) { DeviceGuard dg; return jspm::get_timing(e->multi, out, reset); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = resolve_timing(e)) return rc;
     if (out) *out = e->acc;
@@ -2500,7 +2515,7 @@ void* jsp_engine_stream(jsp_engine* e) {
 
 int jsp_engine_sync(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::sync(e->multi);
+    if (e->multi) { DeviceGuard dg; return jspm::sync(e->multi); }
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = svc_settle(e)) return rc;  // the service's last request finished on every tile
     if (int rc = patch_wait(e)) return rc;  // and every patch landed
@@ -2513,7 +2528,7 @@ int jsp_engine_sync(jsp_engine* e) {
 
 int jsp_engine_check(jsp_engine* e) {
     if (int rc = check_engine(e)) return rc;
-    if (e->multi) return jspm::check(e->multi);
+    if (e->multi) { DeviceGuard dg; return jspm::check(e->multi); }
     std::lock_guard<std::mutex> g(e->mu);
     // everything enqueued so far is ordered before the last call's work, so
     // waiting for that (an engine-owned event, or the engine stream) suffices

@@ -188,3 +188,23 @@ def test_device_set_distinct_devices(cfg):
             np.testing.assert_array_equal(got.occ, occ)
     finally:
         e.close()
+
+
+def test_device_set_keeps_the_callers_device():
+    """A device-set engine walks its devices inside each call and hands the
+    calling thread back its current device (a torch rank's NCCL barrier after
+    the bench's device-set leg depends on it). On one GPU the ids are {0, 0};
+    with more, the set is listed last device first."""
+    import torch
+    n = torch.cuda.device_count()
+    ids = list(range(n))[::-1] if n > 1 else [0, 0]
+    torch.cuda.set_device(0)
+    p = synth.config4() if n > 1 else synth.config5()
+    with Engine(devices=ids) as ds:
+        assert torch.cuda.current_device() == 0
+        ds.load(p)
+        assert torch.cuda.current_device() == 0
+        got = ds.place(p.job_class)
+        assert torch.cuda.current_device() == 0
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    assert torch.cuda.current_device() == 0
