@@ -859,7 +859,19 @@ int svc_stop(jsp_engine* e) {
     if (!v.running) return JSP_OK;
     v.running = false;
     __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
-    HIP_TRY(hipStreamSynchronize(v.stream));
+    // The kernel leaves within microseconds of the stop word: poll for it
+    // rather than sleep in a blocking synchronize (whose wake-up costs more
+    // than the exit itself); after 2 ms, block (JSP_SVC_STOP_SPIN=0: always block)
+    static const bool spin = [] { const char* c = std::getenv("JSP_SVC_STOP_SPIN"); return !(c && c[0] == '0'); }();
+    hipError_t q = hipErrorNotReady;
+    if (spin) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((q = hipStreamQuery(v.stream)) == hipErrorNotReady &&
+               std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
+            for (int i = 0; i < 16; ++i) __builtin_ia32_pause();
+    }
+    if (q == hipErrorNotReady) HIP_TRY(hipStreamSynchronize(v.stream));
+    else if (q != hipSuccess) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
     e->grave.flush();  // nothing resident any more: a free no longer waits
     return JSP_OK;
 }
