@@ -1,7 +1,10 @@
 // jsp_engine.cc — host side of the exclusive-topology placement engine:
 // the C ABI of include/jsplace.h over HIP device buffers and the kernels of
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -247,6 +250,12 @@ struct jsp_engine {
         bool running = false;
         hipStream_t stream = nullptr;
         HostBuf box;     // request: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; u32 [8] ready
+        // The request words the dispatcher polls: box, or (JSP_SVC_BAR=1) a
+        // line of fine-grained device memory the host writes through the BAR
+        // -- the dispatcher's polls then stay on the device
+        unsigned long long* req = nullptr;
+        void* bar = nullptr;     // that line (hipFree at engine destruction)
+        bool bar_tried = false;
         HostBuf words;   // done[nb] | stats[2] | err[1] | clk[kSvcClkSlots nb]
         HostBuf assign;  // [cap]
         HostBuf runs;    // fused shape: run_class[cap_runs] | run_len[cap_runs]
@@ -307,6 +316,7 @@ struct jsp_engine {
         if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.stream) (void)hipStreamDestroy(svc.stream);
+        if (svc.bar) (void)hipFree(svc.bar);
     }
 };
 
@@ -848,6 +858,50 @@ int svc_shape(jsp_engine* e) {
 }
 bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
+// A request line in device memory the CPU may write (fine-grained device
+// memory opened to the CPU agent; absent without a large BAR). HSA entry
+// points come from the runtime HIP already loaded (no second runtime).
+void* bar_line(int device) {
+    using IterFn = hsa_status_t (*)(hsa_status_t (*)(hsa_agent_t, void*), void*);
+    using InfoFn = hsa_status_t (*)(hsa_agent_t, hsa_agent_info_t, void*);
+    using AllowFn = hsa_status_t (*)(uint32_t, const hsa_agent_t*, const uint32_t*, const void*);
+    auto iter = reinterpret_cast<IterFn>(dlsym(RTLD_DEFAULT, "hsa_iterate_agents"));
+    static InfoFn info = nullptr;
+    info = reinterpret_cast<InfoFn>(dlsym(RTLD_DEFAULT, "hsa_agent_get_info"));
+    auto allow = reinterpret_cast<AllowFn>(dlsym(RTLD_DEFAULT, "hsa_amd_agents_allow_access"));
+    if (!iter || !info || !allow) return nullptr;
+    hsa_agent_t cpu{};
+    auto find = [](hsa_agent_t a, void* out) -> hsa_status_t {
+        hsa_device_type_t t;
+        if (info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
+            auto* c = static_cast<hsa_agent_t*>(out);
+            if (c->handle == 0) *c = a;
+        }
+        return HSA_STATUS_SUCCESS;
+    };
+    if (iter(find, &cpu) != HSA_STATUS_SUCCESS || cpu.handle == 0) return nullptr;
+    (void)hipSetDevice(device);
+    void* p = nullptr;
+    if (hipExtMallocWithFlags(&p, 4096, hipDeviceMallocFinegrained) != hipSuccess || !p) return nullptr;
+    if (allow(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
+        (void)hipFree(p);
+        return nullptr;
+    }
+    std::memset(p, 0, 64);  // through the BAR
+    __builtin_ia32_sfence();
+    return p;
+}
+
+// Store request words: the second half first (the dispatcher reads both in
+// one 16-byte load and takes a torn read for none); a BAR line is flushed
+// from the write-combining buffers at once.
+void req_store(jsp_engine* e, unsigned long long w0, unsigned long long w1, bool both = true) {
+    unsigned long long* r = e->svc.req ? e->svc.req : e->svc.box.as<unsigned long long>();
+    if (both) __atomic_store_n(r + 1, w1, __ATOMIC_RELEASE);
+    __atomic_store_n(r, w0, __ATOMIC_RELEASE);
+    if (e->svc.req && e->svc.req != e->svc.box.as<unsigned long long>()) __builtin_ia32_sfence();
+}
+
 int patch_wait(jsp_engine* e);
 int svc_stop(jsp_engine* e) {
     auto& v = e->svc;
@@ -858,7 +912,7 @@ int svc_stop(jsp_engine* e) {
     v.pending = 0;  // the stop waits for the kernel to leave, i.e. for every tile to finish
     if (!v.running) return JSP_OK;
     v.running = false;
-    __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
+    req_store(e, (unsigned long long)jsp::kSvcStop, 0, false);
     // The kernel leaves within microseconds of the stop word: poll for it
     // rather than sleep in a blocking synchronize (whose wake-up costs more
     // than the exit itself); after 2 ms, block (JSP_SVC_STOP_SPIN=0: always block)
@@ -982,14 +1036,24 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
         HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
         v.zero_key = key;
     }
-    __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)v.seq, __ATOMIC_RELEASE);
-    __atomic_store_n(v.box.as<unsigned long long>(), (unsigned long long)v.seq, __ATOMIC_RELEASE);
+    {
+        // the request line: in device memory written through the BAR
+        // (JSP_SVC_BAR=1, read at each start), else the pinned box
+        const char* b = std::getenv("JSP_SVC_BAR");
+        const bool want = b && b[0] == '1';
+        if (want && !v.bar && !v.bar_tried) {
+            v.bar_tried = true;
+            v.bar = bar_line(e->device);
+        }
+        v.req = want && v.bar ? static_cast<unsigned long long*>(v.bar) : v.box.as<unsigned long long>();
+    }
+    req_store(e, (unsigned long long)v.seq, (unsigned long long)v.seq);
     v.gen = v.gen % 0x7FFFFFFFu + 1u;
     uint32_t* ready = v.box.as<uint32_t>() + 8;
     __atomic_store_n(ready, 0u, __ATOMIC_RELEASE);
     uint32_t* w = v.words.as<uint32_t>();
     jsp::ServiceArgs a{};
-    a.mailbox = v.box.as<unsigned long long>();
+    a.mailbox = v.req;
     a.granules = v.granules.as<unsigned long long>();
     a.bell = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad);
     a.counter = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128);
@@ -1242,8 +1306,7 @@ uint32_t next_seq(uint32_t q) {
 // 16-byte load and takes a torn read for none).
 void svc_post(jsp_engine* e, uint32_t seq, uint32_t jw, uint32_t n_runs) {
     auto& v = e->svc;
-    __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)n_runs << 32) | seq, __ATOMIC_RELEASE);
-    __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
+    req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)n_runs << 32) | seq);
 }
 
 // Wait for the last snapshot patch's completion word (the rows are then in
@@ -1376,11 +1439,11 @@ void svc_wake(jsp_engine* e) {
         const uint32_t seq = next_seq(v.seq);
         v.seq = seq;
         v.last = std::chrono::steady_clock::now();
-        __atomic_store_n(v.box.as<unsigned long long>() + 1, (unsigned long long)seq, __ATOMIC_RELEASE);
+        req_store(e, (0x80000000ull << 32) | seq, (unsigned long long)seq);
         // rows marked patched, and they stay marked: the patch kernel may not
         // have landed when the warm-up loads them, so the next request (which
         // waits for the patch's completion word) loads them again
-        __atomic_store_n(v.box.as<unsigned long long>(), (0x80000000ull << 32) | seq, __ATOMIC_RELEASE);
+
         v.pending = seq;
     }
 }
@@ -1517,15 +1580,14 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         // load (an inline patch carried here: its n | flags in place of n_runs,
         // which only the fused shape reads and which never carries one inline)
         const uint32_t w2 = carry && (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : n_runs;
-        __atomic_store_n(v.box.as<unsigned long long>() + 1, ((unsigned long long)w2 << 32) | seq,
-                         __ATOMIC_RELEASE);
+
         // the compaction and split tiles keep their rows in LDS: bit 31 of J tells
         // them the snapshot was patched since their previous request (J < 2^30)
         const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? jsp::kReqDirty : 0u) |
                             (carry ? e->patch_bits : 0u);
         carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
         v.rows_dirty = false;
-        __atomic_store_n(v.box.as<unsigned long long>(), ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
+        req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)w2 << 32) | seq);
         const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
         if (rc == kSvcFailed) {
             v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
