@@ -721,13 +721,15 @@ jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_ru
         // write-through hand-off of the tallies to the tail (no release/acquire
         // fences) unless the tail's per-wave upper-class path, which reads them
         // with plain loads, will run
-        a.sc1_out = (!upper || f.fscr_words != 0) && !std::getenv("JSP_FENCED_HANDOFF") ? 1 : 0;
+        static const bool fenced = std::getenv("JSP_FENCED_HANDOFF") != nullptr;
+        a.sc1_out = (!upper || f.fscr_words != 0) && !fenced ? 1 : 0;
     }
     // class groups: a small snapshot's tiles are VALU-bound over many classes;
     // splitting the classes over up to 4 groups of >= 2 multiplies the tiles
     // (each row block read once per group), within 128 tiles
     f.groups = 1;
-    if (e->C > 2 && !std::getenv("JSP_NO_CLASS_GROUPS")) {
+    static const bool no_groups = std::getenv("JSP_NO_CLASS_GROUPS") != nullptr;
+    if (e->C > 2 && !no_groups) {
         const uint32_t by_c = std::min<uint32_t>(4, (e->C + 1) / 2);
         const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
         f.groups = std::max<uint32_t>(1, std::min(by_c, by_t));
@@ -824,10 +826,11 @@ uint32_t split_groups(jsp_engine* e) {
         const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
         g = std::max<uint32_t>(1, std::min(by_c, by_t));
     }
-    if (const char* v = std::getenv("JSP_SPLIT_GROUPS")) {
-        const long x = std::strtol(v, nullptr, 10);
-        if (x >= 1 && x <= (long)std::max<uint32_t>(e->C, 1)) g = (uint32_t)x;
-    }
+    static const long forced = [] {  // read once: split_groups runs on every host-API call
+        const char* v = std::getenv("JSP_SPLIT_GROUPS");
+        return v ? std::strtol(v, nullptr, 10) : 0L;
+    }();
+    if (forced >= 1 && forced <= (long)std::max<uint32_t>(e->C, 1)) g = (uint32_t)forced;
     while (g > 1 && e->n_blocks * g > kSvcMaxBlocks) --g;
     return g;
 }
@@ -853,7 +856,8 @@ int svc_shape(jsp_engine* e) {
     static const bool split_compact = [] { const char* v = std::getenv("JSP_SPLIT_COMPACT"); return v && v[0] == '1'; }();
     if (compact_ok(e) && !(split_compact && split_ok(e))) return 2;
     if (e->svc_mode == JSP_SERVICE_AUTO && split_ok(e)) return 3;
-    if (fused_ok(e) && !std::getenv("JSP_SERVICE_NO_FUSED")) return 1;
+    static const bool no_fused = std::getenv("JSP_SERVICE_NO_FUSED") != nullptr;
+    if (fused_ok(e) && !no_fused) return 1;
     return 0;
 }
 bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
@@ -2084,10 +2088,11 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     // followed by a warm-up request; otherwise the patch kernel.
     const auto t1 = std::chrono::steady_clock::now();
     const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
-    const bool up = svc_patch_on() && v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    const int pmode = svc_patch_mode();
+    const bool up = pmode != 0 && v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
     // a wake stages for the tile shapes' inline buffer once a service has run
     // (run_wake moves it to the descriptor if the fused shape starts instead)
-    const bool wake = !up && svc_patch_on() && svc_wake_wanted(e);
+    const bool wake = !up && pmode != 0 && svc_wake_wanted(e);
     // The delta into pinned staging, read in place. Patches for the service
     // of up to kPatchInlineRows rows go to its fixed inline buffer (layout
     // from n and the column flags, which ride in the request); larger ones,
@@ -2153,7 +2158,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     // the stream for the patch kernel.
     if (up) {
         e->patch_deferred = true;
-        if (svc_patch_mode() == 2) patch_post_deferred(e);  // posted now (svc_patch_mode)
+        if (pmode == 2) patch_post_deferred(e);  // posted now (svc_patch_mode)
     } else if (wake) {
         // held back; the waker restarts the service and posts it (run_wake)
         e->patch_deferred = true;
