@@ -116,3 +116,9 @@ tools/bin/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o
 	@mkdir -p build/diag2 tools/bin/diag
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_STAMPS -c -o build/diag2/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/diag2/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+# A/B build: the recovery's wake runs inside the patch call instead of the
+# waker thread (tools/cold_probe4.py loads it through JSP_LIB_PATH)
+tools/bin/ab_inlinewake/libjsplace.so: jobset_amd/csrc/jsp_engine.cc build/jsp_kernels.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_iw tools/bin/ab_inlinewake
+	$(HIPCC) $(HIPFLAGS) -DJSP_AB_INLINE_WAKE -x hip -c -o build/ab_iw/e.o jobset_amd/csrc/jsp_engine.cc
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/jsp_kernels.o build/ab_iw/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

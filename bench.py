@@ -669,13 +669,6 @@ def main() -> None:
                 if line["host_api_cold_recovery"] is not None and world == 1 and args.cpu_seconds > 0:
                     line["host_api_cold_recovery"]["cpu"] = cpu_cold_recovery(
                         pc, max(10, args.cold_trials // 4), sorted({1, 2, T}), idle_ms)
-                # A/B: the same placements with the walk on the GPU (the fused resident kernel)
-                eng.set_service(True, device_walk=True)
-                ab_shape = SHAPES[settled_place(eng, pc.job_class).fused]
-                ab = host_api_latency(eng, pc, 200)
-                ab["shape"] = ab_shape
-                line["host_api_resident_device_walk"] = ab
-                eng.set_service(True)
             eng.service_stop()
             if world == 1 and args.cpu_seconds > 0:
                 from oracle import oracle as O

@@ -48,11 +48,18 @@
  * (the first call on a different stream waits on an event of the previous
  * one), so a patch after a jsp_place_device never races its tally.
  *
- * Kernel-side failures: the single-class compaction's look-back has a bounded
- * spin. A launch that exceeds it writes its launch number to an error word
- * and leaves that launch's assign[] invalid. jsp_place reports it before it
+ * Kernel-side failures: every wait inside a launch is bounded -- the
+ * single-class compaction's look-back, the pipelined batch walk's wait for an
+ * earlier batch, the one-launch level walk's expanders' wait for the walker.
+ * A wait that gives up writes the launch's tag to an error word and leaves
+ * that launch's assign[] invalid. jsp_place reports it (JSP_EHIP) before it
  * returns; the device path reports it from jsp_engine_check (which waits for
- * the engine's work) or, once visible, from the next call on the engine.
+ * the engine's work) or, once visible, from the next call on the engine. No
+ * timeout returns JSP_OK with a stale assign[].
+ *
+ * Environment: JSP_SERVICE=0 (no resident service), JSP_SERVICE_IDLE_MS
+ * (its idle exit, default 50), JSP_RCCL_LIB (device sets) are the operational
+ * switches; JSP_TEST_HOOKS is for tests only (jsp_engine.cc TestHooks).
  */
 #ifndef JSPLACE_H
 #define JSPLACE_H
@@ -64,7 +71,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 5
+#define JSP_ABI_VERSION 6
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -123,7 +130,7 @@ typedef struct jsp_stats {
     uint32_t runs;             /* replicated-job runs the assignment walked */
     uint32_t fused;            /* launch shape: 0 tally->feas->assign, 1 fused tail, 2 one-class compaction,
                                   3 one-class compaction answered by the resident service,
-                                  4 fused shape answered by the resident service (walk on the GPU),
+                                  4 (unused since ABI v6: the fused resident kernel was retired),
                                   5 split service: resident tiles + the walk on the host,
                                   6 device set: shard tallies combined (RCCL / on-device add), then assign */
     double wall_us;            /* host wall time of the call */
@@ -152,6 +159,9 @@ typedef struct jsp_timing {
                                   launch path instead. When its grid cannot be co-resident the service stays
                                   off until the next upload; otherwise the next call starts it again */
     double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
+    double svc_pre_us;         /* service-answered jsp_place: entry of the service path to the request post
+                                  (a queued wake, settling the previous request, patch bookkeeping) (ABI v6) */
+    double svc_answer_us;      /* ... the request post to the answer's last entry seen (ABI v6) */
     /* jsp_snapshot_patch (ABI v5), host wall clock, always accumulated */
     uint64_t patches;          /* patch calls with at least one row */
     double patch_us;           /* their host time (a waker-thread restart is not in it) */
@@ -164,8 +174,9 @@ typedef struct jsp_timing {
                                  for one leaf-level class, the fused tail for small snapshots */
 
 /* jsp_engine_set_service modes. With AUTO, a host-API jsp_place of the
- * one-class compaction shape or of the fused shape (no tallies requested) is
- * answered by a resident service kernel: one workgroup per tile stays on the
+ * one-class compaction shape or of a multi-class / multi-level shape whose
+ * tiles fit the GPU at once (no tallies requested) is answered by a resident
+ * service kernel: one workgroup per tile stays on the
  * GPU, a dispatcher workgroup polls a request word in pinned host memory, and
  * assign[] goes back into pinned memory -- no launch per placement. It is started by the first such
  * jsp_place, stopped by every upload, jsp_engine_set_service/set_fused and
@@ -181,8 +192,6 @@ typedef struct jsp_timing {
 #define JSP_SERVICE_AUTO 1     /* default: the multi-class / multi-level shapes are answered by the split
                                   service -- resident tiles tally and hand back per-domain feasibility,
                                   the host walks (stats.fused = 5) */
-#define JSP_SERVICE_DEVICE_WALK 2  /* as AUTO, but those shapes walk on the GPU too (the fused resident
-                                      kernel, stats.fused = 4); kept for A/B measurement */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);
@@ -222,16 +231,15 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nodes);
  *    rows; no launch. The patch is posted at once, so it lands during the gap
  *    before the next request, and a request that finds it not yet taken
  *    carries it again (writing a staged delta twice writes the same values);
+ *    a dispatcher that never takes it (bounded wait) is stopped and the patch
+ *    kernel applies it;
  *  - after the service left, while it is armed (the last jsp_place was
  *    answered by it): a patch is the first sign of a recovery, so the engine's
  *    waker thread restarts the service and posts the patch, followed by a
  *    warm-up request without jobs, off the caller's thread;
  *  - otherwise a patch kernel on the engine stream.
  * Later launches wait for its completion word (or are stream-ordered after
- * the patch kernel); uploads and jsp_engine_sync apply pending patches first.
- * JSP_SVC_PATCH=0 (always the kernel), =1 (held back for the next request),
- * JSP_SVC_WAKER=0 (the patch call restarts the service itself) and
- * JSP_SVC_WAKE=0 (no restart on a patch) are A/B switches. */
+ * the patch kernel); uploads and jsp_engine_sync apply pending patches first. */
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n,
                        const uint64_t* labels, const uint32_t* taints,
                        const uint32_t* free_res, const int32_t* excl_owner);

@@ -1,10 +1,7 @@
 // jsp_engine.cc — host side of the exclusive-topology placement engine:
 // the C ABI of include/jsplace.h over HIP device buffers and the kernels of
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
-#include <dlfcn.h>
 #include <hip/hip_runtime.h>
-#include <hsa/hsa.h>
-#include <hsa/hsa_ext_amd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -133,6 +130,60 @@ struct EvPair {
     int tag = 0;  // 0 tally, 1 feas, 2 assign, 3 fused
 };
 
+// Test hooks: JSP_TEST_HOOKS="name=value,...", read at engine creation and
+// again at each snapshot upload. They force, at test sizes, the shapes the
+// engine otherwise picks only for large geometries (the double-buffered and
+// workgroup tallies, multi-chunk tally blocks), shorten the kernels' bounded
+// waits so that their error path runs, and stand in for a smaller GPU. The
+// library's other environment switches are operational only: JSP_SERVICE,
+// JSP_SERVICE_IDLE_MS and (device sets) JSP_RCCL_LIB.
+struct TestHooks {
+    bool tally_one = true;          // tally_one=0: the double-buffered wave tally at any size
+    bool tally_block = false;       // tally_block=1: the workgroup tally instead of the wave tiles
+    uint32_t block_chunks = 1;      // block_chunks=N (1..8): 1024-row chunks per tally workgroup
+    uint32_t block_rows = 0;        // block_rows=N (>= 60): smaller tally row blocks (more tiles)
+    uint32_t lookback_spins = 1u << 22;  // lookback_spins=N: compaction look-back polls before giving up
+    uint32_t pipe_spins = 1u << 24;      // pipe_spins=N: the pipelined batch walk's polls of an earlier batch
+    uint64_t wait_ticks = 200000000ull;  // wait_us=N: the level walk's expanders' wait (100 MHz ticks; 2 s)
+    int cu_limit = 0;               // cu_limit=N: CUs the resident service may count on
+    bool svc_xcd = true;            // svc_xcd=0: the compaction service spread over the XCDs (the
+                                    //   write-through protocol a partition mode would run)
+    uint32_t seq0 = 0;              // seq0=N: the service's first request number
+    bool have_seq0 = false;
+};
+
+TestHooks read_hooks() {
+    TestHooks h;
+    const char* s = std::getenv("JSP_TEST_HOOKS");
+    if (!s) return h;
+    std::string all(s);
+    size_t p = 0;
+    while (p < all.size()) {
+        size_t q = all.find(',', p);
+        if (q == std::string::npos) q = all.size();
+        const std::string kv = all.substr(p, q - p);
+        p = q + 1;
+        const size_t eq = kv.find('=');
+        if (eq == std::string::npos) continue;
+        const std::string k = kv.substr(0, eq);
+        const unsigned long long v = std::strtoull(kv.c_str() + eq + 1, nullptr, 0);
+        if (k == "tally_one") h.tally_one = v != 0;
+        else if (k == "tally_block") h.tally_block = v != 0;
+        else if (k == "block_chunks" && v >= 1 && v <= 8) h.block_chunks = (uint32_t)v;
+        else if (k == "block_rows" && v >= 60) h.block_rows = (uint32_t)v;
+        else if (k == "lookback_spins") h.lookback_spins = (uint32_t)v;
+        else if (k == "pipe_spins") h.pipe_spins = (uint32_t)v;
+        else if (k == "wait_us") h.wait_ticks = v * 100ull;
+        else if (k == "cu_limit") h.cu_limit = (int)v;
+        else if (k == "svc_xcd") h.svc_xcd = v != 0;
+        else if (k == "seq0") {
+            h.seq0 = (uint32_t)v;
+            h.have_seq0 = true;
+        }
+    }
+    return h;
+}
+
 }  // namespace
 
 int jsp_internal_set_err(int code, const char* fmt, ...) {
@@ -166,9 +217,7 @@ struct jsp_engine {
     std::vector<int32_t> h_par[JSP_MAX_LEVELS];
     std::vector<uint32_t> blk_l0, blk_l1;  // leaf range of each tally row block
     uint32_t max_blk_span = 0;             // rows a tally block's first chunk spans, max over blocks
-    bool tally_one = true;                 // one-tile-per-wave tally kernel when the tiles fit (JSP_TALLY_ONE)
-    uint32_t expand_rpw = 16;              // assignment records per expand wave (JSP_EXPAND_RPW, 1..64)
-    bool assign_records = true;            // long runs as records + expand_kernel (JSP_ASSIGN_RECORDS=0: staged stores)
+    TestHooks hooks;                       // JSP_TEST_HOOKS (tests only; defaults otherwise)
     jsp::HostWalk walk;
 
     // snapshot
@@ -204,6 +253,7 @@ struct jsp_engine {
     bool patch_pending = false;
     DevBuf lvl_ready;                   // the one-launch level walk's published record count
     uint32_t lvl_epoch = 0;
+    uint32_t err_tag = 0;               // launches that may report a timed-out wait (kernel error words)
     bool patch_svc = false;             // the pending patch goes to the service's dispatcher
     bool patch_deferred = false;        // ... and is held back for the next request (not posted yet)
     uint32_t patch_bits = 0;            // its request bits (kReqPatch, kReqPatchInline)
@@ -226,8 +276,8 @@ struct jsp_engine {
     // draws on the single-launch kernels' tickets so far (DevBuf ticket [0]
     // tiles, [1] finished tiles): every launch adds its grid / tile count
     unsigned long long tile_draws = 0, done_draws = 0;
-    // test hook, read at snapshot upload: JSP_LOOKBACK_SPINS (look-back polls
-    // before a compaction tile gives up)
+    // look-back polls before a compaction tile gives up (hooks.lookback_spins,
+    // taken at snapshot upload)
     uint32_t spin_limit = 1u << 22;
 
     // stream ordering: work is enqueued on the engine stream or a caller's;
@@ -240,8 +290,6 @@ struct jsp_engine {
     bool last_foreign = false;          // the last call enqueued on a caller's stream
     hipEvent_t ev_switch = nullptr;     // recorded on the engine stream
     hipEvent_t ev_last = nullptr;       // recorded on the last caller stream, at the end of its call
-    HostBuf mark;                       // stream-marker word (JSP_STREAM_MARK=value): written by the caller's
-    uint64_t mark_seq = 0;              //   stream at the end of a device call, waited on by the next stream
 
     // resident placement service: the compaction shape kept on the GPU
     // between host-API placements (place_service_kernel), fed by a host-mapped
@@ -250,28 +298,19 @@ struct jsp_engine {
         bool running = false;
         hipStream_t stream = nullptr;
         HostBuf box;     // request: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; u32 [8] ready
-        // The request words the dispatcher polls: box, or (JSP_SVC_BAR=1) a
-        // line of fine-grained device memory the host writes through the BAR
-        // -- the dispatcher's polls then stay on the device
-        unsigned long long* req = nullptr;
-        void* bar = nullptr;     // that line (hipFree at engine destruction)
-        bool bar_tried = false;
         HostBuf words;   // done[nb] | stats[2] | err[1] | clk[kSvcClkSlots nb]
         HostBuf assign;  // [cap]
-        HostBuf runs;    // fused shape: run_class[cap_runs] | run_len[cap_runs]
-        DevBuf granules; // compaction granules | bell | counter | n_runs, one 128-B line each after the granules
-        DevBuf tally;    // fused shape: the service's own cap[C][L] | occ[L] (device-path launches use e->cap)
+        DevBuf granules; // compaction granules | bell, one 128-B line each after the granules | XCC votes
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
         HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
-        HostBuf pstage;  // inline patch staging (kReqPatchInline, jsp_internal.h)
+        HostBuf pstage;  // inline patch staging (kReqPatchInline, jsp_internal.h), sized at snapshot upload
         uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
         uint32_t blocks = 0;           // row blocks the running service was started for
-        uint32_t cap = 0, cap_runs = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
-        int shape = 0;   // 2 compaction, 1 fused
+        uint32_t cap = 0, nb = 0, seq = 0, err_ack = 0, gen = 0;
+        int shape = 0;   // 2 compaction, 3 split
         bool clk = false;
         bool rows_dirty = true;  // a patch since the last request: its tiles reload their rows from memory
         uint32_t pending = 0;    // a compaction request answered early: its tiles' done words still to come
-        bool early = true;       // compaction answers read from the tagged entries (JSP_SVC_EARLY=0: done words)
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
         std::chrono::steady_clock::time_point t_launch{};
@@ -316,27 +355,16 @@ struct jsp_engine {
         if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.stream) (void)hipStreamDestroy(svc.stream);
-        if (svc.bar) (void)hipFree(svc.bar);
     }
 };
 
 namespace {
 
-constexpr uint32_t kMaxBlockChunks = 8;
-
-// 1024-row chunks per tally workgroup. One: measured on MI355X (cfg4, 1M rows,
-// C=4) the tally takes 14.2 / 18.9 / 23.2 / 28.4 / 39.2 us at 1/2/3/4/8 chunks
-// per workgroup -- the chunk's row/leaf passes, not its HBM loads, set a
-// workgroup's time, and more, smaller-grid workgroups hide each other's
-// latency better than a next-chunk prefetch does. JSP_BLOCK_CHUNKS overrides
-// it (tuning experiments; the parity tests cover 2, 3 and 8).
-uint32_t block_chunks(uint32_t /*N*/) {
-    if (const char* v = std::getenv("JSP_BLOCK_CHUNKS")) {
-        const long x = std::strtol(v, nullptr, 10);
-        if (x >= 1 && x <= (long)kMaxBlockChunks) return (uint32_t)x;
-    }
-    return 1;
-}
+// 1024-row chunks per tally workgroup: one (hooks.block_chunks in tests).
+// Measured on MI355X (cfg4, 1M rows, C=4) the tally takes 14.2 / 18.9 / 23.2 /
+// 28.4 / 39.2 us at 1/2/3/4/8 chunks per workgroup -- the chunk's row/leaf
+// passes, not its HBM loads, set a workgroup's time, and more, smaller-grid
+// workgroups hide each other's latency better than a next-chunk prefetch does.
 constexpr size_t kMaxEvents = 3 * 4096;
 // Above this many tally workgroups the three-launch shape wins: the fused tail
 // runs feasibility + assignment on one 256-thread workgroup.
@@ -345,44 +373,15 @@ constexpr uint32_t kFusedMaxBlocks = 256;
 // Make stream s wait for everything the engine enqueued before (on any
 // stream): the engine stream's work through an event recorded on it now, a
 // caller stream's through ev_last, recorded at the end of the call that used
-// it (that stream itself is never touched again: it may be gone).
-// How the end of a device call on a caller's stream is marked (A/B,
-// JSP_STREAM_MARK): 0 an engine-owned event (default), 1 a stream write of a
-// host-mapped sequence word that later streams wait on, 2 nothing (unsafe:
-// measurement only).
-int stream_mark_mode() {
-    static const int m = [] {
-        const char* v = std::getenv("JSP_STREAM_MARK");
-        if (!v) return 0;
-        if (std::strcmp(v, "value") == 0) return 1;
-        if (std::strcmp(v, "none") == 0) return 2;
-        if (std::strcmp(v, "record") == 0) return 3;
-        return 0;
-    }();
-    return m;
-}
-// Mode 0 (default): ev_last rides on the call's kernel launches as their stop
-// event (jsp::set_launch_stop), so it completes with the last kernel and no
-// marker packet follows it; a call that launched nothing records it. Mode 3:
-// an hipEventRecord after every call (the round-2 fix; A/B).
-
-// Flags of ev_last (JSP_EVENT_FLAGS: "sys" = a system-scope release on record,
-// the HIP default; "dev" = device-scope release; "nofence" = none). Ordering a
-// later stream after the device call needs only device scope.
-unsigned ev_last_flags() {
-    const char* v = std::getenv("JSP_EVENT_FLAGS");
-    if (v && std::strcmp(v, "sys") == 0) return hipEventDisableTiming;
-    if (v && std::strcmp(v, "nofence") == 0) return hipEventDisableTiming | hipEventDisableSystemFence;
-    return hipEventDisableTiming | hipEventReleaseToDevice;
-}
-
+// it (that stream itself is never touched again: it may be gone). ev_last
+// rides on the call's kernel launches as their stop event
+// (jsp::set_launch_stop), so it completes with the last kernel and no marker
+// packet follows it; a call that launched nothing records it. Its release is
+// device scope: ordering a later stream after the device call needs no more.
 int wait_prior(jsp_engine* e, hipStream_t s) {
     if (!e->have_last) return JSP_OK;
     if (e->last_foreign) {
-        const int mm = stream_mark_mode();
-        if (mm == 0 || mm == 3) HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
-        else if (mm == 1)
-            HIP_TRY(hipStreamWaitValue64(s, e->mark.p, e->mark_seq, hipStreamWaitValueGte, ~0ull));
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_last, 0));
     } else {
         if (!e->ev_switch) HIP_TRY(hipEventCreateWithFlags(&e->ev_switch, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(e->ev_switch, e->stream));
@@ -400,40 +399,26 @@ int enter_stream(jsp_engine* e, hipStream_t s) {
     if (int rc = patch_fence(e)) return rc;
     if (e->have_last && e->last_stream != s)
         if (int rc = wait_prior(e, s)) return rc;
-    if (s != e->stream && stream_mark_mode() == 0) jsp::set_launch_stop(e->ev_last);
+    if (s != e->stream) jsp::set_launch_stop(e->ev_last);
     return JSP_OK;
 }
 
 // After a call enqueued its work on s: a caller's stream gets ev_last
-// recorded on it while the handle is known to be valid.
+// recorded on it (when no launch carried it) while the handle is known to be
+// valid.
 int leave_stream(jsp_engine* e, hipStream_t s) {
     const bool launched = jsp::launch_stop_used();
     jsp::set_launch_stop(nullptr);
     e->last_stream = s;
     e->have_last = true;
     e->last_foreign = s != e->stream;
-    if (e->last_foreign) {
-        const int mm = stream_mark_mode();
-        if ((mm == 0 && !launched) || mm == 3) {
-            HIP_TRY(hipEventRecord(e->ev_last, s));
-        } else if (mm == 1) {
-            if (!e->mark.p) {
-                HIP_TRY(e->mark.reserve(64));
-                std::memset(e->mark.p, 0, 64);
-            }
-            HIP_TRY(hipStreamWriteValue64(s, e->mark.p, ++e->mark_seq, 0));
-        }
-    }
+    if (e->last_foreign && !launched) HIP_TRY(hipEventRecord(e->ev_last, s));
     return JSP_OK;
 }
 
 // Host wait for the last caller-stream call's work.
 int wait_last_foreign(jsp_engine* e) {
-    const int mm = stream_mark_mode();
-    if (mm == 0 || mm == 3) HIP_TRY(hipEventSynchronize(e->ev_last));
-    else if (mm == 1)
-        while (__atomic_load_n(e->mark.as<uint64_t>(), __ATOMIC_ACQUIRE) < e->mark_seq) __builtin_ia32_pause();
-    else HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipEventSynchronize(e->ev_last));
     return JSP_OK;
 }
 
@@ -445,16 +430,31 @@ int use_engine_stream(jsp_engine* e) {
     return leave_stream(e, e->stream);
 }
 
-// Non-blocking: a compaction launch whose look-back timed out has written its
-// epoch to the host-mapped error word. Reported once, by the next call.
+// Non-blocking: a launch whose bounded wait timed out has written its tag to
+// the host-mapped error word (jsp_internal.h kErr*: the kind in the top two
+// bits). Reported once, by the next call.
 int check_launch_error(jsp_engine* e) {
     const uint32_t w = __atomic_load_n(e->h_err.as<uint32_t>(), __ATOMIC_ACQUIRE);
     if (w != e->err_ack) {
         e->err_ack = w;
+        const uint32_t kind = w & jsp::kErrKindMask, n = w & ~jsp::kErrKindMask;
+        if (kind == jsp::kErrExpand)
+            return set_err(JSP_EHIP, "placement launch %u failed: the level walk's expanders timed out waiting for "
+                                     "the walker's records; that launch's assign[] is invalid", n);
+        if (kind == jsp::kErrPipe)
+            return set_err(JSP_EHIP, "placement launch %u failed: the pipelined batch walk timed out waiting for an "
+                                     "earlier batch; that launch's assign[] is invalid", n);
         return set_err(JSP_EHIP, "placement launch %u failed: the compaction look-back timed out (a workgroup "
-                                 "never published its count); that launch's assign[] is invalid", w);
+                                 "never published its count); that launch's assign[] is invalid", n);
     }
     return JSP_OK;
+}
+
+// The next error tag of a launch that may time out in a bounded wait (never
+// 0 in the low 30 bits, so it always differs from an acknowledged word).
+uint32_t next_err_tag(jsp_engine* e, uint32_t kind) {
+    e->err_tag = e->err_tag % 0x3FFFFFFFu + 1u;
+    return kind | e->err_tag;
 }
 
 // Host placement path: wait for the kernel's completion words (one per
@@ -560,43 +560,34 @@ jsp::TallyArgs tally_args(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint3
     return a;
 }
 
-// Workgroups of the wave-tile tally: JSP_TALLY_WPS waves per SIMD (default 4:
-// best warm and cold of 1-8 on cfg4, tools/ab_probe.py tally, profiles/r03)
-// over the CUs, never more than the tiles need and never fewer than 64 tiles
-// per wave allow.
+// Workgroups of the wave-tile tally: 4 waves per SIMD (best warm and cold of
+// 1-8 on cfg4, profiles/r03) over the CUs, never more than the tiles need and
+// never fewer than 64 tiles per wave allow.
 uint32_t tally_wave_grid(jsp_engine* e) {
     // one tile per wave (grid 0: the one-set kernel) while every tile fits
-    // 6 waves per SIMD (JSP_TALLY_ONE=0 at engine creation: the
-    // double-buffered kernel, A/B and tests)
-    if (e->tally_one && e->n_wtiles <= (uint32_t)std::max(e->n_cu, 1) * 4u * 6u) return 0;
-    static const uint32_t wps = [] {
-        const char* v = std::getenv("JSP_TALLY_WPS");
-        const long x = v ? std::strtol(v, nullptr, 10) : 4;
-        return (uint32_t)(x >= 1 && x <= 16 ? x : 4);
-    }();
+    // 6 waves per SIMD; beyond that the double-buffered kernel
+    if (e->hooks.tally_one && e->n_wtiles <= (uint32_t)std::max(e->n_cu, 1) * 4u * 6u) return 0;
+    constexpr uint32_t wps = 4;
     // at least n_wtiles / 64 waves: a wave holds at most 64 tile descriptors
     const uint32_t waves = std::max<uint32_t>(std::min<uint32_t>(e->n_wtiles, (uint32_t)std::max(e->n_cu, 1) * 4u * wps),
                                               (e->n_wtiles + 63) / 64);
     return std::max<uint32_t>(1, (waves + jsp::kTallyWaves - 1) / jsp::kTallyWaves);
 }
 
-// The tally alone (three-launch shape, jsp_tally_device): the wave-tile
-// kernel; JSP_TALLY_BLOCK=1 runs the workgroup-block kernel instead (A/B).
 // Whether the wave tally can fold the feasibility words into itself (the
 // three-launch shape on the engine's own unsharded tallies): at most 4
 // classes (one wave pass), all at the leaf level, wave tiles available.
-// JSP_FEAS_FOLD=0 keeps the feasibility launch (A/B).
 bool fold_ok(jsp_engine* e) {
-    static const bool on = [] { const char* v = std::getenv("JSP_FEAS_FOLD"); return !(v && v[0] == '0'); }();
-    if (!on || e->C < 1 || e->C > 4 || e->n_wtiles == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total)
+    if (e->C < 1 || e->C > 4 || e->n_wtiles == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total ||
+        e->hooks.tally_block)
         return false;
-    static const bool block = [] { const char* v = std::getenv("JSP_TALLY_BLOCK"); return v && v[0] == '1'; }();
-    if (block) return false;
     for (const auto& c : e->cls_h)
         if (c.level + 1 != e->K) return false;
     return (uint64_t)(e->C + 1) * e->L_total * 4 < (1ull << 31);
 }
 
+// The tally alone (three-launch shape, jsp_tally_device): the wave-tile
+// kernel when every leaf fits a wave tile, else the workgroup-block kernel.
 int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s, bool fold = false) {
     jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
     if (fold) {
@@ -604,7 +595,7 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
         a.fold_nw = (e->L_total + 63) / 64;
     }
     if (e->n_blocks == 0) return JSP_OK;
-    static const bool block = [] { const char* v = std::getenv("JSP_TALLY_BLOCK"); return v && v[0] == '1'; }();
+    const bool block = e->hooks.tally_block;
     EvPair* p = ev_begin(e, 0, s);
     uint32_t c0 = 0;
     do {
@@ -625,10 +616,9 @@ int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hip
 uint32_t* stats_ptr(jsp_engine* e) { return e->stats_override ? e->stats_override : e->stats.as<uint32_t>(); }
 
 // The level walker's shape: every class at one level of <= kLevelMaxWords
-// words, <= kLevelMaxRuns runs, records on (JSP_ASSIGN_LEVEL=0: off, A/B).
+// words, <= kLevelMaxRuns runs.
 bool level_walk_ok(jsp_engine* e, uint32_t n_runs) {
-    static const bool on = [] { const char* v = std::getenv("JSP_ASSIGN_LEVEL"); return !(v && v[0] == '0'); }();
-    if (!on || !e->assign_records || e->C < 1 || n_runs > jsp::kLevelMaxRuns) return false;
+    if (e->C < 1 || n_runs > jsp::kLevelMaxRuns) return false;
     const uint32_t lvl = e->cls_h[0].level;
     for (const auto& c : e->cls_h)
         if (c.level != lvl) return false;
@@ -647,31 +637,29 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
     p = ev_begin(e, 2, s);
     if (e->recs.reserve(sizeof(jsp::AssignRec) * (size_t)std::max<uint32_t>(J, 1), grave(e)) != hipSuccess)
         return set_err(JSP_ENOMEM, "assignment records (%u jobs)", J);
+    jsp::WaitErr we{e->h_err.as<uint32_t>(), 0u, e->hooks.pipe_spins, e->hooks.wait_ticks};
     if (level_walk_ok(e, n_runs)) {
+        // the expansion rides in the walker's launch: its expanders wait
+        // (bounded) for the walker's record count, and one that gives up
+        // writes the launch's tag to the error word (kErrExpand)
         const uint32_t nw = (e->D[e->cls_h[0].level] + 63) / 64;
-        // the expansion rides in the walker's launch (JSP_LEVEL_ONE_LAUNCH=0: a second launch, A/B)
-        const char* ov = std::getenv("JSP_LEVEL_ONE_LAUNCH");  // read per call (in-process A/B)
-        const bool one = !(ov && ov[0] == '0');
-        unsigned long long* ready = nullptr;
-        if (one) {
-            if (!e->lvl_ready.p) {
-                HIP_TRY(e->lvl_ready.reserve(64));
-                HIP_TRY(hipMemsetAsync(e->lvl_ready.p, 0, 64, s));
-            }
-            ready = e->lvl_ready.as<unsigned long long>();
-            e->lvl_epoch = e->lvl_epoch % 0x7FFFFFFFu + 1u;
+        if (!e->lvl_ready.p) {
+            HIP_TRY(e->lvl_ready.reserve(64));
+            HIP_TRY(hipMemsetAsync(e->lvl_ready.p, 0, 64, s));
         }
+        e->lvl_epoch = e->lvl_epoch % 0x7FFFFFFFu + 1u;
+        we.tag = next_err_tag(e, jsp::kErrExpand);
         HIP_TRY(jsp::launch_assign_level(e->feas.as<uint64_t>(), e->C, nw, d_run_class, d_run_len, n_runs, J, d_assign,
-                                         stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(),
-                                         e->expand_rpw, s, ready, e->lvl_epoch));
+                                         stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(), s,
+                                         e->lvl_ready.as<unsigned long long>(), e->lvl_epoch, we));
         ev_end(p, s);
         return JSP_OK;
     }
+    we.tag = next_err_tag(e, jsp::kErrPipe);
     HIP_TRY(jsp::launch_assign(e->feas.as<uint64_t>(), e->word_off.as<uint32_t>(), e->cls.as<jsp::DevClass>(),
                                e->C, e->topo, e->t_off_h[e->K], e->feas_words, d_run_class, d_run_len, n_runs, J,
-                               d_assign,
-                               stats_ptr(e), e->stats.as<uint32_t>() + 3,
-                               e->assign_records ? e->recs.as<jsp::AssignRec>() : nullptr, e->expand_rpw, s));
+                               d_assign, stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(), s,
+                               we));
     ev_end(p, s);
     return JSP_OK;
 }
@@ -721,21 +709,20 @@ jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_ru
         // write-through hand-off of the tallies to the tail (no release/acquire
         // fences) unless the tail's per-wave upper-class path, which reads them
         // with plain loads, will run
-        static const bool fenced = std::getenv("JSP_FENCED_HANDOFF") != nullptr;
-        a.sc1_out = (!upper || f.fscr_words != 0) && !fenced ? 1 : 0;
+        a.sc1_out = !upper || f.fscr_words != 0 ? 1 : 0;
     }
     // class groups: a small snapshot's tiles are VALU-bound over many classes;
     // splitting the classes over up to 4 groups of >= 2 multiplies the tiles
     // (each row block read once per group), within 128 tiles
     f.groups = 1;
-    static const bool no_groups = std::getenv("JSP_NO_CLASS_GROUPS") != nullptr;
-    if (e->C > 2 && !no_groups) {
+    if (e->C > 2) {
         const uint32_t by_c = std::min<uint32_t>(4, (e->C + 1) / 2);
         const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
         f.groups = std::max<uint32_t>(1, std::min(by_c, by_t));
     }
     f.cpg = (a.nc + f.groups - 1) / f.groups;
-    f.pipe = jsp::pipe_walk_enabled() ? 1u : 0u;
+    f.we = jsp::WaitErr{e->h_err.as<uint32_t>(), next_err_tag(e, jsp::kErrPipe), e->hooks.pipe_spins,
+                        e->hooks.wait_ticks};
     f.lds_bytes = jsp::fused_lds_bytes(f.t_words, f.feas_words, f.cpg, f.cpg + a.do_occ, a.la,
                                        f.topo_in_lds ? topo_words : 0u, f.fscr_words);
     return f;
@@ -805,7 +792,6 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
 // service is seen by a stream query and the request re-posted once).
 constexpr uint32_t kSvcMaxBlocks = 255;  // one tile per workgroup + the dispatcher, all co-resident (<= one per CU)
 constexpr int kSvcGone = 1;
-constexpr int kSvcUseLaunch = 2;  // svc_place: the service is (re)starting; answer this call on the launch path
 
 double svc_idle_ms() {
     static const double ms = [] {
@@ -817,8 +803,8 @@ double svc_idle_ms() {
 }
 
 // Class groups of the split service's tiles: as the fused shape's (up to 4
-// groups of >= 2 classes, within 128 tiles); JSP_SPLIT_GROUPS overrides it
-// (A/B runs), capped by the co-resident tile limit.
+// groups of >= 2 classes, within 128 tiles), capped by the co-resident tile
+// limit.
 uint32_t split_groups(jsp_engine* e) {
     uint32_t g = 1;
     if (e->C > 2) {
@@ -826,11 +812,6 @@ uint32_t split_groups(jsp_engine* e) {
         const uint32_t by_t = std::max<uint32_t>(1, 128 / std::max<uint32_t>(e->n_blocks, 1));
         g = std::max<uint32_t>(1, std::min(by_c, by_t));
     }
-    static const long forced = [] {  // read once: split_groups runs on every host-API call
-        const char* v = std::getenv("JSP_SPLIT_GROUPS");
-        return v ? std::strtol(v, nullptr, 10) : 0L;
-    }();
-    if (forced >= 1 && forced <= (long)std::max<uint32_t>(e->C, 1)) g = (uint32_t)forced;
     while (g > 1 && e->n_blocks * g > kSvcMaxBlocks) --g;
     return g;
 }
@@ -845,65 +826,27 @@ bool split_ok(jsp_engine* e) {
 }
 
 // The shape the service would run for the engine's current state (2
-// compaction, 3 split, 1 fused), 0 = none. The split shape answers
-// everything the fused one would (and more: no LDS limit on the walk);
-// JSP_SERVICE_DEVICE_WALK keeps the fused device walk (A/B), JSP_SPLIT_COMPACT=1
-// sends the one-class leaf shape through the split service too.
+// compaction, 3 split), 0 = none. The split shape answers every multi-class
+// or multi-level shape the fused launch would (and more: no LDS limit on the
+// walk, which runs on the host).
 int svc_shape(jsp_engine* e) {
     if (e->svc_mode == JSP_SERVICE_OFF || !e->have_topo || !e->have_snap || !e->have_cls ||
         e->n_blocks > kSvcMaxBlocks || e->svc.broken)
         return 0;
-    static const bool split_compact = [] { const char* v = std::getenv("JSP_SPLIT_COMPACT"); return v && v[0] == '1'; }();
-    if (compact_ok(e) && !(split_compact && split_ok(e))) return 2;
-    if (e->svc_mode == JSP_SERVICE_AUTO && split_ok(e)) return 3;
-    static const bool no_fused = std::getenv("JSP_SERVICE_NO_FUSED") != nullptr;
-    if (fused_ok(e) && !no_fused) return 1;
+    if (compact_ok(e)) return 2;
+    if (split_ok(e)) return 3;
     return 0;
 }
 bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
-// A request line in device memory the CPU may write (fine-grained device
-// memory opened to the CPU agent; absent without a large BAR). HSA entry
-// points come from the runtime HIP already loaded (no second runtime).
-void* bar_line(int device) {
-    using IterFn = hsa_status_t (*)(hsa_status_t (*)(hsa_agent_t, void*), void*);
-    using InfoFn = hsa_status_t (*)(hsa_agent_t, hsa_agent_info_t, void*);
-    using AllowFn = hsa_status_t (*)(uint32_t, const hsa_agent_t*, const uint32_t*, const void*);
-    auto iter = reinterpret_cast<IterFn>(dlsym(RTLD_DEFAULT, "hsa_iterate_agents"));
-    static InfoFn info = nullptr;
-    info = reinterpret_cast<InfoFn>(dlsym(RTLD_DEFAULT, "hsa_agent_get_info"));
-    auto allow = reinterpret_cast<AllowFn>(dlsym(RTLD_DEFAULT, "hsa_amd_agents_allow_access"));
-    if (!iter || !info || !allow) return nullptr;
-    hsa_agent_t cpu{};
-    auto find = [](hsa_agent_t a, void* out) -> hsa_status_t {
-        hsa_device_type_t t;
-        if (info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS && t == HSA_DEVICE_TYPE_CPU) {
-            auto* c = static_cast<hsa_agent_t*>(out);
-            if (c->handle == 0) *c = a;
-        }
-        return HSA_STATUS_SUCCESS;
-    };
-    if (iter(find, &cpu) != HSA_STATUS_SUCCESS || cpu.handle == 0) return nullptr;
-    (void)hipSetDevice(device);
-    void* p = nullptr;
-    if (hipExtMallocWithFlags(&p, 4096, hipDeviceMallocFinegrained) != hipSuccess || !p) return nullptr;
-    if (allow(1, &cpu, nullptr, p) != HSA_STATUS_SUCCESS) {
-        (void)hipFree(p);
-        return nullptr;
-    }
-    std::memset(p, 0, 64);  // through the BAR
-    __builtin_ia32_sfence();
-    return p;
-}
-
-// Store request words: the second half first (the dispatcher reads both in
-// one 16-byte load and takes a torn read for none); a BAR line is flushed
-// from the write-combining buffers at once.
+// Store request words (pinned host memory the dispatcher polls): the second
+// half first (the dispatcher reads both in one 16-byte load and takes a torn
+// read for none). A request line in device memory written through the BAR
+// was measured slower on every shape.
 void req_store(jsp_engine* e, unsigned long long w0, unsigned long long w1, bool both = true) {
-    unsigned long long* r = e->svc.req ? e->svc.req : e->svc.box.as<unsigned long long>();
+    unsigned long long* r = e->svc.box.as<unsigned long long>();
     if (both) __atomic_store_n(r + 1, w1, __ATOMIC_RELEASE);
     __atomic_store_n(r, w0, __ATOMIC_RELEASE);
-    if (e->svc.req && e->svc.req != e->svc.box.as<unsigned long long>()) __builtin_ia32_sfence();
 }
 
 int patch_wait(jsp_engine* e);
@@ -919,10 +862,9 @@ int svc_stop(jsp_engine* e) {
     req_store(e, (unsigned long long)jsp::kSvcStop, 0, false);
     // The kernel leaves within microseconds of the stop word: poll for it
     // rather than sleep in a blocking synchronize (whose wake-up costs more
-    // than the exit itself); after 2 ms, block (JSP_SVC_STOP_SPIN=0: always block)
-    static const bool spin = [] { const char* c = std::getenv("JSP_SVC_STOP_SPIN"); return !(c && c[0] == '0'); }();
+    // than the exit itself); after 2 ms, block
     hipError_t q = hipErrorNotReady;
-    if (spin) {
+    {
         const auto t0 = std::chrono::steady_clock::now();
         while ((q = hipStreamQuery(v.stream)) == hipErrorNotReady &&
                std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(2))
@@ -947,7 +889,7 @@ int svc_suspend(jsp_engine* e) {
     return svc_stop(e);
 }
 
-int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready);
+int svc_start(jsp_engine* e, uint32_t J, bool wait_ready);
 int svc_wait_ready(jsp_engine* e);
 // The upload returns once the new service polls, so the recovery's "post-delete
 // snapshot uploaded -> jsp_place" finds it ready instead of waiting for its
@@ -955,35 +897,16 @@ int svc_wait_ready(jsp_engine* e);
 void svc_resume(jsp_engine* e) {
     if (e->svc.resume && svc_ok(e)) {
         e->svc.resume = false;
-        (void)svc_start(e, 0, 0, true);
+        (void)svc_start(e, 0, true);
     }
 }
 
-// The compaction service's resident path (ServiceArgs::resident;
-// JSP_SVC_RESIDENT=0: the LDS row cache path). Read at each service start.
-bool svc_resident() {
-    const char* c = std::getenv("JSP_SVC_RESIDENT");
-    return !(c && c[0] == '0');
-}
+void start_waker(jsp_engine* e);
 
-// The compaction service co-located on one XCD (ServiceArgs::spread;
-// JSP_SVC_XCD=0: off). Read at each service start (in-process A/B).
-bool svc_xcd() {
-    const char* c = std::getenv("JSP_SVC_XCD");
-    return !(c && c[0] == '0');
-}
-
-// Resident tiles keep their rows in LDS between requests (JSP_SVC_ROW_CACHE=0:
-// reload every request; read at each service start, so an A/B can switch it
-// inside one process).
-bool svc_row_cache() {
-    const char* c = std::getenv("JSP_SVC_ROW_CACHE");
-    return !(c && c[0] == '0');
-}
-
-int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
+int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     auto& v = e->svc;
     if (!v.stream) HIP_TRY(hipStreamCreateWithFlags(&v.stream, hipStreamNonBlocking));
+    start_waker(e);  // created with the first service, never on a recovery's path
     const uint32_t nb = e->n_blocks;
     if (J > v.cap || !v.assign.p) {
         const uint32_t cap = std::max<uint32_t>(4096, J + J / 2);
@@ -991,11 +914,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
         v.cap = cap;
     }
     const int shape = svc_shape(e);
-    if (shape == 1 && (n_runs > v.cap_runs || !v.runs.p)) {
-        const uint32_t cr = std::max<uint32_t>(1024, n_runs + n_runs / 2);
-        HIP_TRY(v.runs.reserve((size_t)cr * 8));
-        v.cap_runs = cr;
-    }
+    if (shape == 0) return set_err(JSP_ESTATE, "no resident-service shape for this engine state");
     uint32_t n_tiles = nb;  // workgroups that answer (and write a done word), dispatcher excluded
     // The host-side layout (split slots, the host walk's tile table, the done
     // and stamp words) is rebuilt only when the geometry changes: every
@@ -1024,32 +943,21 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     }
     HIP_TRY(v.box.reserve(64));
     const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
-    // granules, then bell, counter, n_runs on lines of their own. Zeroed only
-    // when allocated or the geometry changes: granule tags and request
-    // numbers never repeat across starts, a stop in the bell carries its
-    // service's generation, and the fused counter stays a multiple of the
-    // tile count -- so a restart after an idle exit (the recovery's cold
-    // start) costs the launch alone. Every write the service stages from
-    // (uploads) was synchronous, and rows are fenced per request
-    // (patch_wait), so the launch need not wait for the engine's streams.
+    // granules, then the bell on a line of its own, then the XCC votes.
+    // Zeroed only when allocated or the geometry changes: granule tags and
+    // request numbers never repeat across starts and a stop in the bell
+    // carries its service's generation -- so a restart after an idle exit
+    // (the recovery's cold start) costs the launch alone. Every write the
+    // service stages from (uploads) was synchronous, and rows are fenced per
+    // request (patch_wait), so the launch need not wait for the engine's
+    // streams.
     const size_t xbytes = ((size_t)4 * (nb + 1) + 127) & ~size_t(127);  // XCC vote words (co-located service)
-    if (gpad + 3 * 128 + xbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
-    HIP_TRY(v.granules.reserve(gpad + 3 * 128 + xbytes));
+    if (gpad + 128 + xbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
+    HIP_TRY(v.granules.reserve(gpad + 128 + xbytes));
     const unsigned long long key = ((unsigned long long)nb << 8) | ((unsigned long long)n_tiles << 40) | (unsigned)shape;
     if (v.zero_key != key) {
-        HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 3 * 128, v.stream));
+        HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 128, v.stream));
         v.zero_key = key;
-    }
-    {
-        // the request line: in device memory written through the BAR
-        // (JSP_SVC_BAR=1, read at each start), else the pinned box
-        const char* b = std::getenv("JSP_SVC_BAR");
-        const bool want = b && b[0] == '1';
-        if (want && !v.bar && !v.bar_tried) {
-            v.bar_tried = true;
-            v.bar = bar_line(e->device);
-        }
-        v.req = want && v.bar ? static_cast<unsigned long long*>(v.bar) : v.box.as<unsigned long long>();
     }
     req_store(e, (unsigned long long)v.seq, (unsigned long long)v.seq);
     v.gen = v.gen % 0x7FFFFFFFu + 1u;
@@ -1057,28 +965,27 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     __atomic_store_n(ready, 0u, __ATOMIC_RELEASE);
     uint32_t* w = v.words.as<uint32_t>();
     jsp::ServiceArgs a{};
-    a.mailbox = v.req;
+    a.mailbox = v.box.as<unsigned long long>();
     a.granules = v.granules.as<unsigned long long>();
     a.bell = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad);
-    a.counter = reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128);
-    a.nruns = shape == 1 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 256) : nullptr;
-    a.xcc = reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 384);
+    a.xcc = reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 128);
     if (!v.pdesc.p) HIP_TRY(v.pdesc.reserve(sizeof(jsp::PatchDesc)));
     if (!e->h_patch_done.p) {
         HIP_TRY(e->h_patch_done.reserve(128));
         std::memset(e->h_patch_done.p, 0, 128);
     }
-    {
-        const size_t pb = jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, e->W, e->R).bytes;
-        if (pb > v.pstage.bytes) HIP_TRY(v.pstage.reserve(pb));  // not resident now: a free does not wait
-    }
+    // the inline staging was sized for this W/R at snapshot upload (the
+    // service was stopped then, and no patch was pending): never reallocated
+    // here, where a staged patch may be waiting in it
+    if (jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, e->W, e->R).bytes > v.pstage.bytes)
+        return set_err(JSP_ESTATE, "inline patch staging not sized for W=%u R=%u", e->W, e->R);
     a.pstage = v.pstage.as<const char>();
     a.pdesc = v.pdesc.as<jsp::PatchDesc>();
     a.pdone = e->h_patch_done.as<uint32_t>();
     a.taken = e->h_patch_done.as<uint32_t>() + 16;  // its own line
     // co-located compaction service: all its workgroups on one XCD when it
-    // fits one (32 CUs, one workgroup per CU); JSP_SVC_XCD=0 spreads it (A/B)
-    a.spread = shape == 2 && nb + 1 <= 32 && svc_xcd() ? 8u : 1u;
+    // fits one (32 CUs, one workgroup per CU)
+    a.spread = shape == 2 && nb + 1 <= 32 && e->hooks.svc_xcd ? 8u : 1u;
     a.pods = e->cls_h[0].pods;
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();
@@ -1091,10 +998,6 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     a.ready = ready;
     a.gen = v.gen;
     v.err_ack = __atomic_load_n(w + n_tiles + 2, __ATOMIC_ACQUIRE);  // an earlier instance's error is not ours
-    {
-        const char* c = std::getenv("JSP_SVC_EARLY");  // read per service start (in-process A/B)
-        v.early = !(c && c[0] == '0');
-    }
     v.nb = n_tiles;
     v.blocks = nb;
     v.clk = e->timing;
@@ -1106,37 +1009,25 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
     const jsp::TallyArgs ta0 = tally_args(e, nullptr, nullptr, e->L_total);
     size_t lds = 0;
     uint32_t grid = 0;
-    jsp::FusedArgs f{};
-    jsp::TallyArgs ta{};
     jsp::SplitArgs sp{};
+    // the tiles keep their rows on chip between requests when each is one
+    // chunk: the compaction tiles in registers (the resident path), the
+    // split tiles in LDS
+    const bool one_chunk = e->max_blk_span <= (uint32_t)jsp::kChunkRows;
     if (shape == 2) {
-        // the tiles keep their rows on chip between requests when each is one
-        // chunk: in registers (the resident path; JSP_SVC_RESIDENT=0: in LDS)
-        const bool one_chunk = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
-        a.resident = one_chunk && svc_resident() ? 1u : 0u;
-        const bool rc = one_chunk && !a.resident;
-        a.row_cache_words = rc ? jsp::service_row_cache_words(e->blk_leaves) : 0u;
-        lds = jsp::service_lds_bytes(e->blk_leaves, (int)e->W, (int)e->R, rc);
+        a.resident = one_chunk ? 1u : 0u;
+        a.row_cache_words = 0u;
+        lds = jsp::service_lds_bytes(e->blk_leaves, (int)e->W, (int)e->R, false);
         grid = nb + 1;
-    } else if (shape == 3) {
+    } else {
         sp.groups = v.groups;
         sp.cpg = v.cpg;
         sp.C = e->C;
         sp.out = v.split.as<uint64_t>();
         sp.topo = e->topo;
-        const bool rc = svc_row_cache() && e->max_blk_span <= (uint32_t)jsp::kChunkRows;
-        a.row_cache_words = rc ? jsp::split_row_cache_words(v.cpg, e->blk_leaves) : 0u;
-        lds = jsp::split_service_lds_bytes(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, rc);
+        a.row_cache_words = one_chunk ? jsp::split_row_cache_words(v.cpg, e->blk_leaves) : 0u;
+        lds = jsp::split_service_lds_bytes(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, one_chunk);
         grid = n_tiles + 1;
-    } else {
-        const size_t cl = (size_t)std::max<uint32_t>(e->C, 1) * std::max<uint32_t>(e->L_total, 1);
-        HIP_TRY(v.tally.reserve((cl + std::max<uint32_t>(e->L_total, 1)) * 4));
-        uint32_t* cap = v.tally.as<uint32_t>();
-        ta = tally_args(e, cap, cap + cl, e->L_total);
-        uint32_t* rc = v.runs.as<uint32_t>();
-        f = fused_args(e, ta, rc, rc + v.cap_runs, 0, 0, v.assign.as<int32_t>(), w + nb);
-        lds = f.lds_bytes;
-        grid = nb * f.groups + 1;
     }
     {
         // the API answer can be one workgroup per CU high at high SGPR counts
@@ -1156,8 +1047,7 @@ int svc_start(jsp_engine* e, uint32_t J, uint32_t n_runs, bool wait_ready) {
                                        "of LDS each", grid, e->n_cu, (long long)fit, lds);
     }
     if (shape == 2) HIP_TRY(jsp::launch_service(ta0, a, v.stream));
-    else if (shape == 3) HIP_TRY(jsp::launch_split_service(ta0, sp, a, v.stream));
-    else HIP_TRY(jsp::launch_fused_service(ta, f, a, v.stream));
+    else HIP_TRY(jsp::launch_split_service(ta0, sp, a, v.stream));
     v.running = true;
     v.pending_ready = true;
     v.t_launch = std::chrono::steady_clock::now();
@@ -1200,7 +1090,7 @@ int svc_wait_ready(jsp_engine* e) {
 int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     auto& v = e->svc;
     const uint32_t* words = v.words.as<uint32_t>();
-    const uint32_t n = v.shape == 1 ? 1u : v.nb;  // fused: the tail's one word
+    const uint32_t n = v.nb;
     const bool split = v.shape == 3;
     // compaction: tiles 0..i-1 have answered, so assign[] up to about i/n of
     // J is final (tiles own consecutive ranges of roughly equal size): start
@@ -1309,7 +1199,6 @@ uint32_t next_seq(uint32_t q) {
 // Post a request word (second half first: the dispatcher reads both in one
 // 16-byte load and takes a torn read for none).
 void svc_post(jsp_engine* e, uint32_t seq, uint32_t jw, uint32_t n_runs) {
-    auto& v = e->svc;
     req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)n_runs << 32) | seq);
 }
 
@@ -1343,15 +1232,25 @@ int patch_wait(jsp_engine* e) {
     }
     patch_post_deferred(e);
     const uint32_t* w = e->h_patch_done.as<uint32_t>();
+    const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::duration<double, std::milli>(2.0 * svc_idle_ms() + 100.0);
     for (uint64_t spins = 1; __atomic_load_n(w, __ATOMIC_ACQUIRE) != e->patch_seq; ++spins) {
         if ((spins & 255) == 0 && e->patch_svc) {
             // posted to the dispatcher: if the service left without taking it
-            // (an idle exit racing the post), apply it with the patch kernel
+            // (an idle exit racing the post), apply it with the patch kernel.
+            // A live service that never takes it (bounded: it polls every few
+            // microseconds) is stopped, and the patch kernel applies it too
+            // (the staged delta is unchanged: writing it twice writes the
+            // same values)
             const hipError_t q = hipStreamQuery(e->svc.stream);
-            if (q == hipErrorNotReady) continue;
+            if (q == hipErrorNotReady && std::chrono::steady_clock::now() - t0 < limit) continue;
             if (__atomic_load_n(w, __ATOMIC_ACQUIRE) == e->patch_seq) break;
-            e->svc.running = false;
             e->patch_svc = false;
+            if (q == hipErrorNotReady) {
+                e->svc.pending = 0;
+                if (int rc = svc_stop(e)) return rc;  // patch_svc is off: the stop does not wait for it
+            }
+            e->svc.running = false;
             if (int rc = use_engine_stream(e)) return rc;
             e->patch_target += (e->last_patch.n + 255) / 256;
             e->last_patch.target = e->patch_target;
@@ -1376,20 +1275,12 @@ int patch_wait(jsp_engine* e) {
 // not after a patch the service applies: they wait for its word first.
 int patch_fence(jsp_engine* e) { return e->patch_pending && e->patch_svc ? patch_wait(e) : JSP_OK; }
 
-// How patches reach the resident service's dispatcher. 2 (default): posted
-// at once, so the dispatcher applies them during the gap before the next
-// request (a recovery's deletions take milliseconds), and a request posted
-// before the patch's completion word came back carries it again (applying a
-// staged patch twice writes the same values; the request may have replaced
-// the patch's own in the mailbox). 1: held back and carried by the next
-// request only. 0: always the patch kernel. JSP_SVC_PATCH, read per call
-// (in-process A/B).
-int svc_patch_mode() {
-    const char* v = std::getenv("JSP_SVC_PATCH");
-    return v && v[0] == '0' ? 0 : v && v[0] == '1' ? 1 : 2;
-}
-bool svc_patch_on() { return svc_patch_mode() != 0; }
-
+// How patches reach the resident service's dispatcher: posted at once, so the
+// dispatcher applies them during the gap before the next request (a
+// recovery's deletions take milliseconds), and a request posted before the
+// patch's completion word came back carries it again (applying a staged
+// patch twice writes the same values; the request may have replaced the
+// patch's own in the mailbox).
 
 // A snapshot patch is the first sign of a recovery: the watch events of the
 // deleted Jobs' pods arrive while the reconciler deletes them in the
@@ -1398,13 +1289,11 @@ bool svc_patch_on() { return svc_patch_mode() != 0; }
 // has been answered by the resident service (armed), a patch (re)starts it
 // here without waiting: the GPU wakes from idle and the grid comes up while
 // the deletions finish, and the recreate's jsp_place finds it polling.
-// JSP_SVC_WAKE=0 turns this off (A/B).
 // Whether a patch should (re)start the service: the host API has been
 // answered by it and it is not up (or about to idle out).
 bool svc_wake_wanted(jsp_engine* e) {
-    static const bool on = [] { const char* v = std::getenv("JSP_SVC_WAKE"); return !(v && v[0] == '0'); }();
     auto& v = e->svc;
-    if (!on || !v.armed || !svc_ok(e)) return false;
+    if (!v.armed || !svc_ok(e)) return false;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
     return !(v.running && since <= 0.5 * svc_idle_ms());
 }
@@ -1422,7 +1311,7 @@ int svc_restart_quiet(jsp_engine* e) {
         v.pending = 0;
         e->grave.flush();
     }
-    if (svc_stop(e) != JSP_OK || svc_start(e, 0, 0, false) != JSP_OK) {
+    if (svc_stop(e) != JSP_OK || svc_start(e, 0, false) != JSP_OK) {
         (void)svc_stop(e);
         g_err.clear();
         return JSP_EHIP;
@@ -1439,17 +1328,14 @@ void svc_wake(jsp_engine* e) {
     // instruction caches while the deletions finish, so the recreate's
     // request runs warm. Posted without waiting (the dispatcher finds it when
     // it starts polling); the next request settles it first (svc_settle).
-    if (v.shape == 2 || v.shape == 3) {
-        const uint32_t seq = next_seq(v.seq);
-        v.seq = seq;
-        v.last = std::chrono::steady_clock::now();
-        req_store(e, (0x80000000ull << 32) | seq, (unsigned long long)seq);
-        // rows marked patched, and they stay marked: the patch kernel may not
-        // have landed when the warm-up loads them, so the next request (which
-        // waits for the patch's completion word) loads them again
-
-        v.pending = seq;
-    }
+    const uint32_t seq = next_seq(v.seq);
+    v.seq = seq;
+    v.last = std::chrono::steady_clock::now();
+    req_store(e, (0x80000000ull << 32) | seq, (unsigned long long)seq);
+    // rows marked patched, and they stay marked: the patch kernel may not
+    // have landed when the warm-up loads them, so the next request (which
+    // waits for the patch's completion word) loads them again
+    v.pending = seq;
 }
 
 // The waker's job (or the next caller's, whichever takes the engine lock
@@ -1469,21 +1355,12 @@ void run_wake(jsp_engine* e) {
     const uint32_t seq = next_seq(v.seq);
     v.seq = seq;
     v.last = std::chrono::steady_clock::now();
-    const bool warm = v.shape == 2 || v.shape == 3;
-    const bool inl = (e->patch_bits & jsp::kReqPatchInline) != 0;
-    if (inl && v.shape == 1) {  // staged inline for a tile shape; the fused shape's n_runs word is taken
-        e->patch_bits &= ~jsp::kReqPatchInline;
-        const jsp::PatchArgs& a = e->last_patch;
-        *v.pdesc.as<jsp::PatchDesc>() = jsp::PatchDesc{a.rows, a.dlab, a.dtaint, a.dfree, a.dexcl, a.n, a.seq};
-    }
-    svc_post(e, seq, e->patch_bits | (warm ? jsp::kReqDirty : jsp::kReqPatchOnly),
+    svc_post(e, seq, e->patch_bits | jsp::kReqDirty,
              (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : 0u);
     e->patch_req = seq;
     e->patch_deferred = false;
-    if (warm) {
-        v.pending = seq;
-        v.rows_dirty = false;  // the warm-up loads the patched rows
-    }
+    v.pending = seq;
+    v.rows_dirty = false;  // the warm-up loads the patched rows
     e->acc.wake_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -1501,17 +1378,22 @@ void waker_main(jsp_engine* e) {
     }
 }
 
-// Hand the wake to the waker thread (started on first use; JSP_SVC_WAKER=0:
-// the caller runs it inline, A/B). Called with mu held.
-void ring_waker(jsp_engine* e) {
-    const char* w = std::getenv("JSP_SVC_WAKER");  // read per call (in-process A/B)
-    const bool on = !(w && w[0] == '0');
-    e->wake_job = true;
-    if (!on) {
-        run_wake(e);
-        return;
-    }
+// The waker thread, created with the engine's first service (thread creation
+// costs ~100 us, which must never land in a recovery's patch call).
+void start_waker(jsp_engine* e) {
     if (!e->waker.joinable()) e->waker = std::thread(waker_main, e);
+}
+
+// Hand the wake to the waker thread. Called with mu held. (Diagnostic A/B
+// build tools/bin/ab_inlinewake, -DJSP_AB_INLINE_WAKE: the patch call runs the
+// wake itself; never the product library.)
+void ring_waker(jsp_engine* e) {
+    e->wake_job = true;
+#ifdef JSP_AB_INLINE_WAKE
+    run_wake(e);
+    return;
+#endif
+    start_waker(e);
     {
         std::lock_guard<std::mutex> l(e->wake_mu);
         e->wake_ring = true;
@@ -1523,11 +1405,11 @@ void ring_waker(jsp_engine* e) {
 int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
               int32_t* assign_out, uint32_t* placed) {
     auto& v = e->svc;
+    const auto t_in = std::chrono::steady_clock::now();
     run_wake(e);  // a recovery's wake the waker has not run yet: run it here
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
-                   (shape == 1 && n_runs > v.cap_runs) ||
                    std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
     // the request's tiles must read the patched rows: a patch held back for
     // the running service rides on this request (its dispatcher applies it
@@ -1536,22 +1418,14 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (!carry)
         if (int rc = patch_wait(e)) return rc;
     // A cold start -- the first request after an idle exit (recoveries are
-    // hours apart), an upload or a geometry change -- launches the service,
-    // waits for its dispatcher to poll and posts to it. Measured after 60 ms
-    // idle on MI355X (profiles/r03, tools/ab_probe.py svc): cfg2 p50 33 us,
-    // max 67 us this way, against 66 / 428 us when the launch path answers the
-    // cold call while the service comes up (JSP_COLD_LAUNCH=1, A/B) -- the
-    // polling dispatcher brings the GPU out of its idle state while the host
-    // waits, and a launch after idling pays that wake-up inside the kernel.
-    static const bool cold_launch = [] { const char* v = std::getenv("JSP_COLD_LAUNCH"); return v && v[0] == '1'; }();
-    // The new service is launched once this call's answer is back
-    // (jsp_place): launched before, its co-resident grid can hold the CUs the
-    // launch path's workgroups need until it idle-exits (a 50 ms stall seen
-    // as the cold-recovery maximum, profiles/r03).
-    if (restart && cold_launch) {
-        if (int rc = svc_stop(e)) return rc;
-        return kSvcUseLaunch;
-    }
+    // hours apart, and a recovery's first patch has normally restarted it
+    // already), an upload or a geometry change -- launches the service, waits
+    // for its dispatcher to poll and posts to it. Measured after 60 ms idle on
+    // MI355X (profiles/r03): cfg2 p50 33 us, max 67 us this way, against 66 /
+    // 428 us when the launch path answered the cold call while the service
+    // came up -- the polling dispatcher brings the GPU out of its idle state
+    // while the host waits, and a launch after idling pays that wake-up inside
+    // the kernel.
     if (!restart) {
         if (int rc = svc_wait_ready(e)) return rc;
         if (int rc = svc_settle(e)) return rc;
@@ -1566,31 +1440,30 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     }
     // the compaction answer is read from its tagged entries (timing on: the
     // done words, which carry the per-tile stamps)
-    const bool early = shape == 2 && J > 0 && !e->timing && v.early;
+    const bool early = shape == 2 && J > 0 && !e->timing;
     uint32_t seq = 0, n_early = 0;
+    std::chrono::steady_clock::time_point t_post{};
     for (int attempt = 0;; ++attempt) {
         if (restart) {
             if (int rc = svc_stop(e)) return rc;
-            if (int rc = svc_start(e, J, n_runs, true)) return rc;
-        }
-        if (shape == 1 && n_runs > 0) {  // the tail reads the runs from pinned memory
-            std::memcpy(v.runs.as<uint32_t>(), run_class, (size_t)n_runs * 4);
-            std::memcpy(v.runs.as<uint32_t>() + v.cap_runs, run_len, (size_t)n_runs * 4);
+            if (int rc = svc_start(e, J, true)) return rc;
         }
         seq = next_seq(v.seq);
         v.seq = seq;
         v.last = std::chrono::steady_clock::now();
         // second half first: the dispatcher reads both halves in one 16-byte
         // load (an inline patch carried here: its n | flags in place of n_runs,
-        // which only the fused shape reads and which never carries one inline)
+        // which the tiles do not read)
         const uint32_t w2 = carry && (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : n_runs;
-
-        // the compaction and split tiles keep their rows in LDS: bit 31 of J tells
-        // them the snapshot was patched since their previous request (J < 2^30)
-        const uint32_t jw = J | ((shape == 2 || shape == 3) && v.rows_dirty ? jsp::kReqDirty : 0u) |
-                            (carry ? e->patch_bits : 0u);
+        // the tiles keep their rows on chip: bit 31 of J tells them the
+        // snapshot was patched since their previous request (J < 2^28)
+        const uint32_t jw = J | (v.rows_dirty ? jsp::kReqDirty : 0u) | (carry ? e->patch_bits : 0u);
         carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
         v.rows_dirty = false;
+        if (attempt == 0) {
+            t_post = std::chrono::steady_clock::now();
+            e->acc.svc_pre_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
+        }
         req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)w2 << 32) | seq);
         const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
         if (rc == kSvcFailed) {
@@ -1608,7 +1481,8 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         if (rc) return rc;
         break;
     }
-    if (v.clk && (v.shape == 2 || v.shape == 3) && v.nb > 0) {
+    e->acc.svc_answer_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_post).count();
+    if (v.clk && v.nb > 0) {
         // the request's device time: first tile saw it -> last tile drained
         const uint32_t* clk = v.words.as<uint32_t>() + v.nb + 3;
         const uint32_t ref = clk[0];
@@ -1642,11 +1516,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
                                  "its assign[] is invalid", seq);
     }
     const auto tc = std::chrono::steady_clock::now();
-    if (v.shape == 2) {  // u64 entries: the domain is the low half
+    {  // u64 entries: the domain is the low half
         const unsigned long long* a = v.assign.as<unsigned long long>();
         for (uint32_t j = 0; j < J; ++j) assign_out[j] = (int32_t)(uint32_t)a[j];
-    } else if (J > 0) {
-        std::memcpy(assign_out, v.assign.p, (size_t)J * 4);
     }
     *placed = __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
     // the copy-out's share of the wait (jsp_timing.host_post_us on this path)
@@ -1772,7 +1644,7 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         delete e;
         return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
     }
-    if (hipEventCreateWithFlags(&e->ev_last, ev_last_flags()) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
         delete e;
         return set_err(JSP_EHIP, "hipEventCreate failed");
     }
@@ -1785,16 +1657,13 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         return set_err(JSP_ENOMEM, "error word");
     }
     std::memset(e->h_err.p, 0, 64);
-    if (const char* v = std::getenv("JSP_SERVICE"))
-        e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : std::strcmp(v, "2") == 0 ? JSP_SERVICE_DEVICE_WALK
-                                                                                           : JSP_SERVICE_AUTO;
-    if (const char* v = std::getenv("JSP_TALLY_ONE")) e->tally_one = v[0] != '0';
-    if (const char* v = std::getenv("JSP_ASSIGN_RECORDS")) e->assign_records = v[0] != '0';
-    if (const char* v = std::getenv("JSP_EXPAND_RPW")) e->expand_rpw = (uint32_t)std::clamp(std::atol(v), 1L, 64L);
-    // test hook: CUs the service may count on (stands in for a smaller GPU or a partition)
-    if (const char* v = std::getenv("JSP_SVC_CU_LIMIT")) e->n_cu = std::min<int>(e->n_cu, (int)std::strtol(v, nullptr, 10));
-    // test hook: the service's first request number (tests start it next to 2^30)
-    if (const char* v = std::getenv("JSP_SVC_SEQ0")) e->svc.seq = (uint32_t)std::strtoul(v, nullptr, 0);
+    // operational: JSP_SERVICE=0 keeps the resident service off
+    if (const char* v = std::getenv("JSP_SERVICE")) e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : JSP_SERVICE_AUTO;
+    e->hooks = read_hooks();
+    // test hooks: CUs the service may count on (stands in for a smaller GPU
+    // or a partition), the service's first request number (next to 2^30)
+    if (e->hooks.cu_limit > 0) e->n_cu = std::min<int>(e->n_cu, e->hooks.cu_limit);
+    if (e->hooks.have_seq0) e->svc.seq = e->hooks.seq0;
     *out = e;
     return JSP_OK;
 }
@@ -1950,15 +1819,12 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
         if (ls[l] > ls[l + 1]) return set_err(JSP_EINVAL, "leaf_start not monotone at %u", l);
         max_rows = std::max(max_rows, ls[l + 1] - ls[l]);
     }
-    // workgroup partition: whole leaves, <= 256 leaves each, block_chunks()
-    // 1024-row chunks each (a workgroup with several prefetches its next
-    // chunk's rows while it evaluates one)
-    const uint32_t chunks = block_chunks(N);
+    // workgroup partition: whole leaves, <= 256 leaves each, one 1024-row
+    // chunk each (test hooks: more chunks, or smaller row blocks)
+    e->hooks = read_hooks();
+    const uint32_t chunks = e->hooks.block_chunks;
     uint32_t target_rows = chunks * (uint32_t)jsp::kChunkRows - 4;  // fits even when unaligned
-    if (const char* v = std::getenv("JSP_BLOCK_ROWS")) {  // smaller row blocks (A/B of the tile count)
-        const long x = std::strtol(v, nullptr, 10);
-        if (x >= 60 && x < (long)target_rows) target_rows = (uint32_t)x;
-    }
+    if (e->hooks.block_rows >= 60 && e->hooks.block_rows < target_rows) target_rows = e->hooks.block_rows;
     std::vector<uint32_t> blk{0};
     {
         uint32_t rows = 0, leaves = 0;
@@ -2032,6 +1898,10 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     HIP_TRY(e->granules.reserve(8 * blk.size()));
     HIP_TRY(hipMemsetAsync(e->granules.p, 0, 8 * blk.size(), s));  // look-back granules (epoch 0 never matches)
     HIP_TRY(e->h_done.reserve(4 * blk.size()));
+    // the service's inline patch staging, sized for this W/R now: the service
+    // is stopped and no patch is pending (svc_suspend), so nothing staged can
+    // be lost, and svc_start never reallocates it under a staged patch
+    HIP_TRY(e->svc.pstage.reserve(jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, W, R).bytes));
     HIP_TRY(hipStreamSynchronize(s));
     std::memset(e->h_done.p, 0, 4 * blk.size());  // completion words (epoch 0 never matches)
     e->N = N;
@@ -2049,8 +1919,7 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
         e->blk_leaves = (most + 3) & ~3u;
     }
     e->tile_draws = e->done_draws = 0;
-    e->spin_limit = 1u << 22;
-    if (const char* v = std::getenv("JSP_LOOKBACK_SPINS")) e->spin_limit = (uint32_t)std::strtoul(v, nullptr, 10);
+    e->spin_limit = e->hooks.lookback_spins;
     e->have_snap = true;
     if (e->have_cls) {
         for (auto& c : e->cls_h)
@@ -2080,28 +1949,26 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     auto& v = e->svc;
-    // Who applies it: the running service's dispatcher (held back for the next
-    // request, which carries it -- no host-link round trip of its own; whatever
-    // else reads the rows first posts it alone and waits, patch_wait); after
-    // the service left, a recovery's first patch restarts it at once (its grid
-    // comes up while the delta is staged) and the dispatcher applies it
-    // followed by a warm-up request; otherwise the patch kernel.
+    // Who applies it: the running service's dispatcher (posted at once; a
+    // request that finds it not yet taken carries it again; whatever else
+    // reads the rows first waits for it, patch_wait); after the service left,
+    // a recovery's first patch restarts it (the waker thread: its grid comes
+    // up while the deletions finish) and the dispatcher applies it followed by
+    // a warm-up request; otherwise the patch kernel.
     const auto t1 = std::chrono::steady_clock::now();
     const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
-    const int pmode = svc_patch_mode();
-    const bool up = pmode != 0 && v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
-    // a wake stages for the tile shapes' inline buffer once a service has run
-    // (run_wake moves it to the descriptor if the fused shape starts instead)
-    const bool wake = !up && pmode != 0 && svc_wake_wanted(e);
+    const bool up = v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    const bool wake = !up && svc_wake_wanted(e);
     // The delta into pinned staging, read in place. Patches for the service
     // of up to kPatchInlineRows rows go to its fixed inline buffer (layout
-    // from n and the column flags, which ride in the request); larger ones,
-    // and the patch kernel's, to the engine's staging through a descriptor.
+    // from n and the column flags, which ride in the request; sized for this
+    // W/R at snapshot upload); larger ones, and the patch kernel's, to the
+    // engine's staging through a descriptor.
     const uint32_t W = e->W, R = e->R;
     const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
                         (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
     const bool inl = (up || wake) && n <= jsp::kPatchInlineRows && v.pstage.p &&
-                     jsp::patch_inline_layout(n, 15u, W, R).bytes <= v.pstage.bytes && (wake || v.shape != 1);
+                     jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, W, R).bytes <= v.pstage.bytes;
     const jsp::PatchInlineLayout L = jsp::patch_inline_layout(n, inl ? fl : 15u, W, R);
     char* hp;
     size_t base = 0;
@@ -2158,7 +2025,7 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     // the stream for the patch kernel.
     if (up) {
         e->patch_deferred = true;
-        if (pmode == 2) patch_post_deferred(e);  // posted now (svc_patch_mode)
+        patch_post_deferred(e);  // posted now: it lands during the gap before the next request
     } else if (wake) {
         // held back; the waker restarts the service and posts it (run_wake)
         e->patch_deferred = true;
@@ -2331,15 +2198,10 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
     const bool want_tally = (tally_out && e->C > 0) || occ_out;
-    bool svc_after = false;  // a cold start: the service is launched after the launch path answers
     if (!want_tally && J < jsp::kReqPatchInline && svc_ok(e)) {  // J and the request bits share a word
         const auto t1 = std::chrono::steady_clock::now();
         uint32_t placed = 0;
         const int src = svc_place(e, run_class, run_len, n_runs, J, assign_out, &placed);
-        if (src == kSvcUseLaunch) {
-            svc_after = true;
-            goto launch_path;
-        }
         if (src != JSP_OK) {
             // the service could not answer: stop it and answer this call on the
             // launch path. A geometry failure (its grid cannot be co-resident,
@@ -2356,7 +2218,7 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         {
         const auto t2 = std::chrono::steady_clock::now();
         e->svc.armed = true;
-        e->last_shape = e->svc.shape == 1 ? 4 : e->svc.shape == 3 ? 5 : 3;
+        e->last_shape = e->svc.shape == 3 ? 5 : 3;
         if (stats) {
             stats->jobs = J;
             stats->runs = n_runs;
@@ -2425,18 +2287,6 @@ launch_path:
     e->acc.host_launch_us += us(t2 - t1).count();
     e->acc.host_wait_us += us(t3 - t2).count();
     e->acc.host_post_us += us(t4 - t3).count();
-    if (svc_after) {
-        const int sr = svc_start(e, J, n_runs, false);
-        if (sr != JSP_OK) {
-            // cannot start here: not co-resident on this GPU (the launch path
-            // answers until the next upload) or a transient failure (the next
-            // call tries again); this call's answer stands either way
-            (void)svc_stop(e);
-            if (sr == JSP_ERANGE) e->svc.broken = true;
-            e->acc.svc_fallbacks += 1;
-            g_err.clear();
-        }
-    }
     return JSP_OK;
 }
 
@@ -2532,7 +2382,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 1, mode); }
     std::lock_guard<std::mutex> g(e->mu);
-    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO && mode != JSP_SERVICE_DEVICE_WALK)
+    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO)
         return set_err(JSP_EINVAL, "service mode %d", mode);
     if (mode != e->svc_mode) {  // the running service's shape may change
         e->svc.resume = false;

@@ -87,6 +87,20 @@ struct TallyArgs {
 // workgroups that started first instead of waiting for the last XCD.
 constexpr uint32_t kSpareBlocks = 64;
 
+// Bounded waits inside a launch (the pipelined batch walk's polls of an
+// earlier batch, the level walk's expanders' wait for the walker): a wait
+// that gives up writes `tag` to the engine's host-mapped error word, which the
+// host reports as JSP_EHIP (jsp_engine.cc check_launch_error) -- never a stale
+// assign[] with success. The tag's top two bits say which wait (kErr*); the
+// compaction's look-back writes its launch number (kind 0).
+constexpr uint32_t kErrLookback = 0u, kErrExpand = 1u << 30, kErrPipe = 2u << 30, kErrKindMask = 3u << 30;
+struct WaitErr {
+    uint32_t* err;         // host-mapped error word (null: no report)
+    uint32_t tag;          // written there by a wait that gave up
+    uint32_t pipe_spins;   // polls of the pipelined batch walk before it gives up
+    uint64_t wait_ticks;   // 100 MHz ticks the level walk's expanders wait for the walker
+};
+
 // Tail of place_fused_kernel (the last tally workgroup runs the assignment).
 struct FusedArgs {
     unsigned long long* ticket;  // [0] tile ticket, [1] finished-tile count; zeroed at snapshot upload
@@ -112,9 +126,8 @@ struct FusedArgs {
     uint32_t epoch;              // value written to *done when the tail has finished
     uint32_t groups;             // class groups: tile t tallies row block t / groups, classes of group t % groups
     uint32_t cpg;                // classes per group (group 0 also counts occupancy)
-    uint32_t pipe;               // pipelined batch walk allowed
+    WaitErr we;                  // the pipelined batch walk's bounded wait
 };
-bool pipe_walk_enabled();
 
 // A fused tile's share: row block and class range.
 struct FusedTile {
@@ -210,9 +223,7 @@ struct ServiceArgs {
     unsigned long long idle_ticks;      // 100 MHz ticks without a request before a workgroup leaves
     uint32_t* ready;                    // host-mapped: the dispatcher writes gen once it polls
     uint32_t gen;                       // service launch number
-    uint32_t* nruns;                    // device word: the request's run count (fused shape), or null
-    unsigned long long* counter;        // device: finished tiles over all requests (fused shape)
-    uint32_t row_cache_words;           // compaction shape: LDS word offset of the tiles' row copy, 0 = none
+    uint32_t row_cache_words;           // split shape: LDS word offset of the tiles' row copy, 0 = none
     // XCD co-location (compaction shape): the grid is spread x (tiles + 1)
     // workgroups and only those with blockIdx % spread == 0 stay -- one XCD
     // under the round-robin dealing of workgroups to XCDs. Each survivor
@@ -308,14 +319,13 @@ hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t 
 // rows kept between requests, from word service_row_cache_words(la) on
 uint32_t service_row_cache_words(uint32_t la);
 size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache);
-hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s);
 size_t compact_lds_bytes(uint32_t la);
 hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);
 size_t split_lds_bytes(uint32_t cpg, uint32_t la);
 // the split service's LDS: split_lds_bytes, then (row_cache) the tile's rows
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la);
 size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache);
-// Workgroups of the resident service kernel (shape 2 compaction, 1 fused, 3 split) of
+// Workgroups of the resident service kernel (shape 2 compaction, 3 split) of
 // this W/R that one CU holds at once with lds_bytes each (occupancy API).
 hipError_t service_occupancy(const TallyArgs& a, int shape, size_t lds_bytes, int* blocks_per_cu);
 size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint32_t nv, uint32_t la,
@@ -331,7 +341,7 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                         uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s);
+                         uint32_t* rec_count, AssignRec* recs, hipStream_t s, const WaitErr& we);
 // The level walker (assign_level_kernel): every class at one topology level
 // of nw <= kLevelMaxWords words and at most kLevelMaxRuns runs. 256 threads
 // hold the taken bits of their words in registers and walk the runs in
@@ -342,13 +352,14 @@ hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const D
 constexpr uint32_t kLevelMaxWords = 256 * 8;
 constexpr uint32_t kLevelMaxRuns = 32;
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
-// ready (device u64, or null: a second launch expands): the walker publishes
-// (epoch << 32 | 1 << 31 | record count) there once its records are written,
-// and the launch's other workgroups expand them (epoch: new per launch, != 0).
+// ready (device u64): the walker publishes (epoch << 32 | 1 << 31 | record
+// count) there once its records are written, and the launch's other
+// workgroups expand them (epoch: new per launch, != 0); an expander that
+// waits longer than we.wait_ticks writes we.tag to the error word.
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s,
-                               unsigned long long* ready = nullptr, uint32_t epoch = 0);
+                               uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
+                               uint32_t epoch, const WaitErr& we);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

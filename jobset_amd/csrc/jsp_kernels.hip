@@ -1507,7 +1507,6 @@ constexpr uint32_t kChainUnrollMin = 6;
 #define JSP_PIPE_WAVES 4
 #endif
 constexpr uint32_t kPipeWaves = JSP_PIPE_WAVES;    // waves of the pipelined batch walk
-constexpr uint32_t kPipeSpinLimit = 1u << 24;      // bounded wait on an earlier batch's progress  // visiting jobs from which a word takes the unrolled chain
 
 // One word of a batch (wave-wide): lane c holds class c's free feasible bits
 // `g` of word w; the batch's jobs still without a domain (R; lane j = job j of
@@ -1612,13 +1611,16 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                              uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats,
                              uint64_t* s_taken, const AssignMeta& m, const uint32_t* s_topo, uint64_t* s_win,
                              uint32_t* s_stage, uint32_t stage_cap, AssignRec* __restrict__ recs,
-                             uint32_t* __restrict__ rec_count, uint32_t pipe_allowed, uint32_t len0 = ~0u,
+                             uint32_t* __restrict__ rec_count, const WaitErr& wait, uint32_t len0 = ~0u,
                              uint32_t rc0 = 0u) {
     // len0 != ~0u: the caller loaded the first tile's run (thread tid's) already
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t K = topo.K;
     // the pipelined walk keeps its batch table and progress words in the stage
-    const bool pipe_ok = pipe_allowed != 0 && NT >= 64 * (int)kPipeWaves && stage_cap >= 4u * NT + 2u * kPipeWaves + 8u;
+    const bool pipe_ok = NT >= 64 * (int)kPipeWaves && stage_cap >= 4u * NT + 2u * kPipeWaves + 8u;
+    // a pipelined wait that gave up (wait.pipe_spins polls): the launch
+    // reports it through wait.err at the end instead of a stale assign[]
+    bool pipe_fail = false;
     // wave 0: class state in registers, lane c = class c (C <= kMaxClasses = 64)
     uint32_t my_cur = 0, my_lvl = 0, my_woff = 0, my_D = 0, my_toff = 0;
     if (wid == 0 && (uint32_t)lane < C) {
@@ -1721,7 +1723,8 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 }
                 if (lane == 0) {
                     m.s_misc[0] = nbat;
-                    *s_pcnt = 0;
+                    s_pcnt[0] = 0;
+                    s_pcnt[1] = 0;  // timed-out flag
                 }
                 if (lane < (int)kPipeWaves) s_prog[lane] = 0ull;
             }
@@ -1785,7 +1788,10 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                             const uint32_t pb = (uint32_t)(x >> 32), pr = (uint32_t)x;
                             known[k - 1] = pb > a ? 0xFFFFFFFFu : pb == a ? pr : 0u;
                             if (known[k - 1] > w) break;
-                            if (spins > kPipeSpinLimit) break;  // never waits forever (a bug shows as a parity failure)
+                            if (spins >= wait.pipe_spins) {  // never waits forever: reported, never silent
+                                __hip_atomic_store(s_pcnt + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                                break;
+                            }
                             __builtin_amdgcn_s_sleep(1);
                         }
                     }
@@ -1828,7 +1834,10 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
                 rs.T = Tn;
                 if ((uint32_t)lane < C) my_cur = m.s_cursor[lane];
             }
-            if (tid == 0) placed += *s_pcnt;
+            if (tid == 0) {
+                placed += s_pcnt[0];
+                pipe_fail |= s_pcnt[1] != 0u;
+            }
         } else if (wid == 0 && regmode) {
             // Short runs are taken in batches: up to 64 consecutive jobs (lane = job)
             // of short runs at one level. Within a batch the lowest-index greedy
@@ -2054,6 +2063,8 @@ __device__ __forceinline__ void assign_block(const uint64_t* __restrict__ feas, 
         stats[0] = n_runs;
         stats[1] = placed;
     }
+    if (tid == 0 && pipe_fail && wait.err != nullptr)
+        __hip_atomic_store(wait.err, wait.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     if (tid == 0 && rec_count != nullptr) *rec_count = m.s_misc[1];  // records for expand_kernel
     JSP_STAMP(4000u, 7);
 }
@@ -2065,7 +2076,7 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     uint32_t C, TopoDev topo, const uint32_t* __restrict__ run_class, const uint32_t* __restrict__ run_len,
     uint32_t n_runs, uint32_t J, int32_t* __restrict__ assign, uint32_t* __restrict__ stats, uint32_t feas_words,
     uint32_t feas_in_lds, uint32_t topo_in_lds, uint32_t topo_words, uint32_t stage_cap, AssignRec* __restrict__ recs,
-    uint32_t* __restrict__ rec_count, uint32_t pipe) {
+    uint32_t* __restrict__ rec_count, WaitErr wait) {
     extern __shared__ __attribute__((aligned(16))) uint64_t s_dyn[];
     const uint32_t tw = taken_words(topo);
     uint64_t* s_win = s_dyn + tw;
@@ -2103,11 +2114,15 @@ __global__ __launch_bounds__(kAssignThreads) void assign_kernel(
     const uint64_t* F = feas_in_lds ? s_feas : feas;
     if (topo_in_lds)
         assign_block<kAssignThreads, true>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m, s_topo,
-                                           s_win, s_stage, stage_cap, recs, rec_count, pipe, len0, rc0);
+                                           s_win, s_stage, stage_cap, recs, rec_count, wait, len0, rc0);
     else
         assign_block<kAssignThreads, false>(F, C, topo, run_class, run_len, n_runs, J, assign, stats, s_dyn, m,
-                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count, pipe, len0, rc0);
+                                            s_topo, s_win, s_stage, stage_cap, recs, rec_count, wait, len0, rc0);
 }
+
+// Records per expanding wave: 1, 4 and 16 are equal within noise on cfg4, 64
+// is slower.
+constexpr uint32_t kExpandRpw = 16;
 
 // Expansion of assign_kernel's records: a wave owns rpw (<= 64) consecutive
 // records of the host's bound (records <= min(J, feas_words + runs)); lane i
@@ -2137,13 +2152,14 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
     }
 }
 
-constexpr uint32_t kLevelEarly = 1u << 30;  // rpw flag: publish the record count after every run
 // The expanders of the one-launch level walk: wave g owns records
 // [g rpw, g rpw + rpw). It waits (bounded) for the walker's published count
 // of this launch (epoch-tagged), reads its records write-through and writes
-// their jobs' domains as expand_kernel does.
+// their jobs' domains as expand_kernel does. A wave that gives up (the
+// walker, dispatched first, never published within wait.wait_ticks) writes
+// the launch's tag to the error word: the call fails, never a stale assign[].
 __device__ void level_expand(const AssignRec* recs, const unsigned long long* ready, uint32_t epoch, uint32_t bound,
-                             uint32_t rpw, int32_t* assign) {
+                             uint32_t rpw, int32_t* assign, const WaitErr& wait) {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t r0 = ((blockIdx.x - 1) * (blockDim.x >> 6) + (threadIdx.x >> 6)) * rpw;
     if (r0 >= bound) return;  // wave-uniform
@@ -2151,13 +2167,15 @@ __device__ void level_expand(const AssignRec* recs, const unsigned long long* re
     uint32_t n = 0;
     while (true) {
         const unsigned long long x = __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // the final count (done bit), or a partial one (early expansion) that
-        // already covers this wave's records
-        if ((uint32_t)(x >> 32) == epoch && ((x & 0x80000000ull) || ((uint32_t)x & 0x7FFFFFFFu) >= r0 + rpw)) {
+        if ((uint32_t)(x >> 32) == epoch && (x & 0x80000000ull)) {  // this launch's final count
             n = (uint32_t)x & 0x7FFFFFFFu;
             break;
         }
-        if (wall_clock64() - t0 > 100000000ull) return;  // 1 s: the walker never published (its error shows in stats)
+        if (wall_clock64() - t0 >= wait.wait_ticks) {
+            if (lane == 0 && wait.err != nullptr)
+                __hip_atomic_store(wait.err, wait.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
         __builtin_amdgcn_s_sleep(2);
     }
     if (r0 >= n) return;
@@ -2206,15 +2224,14 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
                                                                      uint32_t* __restrict__ rec_count,
                                                                      AssignRec* __restrict__ recs,
                                                                      unsigned long long* __restrict__ ready,
-                                                                     uint32_t epoch, uint32_t bound, uint32_t rpw) {
+                                                                     uint32_t epoch, uint32_t bound, uint32_t rpw,
+                                                                     WaitErr wait) {
     // Expansion in the same launch (ready != null): workgroups 1.. wait for
     // the walker (workgroup 0, dispatched first, never waits for them) to
     // publish its record count, then expand the records as expand_kernel
     // does -- no second launch and no launch gap between walk and expansion.
-    const bool early = ready != nullptr && (rpw & kLevelEarly) != 0u;
-    rpw &= ~kLevelEarly;
     if (ready != nullptr && blockIdx.x > 0) {
-        level_expand(recs, ready, epoch, bound, rpw, assign);
+        level_expand(recs, ready, epoch, bound, rpw, assign, wait);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][NT]
@@ -2272,12 +2289,6 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
         const uint32_t used = total_free < n ? total_free : n;
         if (r < 4) JSP_STAMP(4051u, r);  // diagnostic: this run's scan is done
         const uint32_t rec_base = s_base[r & 1u];  // published by run r - 1 before this scan's barrier
-        // early expansion (rpw & kLevelEarly): the records of runs < r are out
-        // (every thread waited for its stores before this scan's barrier), so
-        // the expanders may start on them while this run is walked
-        if (early && r > 0 && tid == 0)
-            __hip_atomic_store(ready, ((unsigned long long)epoch << 32) | rec_base, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
         uint32_t rem = used > pre ? used - pre : 0u;
         uint32_t slot = rec_base + (pre_p >> 18);
         uint32_t base = jpos + pre;
@@ -2311,7 +2322,6 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
         }
         if (used == 0u && tid == 0) s_base[(r + 1) & 1u] = rec_base;
         if (r < 4) JSP_STAMP(4051u, 4 + r);  // diagnostic: this run's records issued
-        if (early) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this run's records are out
         if (tid == 0) {  // the run's unplaceable tail, written after the walk (off the runs' chain)
             s_u0[r] = jpos + used;
             s_u1[r] = jpos + n;
@@ -2682,11 +2692,11 @@ __device__ __forceinline__ void fused_tail(const TallyArgs& a, const FusedArgs& 
     if (f.topo_in_lds)
         assign_block<kTallyThreads, true>(s_feas, f.C, f.topo, f.run_class, f.run_len, n_runs, J, f.assign,
                                           f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
-                                          f.pipe);
+                                          f.we);
     else
         assign_block<kTallyThreads, false>(s_feas, f.C, f.topo, f.run_class, f.run_len, n_runs, J, f.assign,
                                            f.stats, s_taken, m, s_topo, s_win, s_stage, kFusedStage, nullptr, nullptr,
-                                           f.pipe);
+                                           f.we);
     JSP_CLK(4090u, 2);
     JSP_STAMP(4090u, 3);
     if (done) signal_host(done, epoch, true);
@@ -3008,12 +3018,8 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                 if (q != seq && q != 0 && x.z == q) {
                     if ((x.y & kReqPatch) == 0u) {
                         const unsigned long long m = ((unsigned long long)x.y << 32) | q;
-                        // n_runs first (the tail reads it after the bell), then ring at
-                        // once (the first wave to see it; a second ringer writes the same words)
-                        if (v.nruns) {
-                            __hip_atomic_store(v.nruns, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                        }
+                        // ring at once (the first wave to see it; a second
+                        // ringer writes the same word)
                         if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
@@ -3047,10 +3053,6 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
                 const unsigned long long m =
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
-                if (v.nruns) {
-                    __hip_atomic_store(v.nruns, nr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                }
                 if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
@@ -3290,77 +3292,6 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         seq = next;
         __syncthreads();  // s_x[16..17] and the tally carve are rewritten by the next request
-    }
-}
-
-// The fused shape kept resident (cfg3, cfg5: several classes or levels, a
-// small snapshot): one workgroup per tally tile + the dispatcher, all with the
-// fused launch's LDS. Per request each tile tallies its leaves (sc1 row
-// loads), publishes its sums as the fused kernel does and adds to a device
-// counter; the tile whose add completes the request's count runs fused_tail
-// (runs, assign[], stats and the done word in pinned host memory).
-template <int W, int R>
-__global__ __launch_bounds__(kTallyThreads) void place_fused_service_kernel(TallyArgs a, FusedArgs f, ServiceArgs v) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-    const uint32_t tile = blockIdx.x;
-    const uint32_t n_tiles = a.n_blocks * f.groups;
-    if (tile == n_tiles) {
-        service_dispatch(v, a, lds);
-        return;
-    }
-    uint32_t* s_x = fused_flags(lds, a, f);  // [0] request seq [1] J [2] last-arriver flag
-    const FusedTile ft = fused_tile(tile, f.groups, f.cpg, f.C);
-    TallyArgs ag = a;
-    ag.c0 = ft.c0;
-    ag.nc = ft.nc;
-    ag.do_occ = ft.do_occ;
-    uint32_t seq = v.seq0;
-    while (true) {
-        if (threadIdx.x == 0) {
-            uint32_t next = 0, J = 0;  // next == 0: leave
-            const uint64_t t0 = wall_clock64();
-            while (true) {
-                const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const uint32_t q = (uint32_t)m;
-                // a stop carries its service's generation: one left by an
-                // earlier service in this (unzeroed) bell is not for us
-                if (q == kSvcStop && (uint32_t)(m >> 32) == v.gen) break;
-                if (q != seq && q != 0 && q != kSvcStop) {
-                    next = q;
-                    J = (uint32_t)(m >> 32);
-                    break;
-                }
-                if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            s_x[0] = next;
-            s_x[1] = J;
-        }
-        __syncthreads();
-        const uint32_t next = s_x[0], J = s_x[1];
-        if (next == 0) return;
-        tally_block<W, R, false, true>(ag, ft.blk, lds);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            if (!a.sc1_out) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            const unsigned long long old =
-                __hip_atomic_fetch_add(v.counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            s_x[2] = (old + 1) % n_tiles == 0 ? 1u : 0u;  // requests never overlap: the host waits
-        }
-        __syncthreads();
-        if (s_x[2] != 0) {
-            // the request's fields are passed apart: a modified copy of f would
-            // live in scratch (its arrays are indexed at run time)
-            fused_tail<W, R>(a, f, lds, J, __hip_atomic_load(v.nruns, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                             next, v.done);
-        }
-        // drop this CU's L1 lines before the next request (patches come from
-        // other launches), off the request path
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        seq = next;
-        __syncthreads();  // s_x and the tally carve are rewritten by the next request
     }
 }
 
@@ -3746,18 +3677,6 @@ hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t 
     JSP_DISPATCH_WR(launch_service_wr, a, v, s)
 }
 
-template <int W, int R>
-static hipError_t launch_fused_service_wr(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v,
-                                          hipStream_t s) {
-    jsp_launch((place_fused_service_kernel<W, R>), dim3(a.n_blocks * f.groups + 1), dim3(kTallyThreads), f.lds_bytes,
-                       s, a, f, v);
-    return hipGetLastError();
-}
-
-hipError_t launch_fused_service(const TallyArgs& a, const FusedArgs& f, const ServiceArgs& v, hipStream_t s) {
-    JSP_DISPATCH_WR(launch_fused_service_wr, a, f, v, s)
-}
-
 size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
     return sizeof(uint32_t) * ((size_t)tally_lds_words((int)cpg, (int)cpg + 1, (int)la) + 16 + kTallyThreads + 4);
 }
@@ -3783,9 +3702,8 @@ hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const S
 
 template <int W, int R>
 static hipError_t service_occupancy_wr(const TallyArgs&, int shape, size_t lds_bytes, int* blocks) {
-    const void* fn = shape == 2   ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
-                     : shape == 3 ? reinterpret_cast<const void*>(&place_split_service_kernel<W, R>)
-                                  : reinterpret_cast<const void*>(&place_fused_service_kernel<W, R>);
+    const void* fn = shape == 2 ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
+                                : reinterpret_cast<const void*>(&place_split_service_kernel<W, R>);
     return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, fn, kTallyThreads, lds_bytes);
 }
 
@@ -3852,47 +3770,38 @@ hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, co
     return hipGetLastError();
 }
 
-// The pipelined batch walk (assign_block); JSP_NO_PIPE=1 turns it off (A/B runs).
-bool pipe_walk_enabled() {
-    static const bool on = [] {
-        const char* v = std::getenv("JSP_NO_PIPE");
-        return !(v && v[0] == '1');
-    }();
-    return on;
-}
-
 hipError_t launch_assign(const uint64_t* feas, const uint32_t* word_off, const DevClass* cls, uint32_t C,
                          const TopoDev& topo, uint32_t t_words, uint32_t feas_words, const uint32_t* run_class,
                          const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                         uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s) {
+                         uint32_t* rec_count, AssignRec* recs, hipStream_t s, const WaitErr& we) {
     const uint32_t topo_words = topo.K > 1 ? topo_table_words(topo.K, topo.D) : 0u;
     const AssignPlan p = plan_assign(t_words, feas_words, topo_words);
     if (p.lds_bytes == 0) return hipErrorInvalidValue;
     jsp_launch(assign_kernel, dim3(1), dim3(kAssignThreads), p.lds_bytes, s, feas, word_off, cls, C, topo,
                        run_class, run_len, n_runs, J, assign, stats, feas_words, p.feas_in_lds, p.topo_in_lds,
-                       topo_words, p.stage_cap, recs, rec_count, pipe_walk_enabled() ? 1u : 0u);
+                       topo_words, p.stage_cap, recs, rec_count, we);
     if (hipError_t e = hipGetLastError(); e != hipSuccess || recs == nullptr || J == 0) return e;
     // Records never outnumber the placed jobs (each taken domain is in one
     // record), nor the feasibility words plus one per run (a run's records are
     // distinct words of its class; the next run of the class may share one).
     const uint64_t wb = (uint64_t)feas_words + n_runs;
     const uint32_t bound = wb < J ? (uint32_t)wb : J;
-    const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
+    const uint32_t rpw = kExpandRpw;
     const uint32_t waves = (bound + rpw - 1) / rpw;
     jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
     return hipGetLastError();
 }
 
-// the level walker's shape for nw words: (words per thread, threads);
-// JSP_LEVEL_NT=256 keeps 256 threads up to 2048 words (A/B)
+// the level walker's shape for nw words: (words per thread, threads). Up to
+// 256 words, 256 threads with one word each; above, 1024 threads with one or
+// two words each (four waves per SIMD hide each other's latency in the
+// per-run chain)
 static void level_shape(uint32_t nw, uint32_t* wpt, uint32_t* nt) {
-    static const bool narrow = [] { const char* v = std::getenv("JSP_LEVEL_NT"); return v && std::atoi(v) == 256; }();
     *wpt = 0;
     *nt = 256;
     if (nw <= 256) *wpt = 1;
-    else if (!narrow && nw <= 1024) { *wpt = 1; *nt = 1024; }
-    else if (!narrow && nw <= 2048) { *wpt = 2; *nt = 1024; }
-    else if (narrow && nw <= 2048) *wpt = nw <= 512 ? 2u : nw <= 1024 ? 4u : 8u;
+    else if (nw <= 1024) { *wpt = 1; *nt = 1024; }
+    else if (nw <= 2048) { *wpt = 2; *nt = 1024; }
 }
 
 size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
@@ -3903,43 +3812,33 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
 
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
-                               uint32_t* rec_count, AssignRec* recs, uint32_t expand_rpw, hipStream_t s,
-                               unsigned long long* ready, uint32_t epoch) {
+                               uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
+                               uint32_t epoch, const WaitErr& we) {
     uint32_t wpt, nt;
     level_shape(nw, &wpt, &nt);
     const size_t lds = level_walk_lds_bytes(C, nw);
-    if (wpt == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || lds > 128u * 1024u)
+    if (wpt == 0 || nw == 0 || n_runs > kLevelMaxRuns || recs == nullptr || ready == nullptr || lds > 128u * 1024u)
         return hipErrorInvalidValue;
     // records: one per (run, word) that gives domains away; a class's runs
     // take its words in order, so at most its words plus one per run
     const uint64_t wb = (uint64_t)C * nw + n_runs;
     const uint32_t bound = wb < J ? (uint32_t)wb : J;
-    const uint32_t rpw = expand_rpw < 1 ? 1u : expand_rpw > 64 ? 64u : expand_rpw;
+    const uint32_t rpw = kExpandRpw;
     const uint32_t waves = (bound + rpw - 1) / rpw;
-    // one launch (ready != null): the walker plus the expanders behind it
+    // one launch: the walker plus the expanders behind it (none for J = 0)
     unsigned long long* rd = J > 0 ? ready : nullptr;
     const uint32_t wpb = nt / 64;  // expander waves per workgroup
     const dim3 g(rd ? 1u + (waves + wpb - 1) / wpb : 1u), b(nt);
-    // early expansion (JSP_LEVEL_EARLY=1, A/B): the walker publishes after every run
-    static const bool early = [] { const char* v = std::getenv("JSP_LEVEL_EARLY"); return v && v[0] == '1'; }();
-    const uint32_t rpw_k = rpw | (rd && early ? kLevelEarly : 0u);
 #define JSP_LEVEL_LAUNCH(W_, N_) \
     jsp_launch((assign_level_kernel<W_, N_>), g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, \
-               stats, rec_count, recs, rd, epoch, bound, rpw_k)
+               stats, rec_count, recs, rd, epoch, bound, rpw, we)
     if (nt == 1024) {
         if (wpt == 1) JSP_LEVEL_LAUNCH(1, 1024);
         else JSP_LEVEL_LAUNCH(2, 1024);
     } else {
-        switch (wpt) {
-            case 1: JSP_LEVEL_LAUNCH(1, 256); break;
-            case 2: JSP_LEVEL_LAUNCH(2, 256); break;
-            case 4: JSP_LEVEL_LAUNCH(4, 256); break;
-            default: JSP_LEVEL_LAUNCH(8, 256); break;
-        }
+        JSP_LEVEL_LAUNCH(1, 256);
     }
 #undef JSP_LEVEL_LAUNCH
-    if (hipError_t e = hipGetLastError(); e != hipSuccess || J == 0 || rd) return e;
-    jsp_launch(expand_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, recs, rec_count, bound, rpw, assign);
     return hipGetLastError();
 }
 

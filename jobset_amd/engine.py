@@ -258,13 +258,10 @@ class Engine:
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
-    def set_service(self, enable: bool, device_walk: bool = False) -> None:
+    def set_service(self, enable: bool) -> None:
         """Resident placement service for host-API placements
-        (jsp_engine_set_service; on by default). device_walk: the
-        multi-class shapes walk on the GPU (fused resident kernel) instead of
-        the split service's host walk (A/B)."""
-        mode = native.JSP_SERVICE_OFF if not enable else (
-            native.JSP_SERVICE_DEVICE_WALK if device_walk else native.JSP_SERVICE_AUTO)
+        (jsp_engine_set_service; on by default)."""
+        mode = native.JSP_SERVICE_AUTO if enable else native.JSP_SERVICE_OFF
         check(self._lib.jsp_engine_set_service(self._h, mode))
 
     def service_stop(self) -> None:

@@ -49,12 +49,13 @@ class JspTiming(ctypes.Structure):
                 ("host_launch_us", ctypes.c_double), ("host_wait_us", ctypes.c_double),
                 ("host_post_us", ctypes.c_double), ("svc_calls", ctypes.c_uint64), ("svc_starts", ctypes.c_uint64),
                 ("svc_us", ctypes.c_double), ("svc_fallbacks", ctypes.c_uint64),
-                ("svc_ready_us", ctypes.c_double), ("patches", ctypes.c_uint64), ("patch_us", ctypes.c_double),
+                ("svc_ready_us", ctypes.c_double), ("svc_pre_us", ctypes.c_double),
+                ("svc_answer_us", ctypes.c_double), ("patches", ctypes.c_uint64), ("patch_us", ctypes.c_double),
                 ("wake_us", ctypes.c_double)]
 
 
 JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
-JSP_SERVICE_OFF, JSP_SERVICE_AUTO, JSP_SERVICE_DEVICE_WALK = 0, 1, 2
+JSP_SERVICE_OFF, JSP_SERVICE_AUTO = 0, 1
 
 
 # (name, restype, argtypes) — every entry point declared in include/jsplace.h

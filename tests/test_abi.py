@@ -35,11 +35,20 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_struct_layout():
     lib = native.lib()
-    assert lib.jsp_abi_version() == 5
+    assert lib.jsp_abi_version() == 6
     # layouts the Go cgo wrapper relies on
     assert ctypes.sizeof(native.JspJobClass) == 8 * 4 * 2 + 4 * 3 + 4 * 4 + 4  # 100 B + 4 pad
     assert ctypes.sizeof(native.JspTopology) == 4 + 4 * 4 + 4 + 8 * 4
     assert ctypes.sizeof(native.JspStats) == 24
+
+
+def test_library_reads_only_operational_switches():
+    """The shipped library names no A/B switch: the only environment
+    variables it reads are the operational ones and the tests' hook string
+    (jsplace.h "Environment")."""
+    blob = open(os.path.join(ROOT, "jobset_amd", "libjsplace.so"), "rb").read()
+    names = {n.decode() for n in re.findall(rb"JSP_[A-Z0-9_]+", blob)}
+    assert names <= {"JSP_SERVICE", "JSP_SERVICE_IDLE_MS", "JSP_RCCL_LIB", "JSP_TEST_HOOKS"}, names
 
 
 def test_no_gpu_fails_loudly():

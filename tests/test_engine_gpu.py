@@ -86,7 +86,7 @@ def test_multichunk_workgroups_parity(any_engine, monkeypatch, chunks, seed):
     """Workgroups owning several 1024-row chunks (the next chunk's rows are
     prefetched while one is evaluated): ragged leaves straddle chunk borders;
     every launch shape, incl. the fused tail and the single-class compaction."""
-    monkeypatch.setenv("JSP_BLOCK_CHUNKS", str(chunks))
+    monkeypatch.setenv("JSP_TEST_HOOKS", f"block_chunks={chunks}")  # read at snapshot upload
     p = synth.random_problem(3000 + seed, max_nodes=60_000, max_leaves=3000)
     got, a, cap, occ = run_both(any_engine, p)
     assert_same(got, a, cap, occ)
@@ -326,10 +326,10 @@ def test_double_buffered_wave_tally(monkeypatch, cfg):
     """The tally's double-buffered wave kernel (several tiles per wave, the next
     tile's rows in flight while one is evaluated): the default one-tile-per-wave
     kernel covers snapshots up to ~6k tiles, so this path is forced here
-    (JSP_TALLY_ONE=0, read at engine creation) and 1-8 waves per SIMD are not
-    needed: the tally and the placement must equal the oracle's."""
+    (test hook tally_one=0): the tally and the placement must equal the
+    oracle's."""
     import torch
-    monkeypatch.setenv("JSP_TALLY_ONE", "0")
+    monkeypatch.setenv("JSP_TEST_HOOKS", "tally_one=0")
     e = Engine(0)
     try:
         p = synth.CONFIGS[cfg]()
@@ -346,26 +346,20 @@ def test_double_buffered_wave_tally(monkeypatch, cfg):
         e.close()
 
 
-@pytest.mark.parametrize("rpw", ["1", "7", "64", "staged"])
-def test_expand_records_per_wave(monkeypatch, rpw):
-    """The three-launch path's record expansion with 1, 7 (records straddling
-    waves unevenly) and 64 records per wave (JSP_EXPAND_RPW, read at engine
-    creation; default 16): each configuration places as the oracle does."""
-    if rpw == "staged":  # long runs through the LDS stage and coalesced stores, no records
-        monkeypatch.setenv("JSP_ASSIGN_RECORDS", "0")
-    else:
-        monkeypatch.setenv("JSP_EXPAND_RPW", rpw)
-    e = Engine(0)
+def test_expand_records_three_launch(engine):
+    """The three-launch path's long runs as records expanded by the grid
+    (16 records per wave, straddling waves unevenly on ragged problems):
+    each configuration places as the oracle does."""
+    engine.set_fused(False)
     try:
-        e.set_fused(False)
         probs = [synth.CONFIGS[cfg]() for cfg in (1, 2, 4, 5)]
         probs += [synth.random_problem(7000 + s, max_nodes=100_000, max_jobs=20_000) for s in range(6)]
         for p in probs:
-            got, a, cap, occ = run_both(e, p)
+            got, a, cap, occ = run_both(engine, p)
             assert got.fused == 0
             assert_same(got, a, cap, occ)
     finally:
-        e.close()
+        engine.set_fused(True)
 
 
 def test_patch_then_place(engine):
@@ -562,14 +556,14 @@ def test_host_placer_equals_place(engine):
 def test_lookback_timeout_is_reported(engine, monkeypatch):
     """A compaction launch whose look-back gives up must not return a silently
     wrong assign[]: jsp_place raises, and on the device path jsp_engine_check
-    (or the next call) does. JSP_LOOKBACK_SPINS=0 makes every wait a timeout."""
+    (or the next call) does. The hook lookback_spins=0 makes every wait a timeout."""
     import torch
     from jobset_amd.native import JSP_EHIP
     from jobset_amd.snapshot import job_runs
     p = synth.config4()
     p.classes = [p.classes[0]]
     p.job_class = np.zeros(30_000, dtype=np.uint32)
-    monkeypatch.setenv("JSP_LOOKBACK_SPINS", "0")  # read at snapshot upload
+    monkeypatch.setenv("JSP_TEST_HOOKS", "lookback_spins=0")  # read at snapshot upload
     engine.load(p)
     with pytest.raises(JspError) as ei:
         for _ in range(5):  # ~1000 tiles: some tile always finds a predecessor unpublished
@@ -585,7 +579,7 @@ def test_lookback_timeout_is_reported(engine, monkeypatch):
             engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
             engine.check()
     assert ei.value.code == JSP_EHIP
-    monkeypatch.delenv("JSP_LOOKBACK_SPINS")
+    monkeypatch.delenv("JSP_TEST_HOOKS")
     engine.check()  # nothing new since the last report
     engine.load(p)
     got = engine.place(p.job_class, want_tally=True)
@@ -781,15 +775,13 @@ def test_folded_feasibility_and_level_walk(engine, seed):
         engine.set_fused(True)
 
 
-@pytest.mark.parametrize("one", ["1", "0"])
-@pytest.mark.parametrize("seed", range(8))
-def test_level_walk_one_launch_job_counts(engine, monkeypatch, one, seed):
+@pytest.mark.parametrize("seed", range(12))
+def test_level_walk_one_launch_job_counts(engine, seed):
     """The level walk with its expansion in the same launch (expander
-    workgroups wait for the walker's record count; JSP_LEVEL_ONE_LAUNCH=0:
-    a second launch): J = 0, 1, a few, about the domain count and well past
-    it (every run's tail unplaceable), empty leading runs, bit-exact."""
+    workgroups wait for the walker's record count): J = 0, 1, a few, about
+    the domain count and well past it (every run's tail unplaceable), empty
+    leading runs, bit-exact."""
     import dataclasses
-    monkeypatch.setenv("JSP_LEVEL_ONE_LAUNCH", one)
     base = _one_level(synth.random_problem(seed, max_nodes=30_000, max_leaves=3000, max_jobs=3000),
                       0, 4, True, seed)
     K = base.topology.n_levels
@@ -832,3 +824,66 @@ def test_folded_feasibility_after_patches(engine):
         np.testing.assert_array_equal(engine.place(p.job_class).assign, O.place_c(p)[0])
     finally:
         engine.set_fused(True)
+
+
+def _expect_reported_or_exact(engine, p, calls, word):
+    """Place `calls` times: every call either raises JSP_EHIP naming `word`
+    or returns the oracle's answer -- never a stale assign[] with success.
+    Returns how many calls raised."""
+    from jobset_amd.native import JSP_EHIP
+    a = O.place_c(p)[0]
+    errors = 0
+    for _ in range(calls):
+        try:
+            got = engine.place(p.job_class)
+        except JspError as ex:
+            assert ex.code == JSP_EHIP and word in str(ex), str(ex)
+            errors += 1
+            continue
+        np.testing.assert_array_equal(got.assign, a)
+    return errors
+
+
+def test_level_expand_timeout_is_reported(monkeypatch):
+    """The one-launch level walk's expanders wait (bounded) for the walker's
+    record count. One that gives up must fail the call, never leave a stale
+    assign[]: with the hook wait_us=0 every expander that starts before the
+    walker has published gives up at once."""
+    monkeypatch.setenv("JSP_TEST_HOOKS", "wait_us=0")
+    e = Engine(0)
+    try:
+        e.set_fused(False)
+        p = synth.config4()
+        e.load(p)
+        errors = _expect_reported_or_exact(e, p, 6, "expanders")
+        assert errors >= 1
+        monkeypatch.delenv("JSP_TEST_HOOKS")
+        e.load(p)  # hooks are read again at upload: the default wait
+        assert _expect_reported_or_exact(e, p, 3, "expanders") == 0
+    finally:
+        e.close()
+
+
+def test_pipe_walk_timeout_is_reported(monkeypatch):
+    """The pipelined batch walk (many short leaf-level runs) waits for the
+    earlier batches' progress words. A wait that gives up (hook pipe_spins=0:
+    the first wait) fails the call on the launch path and the three-launch
+    path alike; the default limit answers bit-exactly."""
+    errors = 0
+    for seed in range(4):
+        base = synth.random_problem(seed, max_nodes=30_000, max_leaves=3000, max_jobs=3000)
+        p = _one_level(base, base.topology.n_levels - 1, 4, False, seed)
+        monkeypatch.setenv("JSP_TEST_HOOKS", "pipe_spins=0")
+        e = Engine(0)
+        try:
+            e.set_service(False)
+            for fused in (True, False):
+                e.set_fused(fused)
+                e.load(p)
+                errors += _expect_reported_or_exact(e, p, 4, "pipelined")
+            monkeypatch.delenv("JSP_TEST_HOOKS")
+            e.load(p)
+            assert _expect_reported_or_exact(e, p, 2, "pipelined") == 0
+        finally:
+            e.close()
+    assert errors >= 1

@@ -63,7 +63,7 @@ def test_no_kernel_uses_scratch():
     kernels = _kernel_notes()
     # every kernel family of the engine is in the library
     for fam in ("tally_kernel", "feas_kernel", "assign_kernel", "expand_kernel", "place_compact_kernel",
-                "place_fused_kernel", "place_service_kernel", "place_fused_service_kernel"):
+                "place_fused_kernel", "place_service_kernel", "place_split_service_kernel", "assign_level_kernel"):
         assert any(fam in k for k in kernels), fam
     # The resident compaction service at R = 1 runs at the SGPR limit (106):
     # the backend reserves a 36-byte frame for its SGPR spill bookkeeping that

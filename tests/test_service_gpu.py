@@ -242,23 +242,15 @@ def test_service_early_answer_then_patch_and_varying_jobs(svc_engine):
     svc_engine.check()
 
 
-# ---------------------------------------------------------------- fused shape (cfg3, cfg5)
-# Two resident forms: the split service (default: tiles hand back per-domain
-# feasibility, the host walks; stats.fused 5) and the fused service (the walk
-# on the GPU by the tile that finished last; stats.fused 4).
-WALKS = [pytest.param(False, id="host-walk"), pytest.param(True, id="device-walk")]
+# ---------------------------------------------------------------- multi-class shapes (cfg3, cfg5)
+# The split service: resident tiles hand back per-domain feasibility, the
+# host walks (stats.fused 5).
 
 
-def walk_shape(device_walk):
-    return 4 if device_walk else 5
-
-
-@pytest.mark.parametrize("device_walk", WALKS)
 @pytest.mark.parametrize("cfg", [3, 5])
-def test_fused_service_configs(svc_engine, cfg, device_walk):
+def test_fused_service_configs(svc_engine, cfg):
     """The multi-class shape resident: several classes / levels, 100 requests
-    each, in both forms."""
-    svc_engine.set_service(True, device_walk=device_walk)
+    each."""
     p = synth.CONFIGS[cfg]()
     svc_engine.load(p)
     a = O.place_c(p)[0]
@@ -266,19 +258,17 @@ def test_fused_service_configs(svc_engine, cfg, device_walk):
     call = svc_engine.host_placer(*job_runs(p.job_class))
     for _ in range(100):
         st = call()
-        assert st.fused == walk_shape(device_walk)
+        assert st.fused == 5
         np.testing.assert_array_equal(call.assign, a)
         assert st.placed == int((a >= 0).sum())
     rc, rl = job_runs(p.job_class)
     assert st.runs == rc.shape[0]
 
 
-@pytest.mark.parametrize("device_walk", WALKS)
 @pytest.mark.parametrize("seed", range(40))
-def test_fused_service_random_parity(svc_engine, seed, device_walk):
+def test_fused_service_random_parity(svc_engine, seed):
     """Ragged random snapshots in their own shape (a resident service when the
     snapshot is small enough), the job order changing between requests."""
-    svc_engine.set_service(True, device_walk=device_walk)
     p = synth.random_problem(seed)
     svc_engine.load(p)
     a = O.place_c(p)[0]
@@ -293,12 +283,10 @@ def test_fused_service_random_parity(svc_engine, seed, device_walk):
     np.testing.assert_array_equal(ref.assign, a)
 
 
-@pytest.mark.parametrize("device_walk", WALKS)
-def test_fused_service_patch_and_device_path(svc_engine, device_walk):
+def test_fused_service_patch_and_device_path(svc_engine):
     """cfg5 resident while device-path launches (their own tally buffers) and
     patches interleave with its requests."""
     import torch
-    svc_engine.set_service(True, device_walk=device_walk)
     p = synth.config5()
     svc_engine.load(p)
     rc, rl = job_runs(p.job_class)
@@ -310,7 +298,7 @@ def test_fused_service_patch_and_device_path(svc_engine, device_walk):
     warm(svc_engine, p.job_class)
     for step in range(20):
         got = svc_engine.place(p.job_class)
-        assert got.fused == walk_shape(device_walk)
+        assert got.fused == 5
         np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
         svc_engine.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(),
                                 side.cuda_stream)
@@ -323,7 +311,7 @@ def test_fused_service_patch_and_device_path(svc_engine, device_walk):
 
 def test_two_engines_with_services(svc_engine):
     """Two engines on one GPU, each with its own resident service (compaction
-    on one, fused on the other), requests interleaved; destroying one while
+    on one, split on the other), requests interleaved; destroying one while
     its service runs leaves the other answering."""
     from jobset_amd.engine import Engine
     p2, q5 = synth.config2(), synth.config5()
@@ -352,7 +340,7 @@ def test_service_request_numbers_across_2_pow_30(monkeypatch):
     before them across 2^30. A service started at 2^30 - 3 answers
     every request bit-exactly through the wrap."""
     from jobset_amd.engine import Engine
-    monkeypatch.setenv("JSP_SVC_SEQ0", str((1 << 30) - 3))
+    monkeypatch.setenv("JSP_TEST_HOOKS", f"seq0={(1 << 30) - 3}")
     e = Engine(0)
     try:
         p = synth.config2()
@@ -378,12 +366,12 @@ def test_service_request_numbers_across_2_pow_30(monkeypatch):
 
 def test_service_that_cannot_fit_falls_back(monkeypatch):
     """Every workgroup of a service grid must be co-resident. On a GPU (or a
-    partition) with too few CUs for the grid -- JSP_SVC_CU_LIMIT stands in for
+    partition) with too few CUs for the grid -- the cu_limit hook stands in for
     one -- the service is not started: the call is answered by the launch
     path (same assign[]), counted once in jsp_timing.svc_fallbacks, and the
     engine stays on the launch path until the next upload."""
     from jobset_amd.engine import Engine
-    monkeypatch.setenv("JSP_SVC_CU_LIMIT", "2")  # read at engine creation
+    monkeypatch.setenv("JSP_TEST_HOOKS", "cu_limit=2")  # read at engine creation
     e = Engine(0)
     try:
         for cfg in (2, 5):
@@ -398,7 +386,7 @@ def test_service_that_cannot_fit_falls_back(monkeypatch):
             assert e.timing(reset=True).svc_fallbacks == 1
     finally:
         e.close()
-    monkeypatch.delenv("JSP_SVC_CU_LIMIT")
+    monkeypatch.delenv("JSP_TEST_HOOKS")
     e = Engine(0)  # no limit: the same snapshot is served by the service
     try:
         p = synth.config2()
@@ -444,20 +432,17 @@ def test_patch_wakes_the_service(svc_engine):
     np.testing.assert_array_equal(got.assign, a)
 
 
-@pytest.mark.parametrize("waker", ["1", "0"])
 @pytest.mark.parametrize("then", ["place", "patch_again", "upload", "tally_launch", "stop", "sync"])
-def test_wake_then_any_reader(svc_engine, monkeypatch, waker, then):
+def test_wake_then_any_reader(svc_engine, then):
     """A recovery's first patch after the service left is held back and the
-    waker thread restarts the service and posts it (JSP_SVC_WAKER=0: the
-    patch call does it inline). Whatever comes next -- the placement, a
-    second patch right behind it, a re-upload, a launch with tallies, an
-    explicit stop, a sync -- finds the patched rows, bit-exact, at once or
-    after the sleep the waker may still be in."""
-    monkeypatch.setenv("JSP_SVC_WAKER", waker)
+    waker thread restarts the service and posts it. Whatever comes next --
+    the placement, a second patch right behind it, a re-upload, a launch
+    with tallies, an explicit stop, a sync -- finds the patched rows,
+    bit-exact, at once or after the sleep the waker may still be in."""
     p = synth.config2()
     svc_engine.load(p)
     assert warm(svc_engine, p.job_class).fused == 3
-    rng = np.random.default_rng(len(then) + int(waker))
+    rng = np.random.default_rng(len(then))
     R = p.nodes.free.shape[0]
     for gap in (0.0, 0.003):
         time.sleep(0.08)  # past JSP_SERVICE_IDLE_MS: the service has left
@@ -528,20 +513,18 @@ def test_async_patch_sizes_then_place(svc_engine, n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mode", ["1", "2", "0"])
+@pytest.mark.parametrize("rep", range(3))
 @pytest.mark.parametrize("then", ["place", "tally_launch", "stop", "patch_again", "shared_rows"])
-def test_patch_applied_by_the_dispatcher(svc_engine, monkeypatch, mode, then):
+def test_patch_applied_by_the_dispatcher(svc_engine, rep, then):
     """A patch while the service is up is applied by its dispatcher: posted
-    at once and carried again by a request that finds it not yet applied
-    (JSP_SVC_PATCH=2, the default), held back and carried by the next request
-    (=1), or the patch kernel (=0). Whatever reads the rows next -- the
-    service's next request, a launch (tallies out), a service stop, another
-    patch (of the same rows) -- sees every patched column, bit-exact."""
-    monkeypatch.setenv("JSP_SVC_PATCH", mode)
+    at once and carried again by a request that finds it not yet applied.
+    Whatever reads the rows next -- the service's next request, a launch
+    (tallies out), a service stop, another patch (of the same rows) -- sees
+    every patched column, bit-exact."""
     p = synth.config2()
     svc_engine.load(p)
     assert warm(svc_engine, p.job_class).fused == 3
-    rng = np.random.default_rng(int(mode) * 10 + len(then))
+    rng = np.random.default_rng(rep * 10 + len(then))
     R = p.nodes.free.shape[0]
     rows0 = None
     for k in range(3):
@@ -599,19 +582,20 @@ def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
     assert svc_engine.timing(reset=True).svc_starts == 0
 
 
-@pytest.mark.parametrize("resident", ["1", "0"])
-@pytest.mark.parametrize("xcd", ["1", "0"])
-def test_service_colocated_and_spread(svc_engine, monkeypatch, xcd, resident):
+@pytest.mark.parametrize("hooks", ["", "svc_xcd=0", "block_chunks=2", "svc_xcd=0,block_chunks=2"])
+def test_service_colocated_and_spread(monkeypatch, hooks):
     """The compaction service co-located on one XCD (plain bell and granule
     stores when every workgroup votes the same XCC id) and spread over the
-    chip (write-through), with the tiles' rows held in registers (resident
-    path) or in LDS: the same answers, across requests, patches and J."""
-    monkeypatch.setenv("JSP_SVC_XCD", xcd)  # read at each service start
-    monkeypatch.setenv("JSP_SVC_RESIDENT", resident)
-    svc_engine.service_stop()
+    chip (write-through, as a partition mode would place it), with the
+    tiles' rows held in registers (one chunk per tile) or reloaded per
+    request (two-chunk tiles): the same answers, across requests, patches
+    and J."""
+    from jobset_amd.engine import Engine
+    monkeypatch.setenv("JSP_TEST_HOOKS", hooks)
+    svc_engine = Engine(0)
     p = synth.config2()
     svc_engine.load(p)
-    rng = np.random.default_rng(int(xcd) + 3)
+    rng = np.random.default_rng(len(hooks) + 3)
     for step in range(30):
         J = [990, 1, 500, 1200][step % 4]
         jc = np.zeros(J, dtype=np.uint32)
@@ -623,4 +607,44 @@ def test_service_colocated_and_spread(svc_engine, monkeypatch, xcd, resident):
             taints = rng.integers(0, 2, size=64).astype(np.uint32)
             svc_engine.patch_rows(rows, taints=taints)
             p.nodes.taints[rows] = taints
+    svc_engine.check()
+    svc_engine.close()
+
+
+@pytest.mark.parametrize("idle", [False, True])
+def test_wider_snapshot_then_inline_patch(svc_engine, idle):
+    """a snapshot upload that widens W and R (after the
+    armed service idled out, or while it runs), then small patches staged in
+    the service's inline buffer, then placements. The inline staging is sized
+    for the new W/R at the upload itself (the service is stopped there and no
+    patch is pending), so a staged delta is never lost to a reallocation or
+    read from freed memory: bit-exact with the oracle."""
+    p = synth.config2()  # W = 1, R = 3
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused == 3
+    if idle:
+        time.sleep(0.08)  # past JSP_SERVICE_IDLE_MS: the service left, still armed
+    N = p.nodes.n_nodes
+    wide = dataclasses.replace(
+        p.nodes,
+        labels=np.vstack([p.nodes.labels, np.zeros((3, N), dtype=np.uint64)]),
+        free=np.vstack([p.nodes.free, np.full((1, N), 1 << 20, dtype=np.uint32)]))
+    q = dataclasses.replace(p, nodes=wide)
+    svc_engine.upload_snapshot(q.nodes)
+    rng = np.random.default_rng(9 + int(idle))
+    for step in range(6):
+        if idle and step == 3:
+            time.sleep(0.08)
+        n = int(rng.integers(1, 30))
+        rows = np.sort(rng.choice(N, size=n, replace=False)).astype(np.uint32)
+        lab = q.nodes.labels[:, rows].copy()
+        lab[3] = rng.integers(0, 1 << 40, size=n).astype(np.uint64)  # a word no class reads
+        free = rng.integers(0, 200_000, size=(4, n)).astype(np.uint32)
+        taints = rng.integers(0, 2, size=n).astype(np.uint32)
+        svc_engine.patch_rows(rows, labels=lab, taints=taints, free=free)
+        q.nodes.labels[:, rows] = lab
+        q.nodes.free[:, rows] = free
+        q.nodes.taints[rows] = taints
+        got = svc_engine.place(q.job_class)
+        np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
     svc_engine.check()
