@@ -1,6 +1,7 @@
 // jsp_engine.cc — host side of the exclusive-topology placement engine:
 // the C ABI of include/jsplace.h over HIP device buffers and the kernels of
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
+#include <emmintrin.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -259,6 +260,13 @@ struct jsp_engine {
     uint32_t patch_bits = 0;            // its request bits (kReqPatch, kReqPatchInline)
     uint32_t patch_nf = 0;              // inline: n | column flags << 16 (the request's n_runs word)
     uint32_t patch_req = 0;             // the request that posted it alone (0: none)
+    // A micro-patch (jsp_internal.h kMailbox*): a patch small enough to ride
+    // in the next request's line, held back until a request carries it (no
+    // staging read, no post of its own); patches of the same columns merge
+    // into it while it is held
+    bool patch_micro = false;
+    uint32_t micro_n = 0, micro_fl = 0;  // its rows (distinct) and column flags
+    uint32_t micro_w[jsp::kMailboxPayload] = {};
     // The waker: a host thread that restarts the service for a recovery's
     // first patch off the caller's thread (the launch after an idle period
     // costs ~10 us of host time). wake_job is guarded by mu; the thread
@@ -457,16 +465,31 @@ uint32_t next_err_tag(jsp_engine* e, uint32_t kind) {
     return kind | e->err_tag;
 }
 
+// A wait's occasional HIP status query (has the stream finished, or failed?):
+// at most once per 20 us. A query is a runtime call whose code and data a
+// cold host core must first fetch, and the waits it guards mostly end within
+// a few microseconds.
+struct QueryPacer {
+    std::chrono::steady_clock::time_point next = std::chrono::steady_clock::now() + std::chrono::microseconds(20);
+    bool due() {
+        const auto t = std::chrono::steady_clock::now();
+        if (t < next) return false;
+        next = t + std::chrono::microseconds(20);
+        return true;
+    }
+};
+
 // Host placement path: wait for the kernel's completion words (one per
 // signalling workgroup) instead of the kernel-end signal. A finished stream
 // whose words are missing, or a failed stream, is an error.
 int wait_done(jsp_engine* e, hipStream_t s, uint32_t n, uint32_t epoch) {
     const uint32_t* words = e->h_done.as<uint32_t>();
     uint32_t i = 0;
+    QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
         while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == epoch) ++i;
         if (i == n) return JSP_OK;
-        if ((spins & 255) == 0) {
+        if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {
                 for (; i < n; ++i)
@@ -839,14 +862,43 @@ int svc_shape(jsp_engine* e) {
 }
 bool svc_ok(jsp_engine* e) { return svc_shape(e) != 0; }
 
-// Store request words (pinned host memory the dispatcher polls): the second
-// half first (the dispatcher reads both in one 16-byte load and takes a torn
-// read for none). A request line in device memory written through the BAR
-// was measured slower on every shape.
-void req_store(jsp_engine* e, unsigned long long w0, unsigned long long w1, bool both = true) {
-    unsigned long long* r = e->svc.box.as<unsigned long long>();
-    if (both) __atomic_store_n(r + 1, w1, __ATOMIC_RELEASE);
-    __atomic_store_n(r, w0, __ATOMIC_RELEASE);
+// The request line (pinned host memory the dispatcher polls, jsp_internal.h
+// kMailbox*) and, on a line of its own after it, the dispatcher's ready word.
+// A request line in device memory written through the BAR was measured
+// slower on every shape.
+constexpr size_t kBoxBytes = jsp::kMailboxBytes + 128;
+constexpr size_t kReadyWord = jsp::kMailboxBytes / 4 + 16;
+
+// One 16-byte chunk of the request line in one store (aligned 16-byte SSE
+// stores are single-copy atomic on x86-64 processors with AVX).
+inline void store16(uint32_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+    _mm_store_si128(reinterpret_cast<__m128i*>(p), _mm_set_epi32((int)d, (int)c, (int)b, (int)a));
+}
+
+// Post request `seq`: the micro-patch payload chunks (micro: the held-back
+// micro-patch rides in it), chunk 1 {seq, rows, patch number, flags}, then
+// chunk 0 -- its second half first: the dispatcher reads the whole line in
+// one load and takes a read whose chunks disagree on seq for none.
+void svc_request(jsp_engine* e, uint32_t seq, uint32_t jw, uint32_t w2, bool micro = false) {
+    uint32_t* b = e->svc.box.as<uint32_t>();
+    uint32_t m = 0, fl = 0, pseq = (jw & jsp::kReqPatch) ? e->patch_seq : 0u;
+    if (micro && e->micro_n > 0) {
+        m = e->micro_n;
+        fl = e->micro_fl;
+        pseq = e->patch_seq;
+        const uint32_t words = m * jsp::micro_row_words(e->W, e->R);
+        for (uint32_t c = 0; 3 * c < words; ++c)
+            store16(b + 4 * (2 + c), seq, e->micro_w[3 * c], e->micro_w[3 * c + 1], e->micro_w[3 * c + 2]);
+    }
+    store16(b + 4, seq, m, pseq, fl);
+    unsigned long long* r = reinterpret_cast<unsigned long long*>(b);
+    __atomic_store_n(r + 1, ((unsigned long long)w2 << 32) | seq, __ATOMIC_RELEASE);
+    __atomic_store_n(r, ((unsigned long long)jw << 32) | seq, __ATOMIC_RELEASE);
+}
+
+// The stop word (every workgroup of the service leaves).
+void svc_post_stop(jsp_engine* e) {
+    __atomic_store_n(e->svc.box.as<unsigned long long>(), (unsigned long long)jsp::kSvcStop, __ATOMIC_RELEASE);
 }
 
 int patch_wait(jsp_engine* e);
@@ -859,7 +911,7 @@ int svc_stop(jsp_engine* e) {
     v.pending = 0;  // the stop waits for the kernel to leave, i.e. for every tile to finish
     if (!v.running) return JSP_OK;
     v.running = false;
-    req_store(e, (unsigned long long)jsp::kSvcStop, 0, false);
+    svc_post_stop(e);
     // The kernel leaves within microseconds of the stop word: poll for it
     // rather than sleep in a blocking synchronize (whose wake-up costs more
     // than the exit itself); after 2 ms, block
@@ -941,7 +993,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
         std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
         v.layout_key = lkey;
     }
-    HIP_TRY(v.box.reserve(64));
+    HIP_TRY(v.box.reserve(kBoxBytes));
     const size_t gbytes = (size_t)8 * std::max<uint32_t>(nb, 1), gpad = (gbytes + 127) & ~size_t(127);
     // granules, then the bell on a line of its own, then the XCC votes.
     // Zeroed only when allocated or the geometry changes: granule tags and
@@ -959,9 +1011,9 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
         HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 128, v.stream));
         v.zero_key = key;
     }
-    req_store(e, (unsigned long long)v.seq, (unsigned long long)v.seq);
+    svc_request(e, v.seq, 0u, 0u);  // already answered: the new dispatcher starts after it
     v.gen = v.gen % 0x7FFFFFFFu + 1u;
-    uint32_t* ready = v.box.as<uint32_t>() + 8;
+    uint32_t* ready = v.box.as<uint32_t>() + kReadyWord;
     __atomic_store_n(ready, 0u, __ATOMIC_RELEASE);
     uint32_t* w = v.words.as<uint32_t>();
     jsp::ServiceArgs a{};
@@ -1062,10 +1114,11 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
 int svc_wait_ready(jsp_engine* e) {
     auto& v = e->svc;
     if (!v.pending_ready) return JSP_OK;
-    const uint32_t* ready = v.box.as<uint32_t>() + 8;
+    const uint32_t* ready = v.box.as<uint32_t>() + kReadyWord;
     const auto t_start = v.t_launch;
+    QueryPacer qp;
     for (uint64_t spins = 1; __atomic_load_n(ready, __ATOMIC_ACQUIRE) != v.gen; ++spins) {
-        if ((spins & 255) == 0) {
+        if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q != hipErrorNotReady) {
                 v.running = false;
@@ -1098,6 +1151,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     const char* as = v.shape == 2 ? static_cast<const char*>(v.assign.p) : nullptr;
     size_t pf = 0;
     uint32_t i = 0;
+    QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
         while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) {
             if (split) e->walk.prefetch_tile(v.split.as<uint64_t>(), i);  // its slots are final: start their misses
@@ -1108,7 +1162,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             }
         }
         if (i == n) return JSP_OK;
-        if ((spins & 255) == 0) {
+        if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {
                 for (; i < n; ++i)
@@ -1155,6 +1209,7 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
     const unsigned long long* a = v.assign.as<unsigned long long>();
     const uint32_t* w = v.words.as<uint32_t>();
     uint32_t i = 0, n = 0;
+    QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
         while (i < J) {
             const unsigned long long x = __atomic_load_n(a + i, __ATOMIC_ACQUIRE);
@@ -1169,6 +1224,7 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
         }
         if ((spins & 255) == 0) {
             if (__atomic_load_n(w + v.nb + 2, __ATOMIC_ACQUIRE) != v.err_ack) return kSvcFailed;
+            if (!qp.due()) continue;
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {  // it left: whatever arrived is all there is
                 for (; i < J; ++i) {
@@ -1196,11 +1252,6 @@ uint32_t next_seq(uint32_t q) {
     return s;
 }
 
-// Post a request word (second half first: the dispatcher reads both in one
-// 16-byte load and takes a torn read for none).
-void svc_post(jsp_engine* e, uint32_t seq, uint32_t jw, uint32_t n_runs) {
-    req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)n_runs << 32) | seq);
-}
 
 // Wait for the last snapshot patch's completion word (the rows are then in
 // memory for every later reader, the resident tiles' `sc1` loads included).
@@ -1214,7 +1265,7 @@ void patch_post_deferred(jsp_engine* e) {
     const uint32_t seq = next_seq(v.seq);
     v.seq = seq;
     v.last = std::chrono::steady_clock::now();
-    svc_post(e, seq, e->patch_bits | jsp::kReqPatchOnly, e->patch_nf);
+    svc_request(e, seq, e->patch_bits | jsp::kReqPatchOnly, e->patch_nf, e->patch_micro);
     e->patch_req = seq;
 }
 
@@ -1331,7 +1382,7 @@ void svc_wake(jsp_engine* e) {
     const uint32_t seq = next_seq(v.seq);
     v.seq = seq;
     v.last = std::chrono::steady_clock::now();
-    req_store(e, (0x80000000ull << 32) | seq, (unsigned long long)seq);
+    svc_request(e, seq, jsp::kReqDirty, 0u);
     // rows marked patched, and they stay marked: the patch kernel may not
     // have landed when the warm-up loads them, so the next request (which
     // waits for the patch's completion word) loads them again
@@ -1355,8 +1406,8 @@ void run_wake(jsp_engine* e) {
     const uint32_t seq = next_seq(v.seq);
     v.seq = seq;
     v.last = std::chrono::steady_clock::now();
-    svc_post(e, seq, e->patch_bits | jsp::kReqDirty,
-             (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : 0u);
+    svc_request(e, seq, e->patch_bits | jsp::kReqDirty, (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : 0u,
+                e->patch_micro);
     e->patch_req = seq;
     e->patch_deferred = false;
     v.pending = seq;
@@ -1458,13 +1509,14 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         // the tiles keep their rows on chip: bit 31 of J tells them the
         // snapshot was patched since their previous request (J < 2^28)
         const uint32_t jw = J | (v.rows_dirty ? jsp::kReqDirty : 0u) | (carry ? e->patch_bits : 0u);
+        const bool micro = carry && e->patch_micro;
         carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
         v.rows_dirty = false;
         if (attempt == 0) {
             t_post = std::chrono::steady_clock::now();
             e->acc.svc_pre_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
         }
-        req_store(e, ((unsigned long long)jw << 32) | seq, ((unsigned long long)w2 << 32) | seq);
+        svc_request(e, seq, jw, w2, micro);
         const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
         if (rc == kSvcFailed) {
             v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
@@ -1524,6 +1576,87 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     // the copy-out's share of the wait (jsp_timing.host_post_us on this path)
     e->acc.host_post_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count();
     e->acc.svc_calls += 1;
+    return JSP_OK;
+}
+
+// ---- micro-patches (jsp_internal.h kMailbox*)
+// Whether the resident service is up and fresh enough to take a patch
+// through its dispatcher (not about to idle out, the engine's shape).
+bool svc_up(jsp_engine* e) {
+    auto& v = e->svc;
+    const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
+    return v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+}
+
+// Merge n rows of one patch call (columns fl) into the held micro-patch: a
+// row already held takes the new values, a new row is appended. All or
+// nothing: false when the rows do not fit.
+bool micro_merge(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels, const uint32_t* taints,
+                 const uint32_t* free_res, const int32_t* excl) {
+    const uint32_t W = e->W, R = e->R, rw = jsp::micro_row_words(W, R), cap = jsp::micro_rows_max(W, R);
+    uint32_t w[jsp::kMailboxPayload];
+    std::memcpy(w, e->micro_w, sizeof w);
+    uint32_t m = e->micro_n;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t r = 0;
+        while (r < m && w[r * rw] != rows[i]) ++r;
+        if (r == m) {
+            if (m == cap) return false;
+            std::memset(w + r * rw, 0, rw * 4);
+            w[r * rw] = rows[i];
+            ++m;
+        }
+        uint32_t* x = w + r * rw;
+        if (labels)
+            for (uint32_t k = 0; k < W; ++k) {
+                const uint64_t l = labels[(size_t)k * n + i];
+                x[1 + 2 * k] = (uint32_t)l;
+                x[2 + 2 * k] = (uint32_t)(l >> 32);
+            }
+        if (taints) x[1 + 2 * W] = taints[i];
+        if (free_res)
+            for (uint32_t k = 0; k < R; ++k) x[2 + 2 * W + k] = free_res[(size_t)k * n + i];
+        if (excl) x[2 + 2 * W + R] = (uint32_t)excl[i];
+    }
+    std::memcpy(e->micro_w, w, sizeof w);
+    e->micro_n = m;
+    return true;
+}
+
+// The held micro-patch in its kernel form too (engine staging, pinned): the
+// patch kernel applies it if the service leaves before a request carries it.
+int micro_stage_kernel_form(jsp_engine* e) {
+    const uint32_t W = e->W, R = e->R, rw = jsp::micro_row_words(W, R), m = e->micro_n, fl = e->micro_fl;
+    const jsp::PatchInlineLayout L = jsp::patch_inline_layout(m, 15u, W, R);
+    HIP_TRY(e->h_patch.reserve(L.bytes, grave(e)));
+    char* hp = static_cast<char*>(e->h_patch.p) - 64;  // the inline layout without its header
+    for (uint32_t r = 0; r < m; ++r) {
+        const uint32_t* x = e->micro_w + r * rw;
+        reinterpret_cast<uint32_t*>(hp + L.rows)[r] = x[0];
+        for (uint32_t k = 0; k < W; ++k)
+            reinterpret_cast<uint64_t*>(hp + L.lab)[(size_t)k * m + r] = ((uint64_t)x[2 + 2 * k] << 32) | x[1 + 2 * k];
+        reinterpret_cast<uint32_t*>(hp + L.taint)[r] = x[1 + 2 * W];
+        for (uint32_t k = 0; k < R; ++k) reinterpret_cast<uint32_t*>(hp + L.free)[(size_t)k * m + r] = x[2 + 2 * W + k];
+        reinterpret_cast<uint32_t*>(hp + L.excl)[r] = x[2 + 2 * W + R];
+    }
+    jsp::PatchArgs& a = e->last_patch;
+    a = jsp::PatchArgs{};
+    a.rows = reinterpret_cast<const uint32_t*>(hp + L.rows);
+    a.n = m;
+    a.npad = e->npad;
+    a.W = W;
+    a.R = R;
+    a.dlab = (fl & jsp::kPatchLab) ? reinterpret_cast<const uint64_t*>(hp + L.lab) : nullptr;
+    a.dtaint = (fl & jsp::kPatchTaint) ? reinterpret_cast<const uint32_t*>(hp + L.taint) : nullptr;
+    a.dfree = (fl & jsp::kPatchFree) ? reinterpret_cast<const uint32_t*>(hp + L.free) : nullptr;
+    a.dexcl = (fl & jsp::kPatchExcl) ? reinterpret_cast<const int32_t*>(hp + L.excl) : nullptr;
+    a.labels = e->labels.as<uint64_t>();
+    a.taints = e->taints.as<uint32_t>();
+    a.freer = e->freer.as<uint32_t>();
+    a.excl = e->excl.as<int32_t>();
+    a.counter = e->patch_ctr.as<unsigned long long>();
+    a.done = e->h_patch_done.as<uint32_t>();
+    a.seq = e->patch_seq;
     return JSP_OK;
 }
 
@@ -1944,11 +2077,53 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
     run_wake(e);  // an earlier patch's wake still queued: run it (that patch then goes to the service)
-    if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
-    if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
+    const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
+                        (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
+    // A patch small enough to ride in the next request's line, while the
+    // service is up: held back (a watch event's few rows; more of the same
+    // columns merge into it) and applied by the dispatcher from the request
+    // itself -- no staging read, no request of its own. Whatever else reads
+    // the rows first posts it alone and waits (patch_wait).
+    const bool small = n <= jsp::micro_rows_max(e->W, e->R);
+    bool micro = false;
+    if (small && e->patch_pending && e->patch_micro && e->patch_deferred && e->micro_fl == fl && svc_up(e))
+        micro = micro_merge(e, rows, n, labels, taints, free_res, excl_owner);  // same patch number: not sent yet
+    if (!micro) {
+        if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
+        if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
+    }
     e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     auto& v = e->svc;
+    if (!e->patch_ctr.p) {
+        if (int rc = use_engine_stream(e)) return rc;
+        HIP_TRY(e->patch_ctr.reserve(64));
+        HIP_TRY(hipMemsetAsync(e->patch_ctr.p, 0, 64, s));
+    }
+    if (!e->h_patch_done.p) {
+        HIP_TRY(e->h_patch_done.reserve(128));
+        std::memset(e->h_patch_done.p, 0, 128);
+    }
+    if (!micro && small && svc_up(e)) {
+        e->micro_n = 0;
+        e->micro_fl = fl;
+        micro = micro_merge(e, rows, n, labels, taints, free_res, excl_owner);  // fits: n <= the row capacity
+        if (micro) {
+            e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
+            e->patch_bits = 0u;  // the request's chunk 1 says it carries micro rows
+            e->patch_nf = 0u;
+            e->patch_req = 0;
+            e->patch_micro = e->patch_pending = e->patch_svc = e->patch_deferred = true;
+        }
+    }
+    if (micro) {
+        if (int rc = micro_stage_kernel_form(e)) return rc;
+        const auto t2 = std::chrono::steady_clock::now();
+        e->acc.patches += 1;
+        e->acc.patch_us += std::chrono::duration<double, std::micro>(t2 - t0).count();
+        return JSP_OK;
+    }
+    e->patch_micro = false;
     // Who applies it: the running service's dispatcher (posted at once; a
     // request that finds it not yet taken carries it again; whatever else
     // reads the rows first waits for it, patch_wait); after the service left,
@@ -1965,8 +2140,6 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     // W/R at snapshot upload); larger ones, and the patch kernel's, to the
     // engine's staging through a descriptor.
     const uint32_t W = e->W, R = e->R;
-    const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
-                        (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
     const bool inl = (up || wake) && n <= jsp::kPatchInlineRows && v.pstage.p &&
                      jsp::patch_inline_layout(jsp::kPatchInlineRows, 15u, W, R).bytes <= v.pstage.bytes;
     const jsp::PatchInlineLayout L = jsp::patch_inline_layout(n, inl ? fl : 15u, W, R);
@@ -1984,15 +2157,6 @@ int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const ui
     if (taints) std::memcpy(hp + L.taint, taints, (size_t)n * 4);
     if (free_res) std::memcpy(hp + L.free, free_res, (size_t)R * n * 4);
     if (excl_owner) std::memcpy(hp + L.excl, excl_owner, (size_t)n * 4);
-    if (!e->patch_ctr.p) {
-        if (int rc = use_engine_stream(e)) return rc;
-        HIP_TRY(e->patch_ctr.reserve(64));
-        HIP_TRY(hipMemsetAsync(e->patch_ctr.p, 0, 64, s));
-    }
-    if (!e->h_patch_done.p) {
-        HIP_TRY(e->h_patch_done.reserve(128));
-        std::memset(e->h_patch_done.p, 0, 128);
-    }
     e->patch_seq = e->patch_seq % 0x7FFFFFFFu + 1u;
     if (inl) __atomic_store_n(reinterpret_cast<uint32_t*>(hp), e->patch_seq, __ATOMIC_RELAXED);  // header
     jsp::PatchArgs a{};

@@ -208,8 +208,27 @@ __host__ __device__ inline PatchInlineLayout patch_inline_layout(uint32_t n, uin
     return L;
 }
 
+// The request line in pinned host memory (ServiceArgs::mailbox), read by the
+// dispatcher in one load of kMailboxChunks 16-byte chunks, each written by one
+// 16-byte host store and tagged with the request's seq (a torn read shows two
+// seqs and is read again):
+//   chunk 0 {seq, J | request bits, seq, n_runs (or an inline patch's n | flags << 16)}
+//   chunk 1 {seq, micro rows m, patch number, column flags}
+//   chunks 2.. {seq, 3 payload words}: m micro-patch rows of 3 + 2W + R words
+//     each {row, labels (u32 halves) [W], taint, free [R], excl} -- a patch
+//     small enough to ride in the request itself (no staging read)
+// A patch number equal to the one the dispatcher applied last is not applied
+// again (a request carrying a patch whose completion word had not come back).
+constexpr uint32_t kMailboxChunks = 8;
+constexpr uint32_t kMailboxPayload = 3 * (kMailboxChunks - 2);  // micro-patch words per request
+constexpr uint32_t kMailboxBytes = 16 * kMailboxChunks;
+__host__ __device__ constexpr uint32_t micro_row_words(uint32_t W, uint32_t R) { return 3u + 2u * W + R; }
+__host__ __device__ constexpr uint32_t micro_rows_max(uint32_t W, uint32_t R) {
+    return kMailboxPayload / micro_row_words(W, R);
+}
+
 struct ServiceArgs {
-    const unsigned long long* mailbox;  // host-mapped 16 B: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; [1] first
+    const unsigned long long* mailbox;  // host-mapped kMailboxBytes request line (above)
     unsigned long long* granules;       // [n_blocks] the service's own look-back granules (tag = seq)
     unsigned long long* bell;           // device word: the dispatcher's copy of the request word (sc1)
     uint32_t pods;

@@ -2986,75 +2986,146 @@ __device__ void service_apply_inline(const ServiceArgs& v, const TallyArgs& a, u
     if (threadIdx.x == 0) __hip_atomic_store(v.pdone, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// A micro-patch carried in the request line (jsp_internal.h kMailbox*): the
+// rows' words are already in LDS (s_w: m records of 3 + 2W + R words, row ids
+// distinct); one thread per word stores it (agent scope: the tiles' sc1
+// reloads find it in L2), every store drains, and thread 0 publishes the
+// patch number. No host-link round trip beyond the request's own.
+__device__ void service_apply_micro(const ServiceArgs& v, const TallyArgs& a, const uint32_t* s_w, uint32_t m,
+                                    uint32_t fl, uint32_t pseq) {
+    const uint32_t W = (uint32_t)a.W, R = (uint32_t)a.R, rw = 3u + 2u * W + R;
+    const uint32_t t = threadIdx.x;
+    if (t < m * rw) {
+        const uint32_t r = t / rw, k = t - r * rw;
+        const uint32_t row = s_w[r * rw], val = s_w[t];
+        if (k >= 1 && k <= 2u * W) {
+            if (fl & kPatchLab) {
+                uint32_t* lab =
+                    reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(a.labels) + (size_t)((k - 1) >> 1) * a.npad + row);
+                __hip_atomic_store(lab + ((k - 1) & 1u), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        } else if (k == 2u * W + 1u) {
+            if (fl & kPatchTaint)
+                __hip_atomic_store(const_cast<uint32_t*>(a.taints) + row, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (k < 2u * W + 2u + R) {
+            if (fl & kPatchFree)
+                __hip_atomic_store(const_cast<uint32_t*>(a.freer) + (size_t)(k - 2u * W - 2u) * a.npad + row, val,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (k == 2u * W + 2u + R) {
+            if (fl & kPatchExcl)
+                __hip_atomic_store(const_cast<int32_t*>(a.excl) + row, (int32_t)val, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(v.pdone, pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The dispatcher's LDS words (s_p): [0] claimed request seq [1] J word [2]
+// stop [3] second request word [4] micro rows [5] patch number [6] column
+// flags [7] last applied patch number [8 .. 8 + kMailboxPayload) micro words.
 __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const TallyArgs& a, uint32_t* s_p,
                                                  bool local = false) {
-    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t rw = 3u + 2u * (uint32_t)a.W + (uint32_t)a.R;  // words of a micro-patch row
     uint32_t seq = v.seq0;
     if (threadIdx.x == 0) {
         s_p[0] = 0;
         s_p[2] = 0;
+        s_p[7] = 0;  // patch numbers are never 0
         __hip_atomic_store(v.ready, v.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     __syncthreads();
-    unsigned long long* mb = const_cast<unsigned long long*>(v.mailbox);
+    const uint32_t* mb = reinterpret_cast<const uint32_t*>(v.mailbox);
     while (true) {
-        if ((threadIdx.x & 63) == 0) {
+        {
+            // every wave polls, the waves a quarter of the host-link round trip apart
             const uint64_t t0 = wall_clock64();
             while (wall_clock64() - t0 < (uint64_t)w * kSvcStaggerTicks) __builtin_amdgcn_s_sleep(1);
             while (true) {
                 if (__hip_atomic_load(s_p + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0 ||
                     __hip_atomic_load(s_p + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0)
                     break;
-                // the 16-byte request {seq, J, seq, n_runs} in one load (the host
-                // writes the second half first; a torn read shows two seqs)
-                uint4 x;
-                asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
-                             : "=v"(x) : "v"(mb) : "memory");
-                const uint32_t q = x.x;
+                // the request line in one load: lane c < kMailboxChunks reads
+                // 16-byte chunk c (each chunk carries the request's seq: a torn
+                // read shows two seqs)
+                uint4 x = make_uint4(0u, 0u, 0u, 0u);
+                if (lane < kMailboxChunks)
+                    asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                                 : "=v"(x) : "v"(mb + 4 * lane) : "memory");
+                const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)x.x, 0);
                 if (q == kSvcStop) {
-                    __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (lane == 0) __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
-                if (q != seq && q != 0 && x.z == q) {
-                    if ((x.y & kReqPatch) == 0u) {
-                        const unsigned long long m = ((unsigned long long)x.y << 32) | q;
-                        // ring at once (the first wave to see it; a second
-                        // ringer writes the same word)
-                        if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint32_t jw = (uint32_t)__builtin_amdgcn_readlane((int)x.y, 0);
+                const uint32_t z0 = (uint32_t)__builtin_amdgcn_readlane((int)x.z, 0);
+                const uint32_t w2 = (uint32_t)__builtin_amdgcn_readlane((int)x.w, 0);
+                const uint32_t tag1 = (uint32_t)__builtin_amdgcn_readlane((int)x.x, 1);
+                const uint32_t m = (uint32_t)__builtin_amdgcn_readlane((int)x.y, 1);
+                const uint32_t nch = m > 0u ? (m * rw + 2u) / 3u : 0u;  // payload chunks in use (3 words each)
+                const bool mine = lane >= 2u && lane < 2u + nch;
+                const bool torn = __ballot(mine && x.x != q) != 0ull;
+                if (q != seq && q != 0 && z0 == q && tag1 == q && !torn && 2u + nch <= kMailboxChunks) {
+                    // claim it (two waves may see it; one hands it on)
+                    uint32_t won = 0;
+                    if (lane == 0) won = atomicCAS(s_p + 0, 0u, q) == 0u ? 1u : 0u;
+                    if (__builtin_amdgcn_readlane((int)won, 0) == 0) break;
+                    const bool patch = (jw & kReqPatch) != 0u || m > 0u;
+                    if (!patch && lane == 0) {
+                        // ring at once: nothing to apply first
+                        const unsigned long long mm = ((unsigned long long)jw << 32) | q;
+                        if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    // a patch first: the whole workgroup applies it below, then
-                    // rings. The host learns that the request was taken (a later
-                    // request then need not carry the patch again).
-                    if (x.y & kReqPatch) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    __hip_atomic_store(s_p + 1, x.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_store(s_p + 3, x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_store(s_p + 0, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    // the host learns that a request with a patch was taken (a
+                    // later request then need not carry the patch again)
+                    if (patch && lane == 0) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (lane == 1) {
+                        s_p[1] = jw;
+                        s_p[3] = w2;
+                        s_p[4] = m;
+                        s_p[5] = x.z;  // patch number
+                        s_p[6] = x.w;  // column flags
+                    }
+                    if (mine) {
+                        s_p[8 + 3 * (lane - 2)] = x.y;
+                        s_p[9 + 3 * (lane - 2)] = x.z;
+                        s_p[10 + 3 * (lane - 2)] = x.w;
+                    }
                     break;
                 }
                 if (w == 0 && wall_clock64() - t0 > v.idle_ticks) {
-                    __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (lane == 0) __hip_atomic_store(s_p + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     break;
                 }
             }
         }
         __syncthreads();
-        const uint32_t q = s_p[0], jw = s_p[1], nr = s_p[3];
-        if (q == 0) {  // stop or idle: every tile leaves too
+        const uint32_t q = s_p[0], jw = s_p[1], nr = s_p[3], m = s_p[4], pseq = s_p[5], fl = s_p[6];
+        if (q == 0) {  // stop or idle: every tile leaves too (a request claimed beside an idle exit is answered first)
             if (threadIdx.x == 0)
                 __hip_atomic_store(v.bell, ((unsigned long long)v.gen << 32) | kSvcStop, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             return;
         }
-        if (jw & kReqPatch) {
-            // each ends with a barrier and the completion word
-            if (jw & kReqPatchInline) service_apply_inline(v, a, nr);
-            else service_apply_patch(v, a);
+        const bool patch = (jw & kReqPatch) != 0u || m > 0u;
+        if (patch) {
+            // a patch this dispatcher applied already (carried again by a
+            // request posted before its completion word came back) is not
+            // applied twice; each apply ends with a barrier and the completion word
+            if (pseq != s_p[7]) {
+                if (m > 0u) service_apply_micro(v, a, s_p + 8, m, fl, pseq);
+                else if (jw & kReqPatchInline) service_apply_inline(v, a, nr);
+                else service_apply_patch(v, a);
+                if (threadIdx.x == 0) s_p[7] = pseq;
+            }
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
-                const unsigned long long m =
+                const unsigned long long mm =
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
-                if (local) __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else __hip_atomic_store(v.bell, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         seq = q;
@@ -3716,7 +3787,8 @@ size_t compact_lds_bytes(uint32_t la) { return sizeof(uint32_t) * (tally_lds_wor
 uint32_t service_row_cache_words(uint32_t la) { return (uint32_t)((compact_lds_bytes(la) + 15) / 16 * 4); }
 
 size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache) {
-    if (!row_cache) return compact_lds_bytes(la);
+    // + the dispatcher's words past the compaction's (service_dispatch s_p: 8 + kMailboxPayload after s_x[16])
+    if (!row_cache) return compact_lds_bytes(la) + sizeof(uint32_t) * (8 + kMailboxPayload);
     return sizeof(uint32_t) * service_row_cache_words(la) + (size_t)(2 * W + 2 + R) * 16 * kTallyThreads;
 }
 

@@ -648,3 +648,65 @@ def test_wider_snapshot_then_inline_patch(svc_engine, idle):
         got = svc_engine.place(q.job_class)
         np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
     svc_engine.check()
+
+
+@pytest.mark.parametrize("then", ["place", "place_twice", "tally_launch", "stop", "sync", "upload", "big_patch"])
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_micro_patches_ride_in_the_request(svc_engine, cfg, then):
+    """Patches of a few rows while the service is up ride in the next
+    request's line (no staging read, no request of their own): consecutive
+    patches of the same columns merge (a row patched twice keeps the last
+    values), a patch of other columns or a larger one sends the held one
+    first, and whatever reads the rows next -- the next request, a launch
+    with tallies, a stop, a sync, an upload -- sees every patched column,
+    bit-exact."""
+    p = synth.CONFIGS[cfg]()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused in (3, 5)
+    rng = np.random.default_rng(cfg * 100 + len(then))
+    N, R = p.nodes.n_nodes, p.nodes.free.shape[0]
+    for step in range(8):
+        k = int(rng.integers(1, 4))
+        hot = int(rng.integers(0, N))
+        for _ in range(k):  # a few watch events, one row each (one row twice)
+            row = np.array([hot if rng.random() < 0.3 else int(rng.integers(0, N))], dtype=np.uint32)
+            if step % 3 == 2:
+                t = rng.integers(0, 2, size=1).astype(np.uint32)
+                svc_engine.patch_rows(row, taints=t)
+                p.nodes.taints[row] = t
+            else:
+                f = rng.integers(0, 200_000, size=(R, 1)).astype(np.uint32)
+                ex = np.where(rng.random(1) < 0.2, 4, -1).astype(np.int32)
+                svc_engine.patch_rows(row, free=f, excl=ex)
+                p.nodes.free[:, row] = f
+                p.nodes.excl[row] = ex
+        if then == "big_patch":
+            rows = np.sort(rng.choice(N, size=50, replace=False)).astype(np.uint32)
+            t = rng.integers(0, 2, size=50).astype(np.uint32)
+            svc_engine.patch_rows(rows, taints=t)
+            p.nodes.taints[rows] = t
+        a, cap, occ = O.place_c(p)
+        if then == "tally_launch":
+            got = svc_engine.place(p.job_class, want_tally=True)
+            np.testing.assert_array_equal(got.cap, cap)
+            np.testing.assert_array_equal(got.occ, occ)
+        elif then == "stop":
+            svc_engine.service_stop()
+            got = svc_engine.place(p.job_class)
+        elif then == "sync":
+            svc_engine.sync()
+            got = svc_engine.place(p.job_class)
+        elif then == "upload":
+            svc_engine.upload_snapshot(p.nodes)
+            got = svc_engine.place(p.job_class)
+        else:
+            got = svc_engine.place(p.job_class)
+            if then == "place_twice":
+                np.testing.assert_array_equal(got.assign, a)
+                got = svc_engine.place(p.job_class)
+        np.testing.assert_array_equal(got.assign, a)
+    got = svc_engine.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+    np.testing.assert_array_equal(got.occ, occ)
