@@ -312,8 +312,9 @@ def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
             gaps.append((t2 - t1) * 1e3)
             shapes[int(st.fused)] = shapes.get(int(st.fused), 0) + 1
         line = _pcts(tot)
-        line.update({"patch_p50_us": _pcts(pat)["p50_us"], "place_p50_us": _pcts(pla)["p50_us"],
-                     "place_p99_us": _pcts(pla)["p99_us"], "gap_ms_p50": round(float(np.median(gaps)), 3),
+        line.update({"patch_p50_us": _pcts(pat)["p50_us"], "patch_p99_us": _pcts(pat)["p99_us"],
+                     "place_p50_us": _pcts(pla)["p50_us"], "place_p99_us": _pcts(pla)["p99_us"],
+                     "gap_ms_p50": round(float(np.median(gaps)), 3),
                      "shapes": {str(k): v for k, v in sorted(shapes.items())}})
         out[f"gap_{gap:g}ms"] = line
     out["note"] = (f"service idle-exited (sleep {idle_ms + 10:.0f} ms), then a one-row patch (jsp_snapshot_patch) and, "
@@ -321,10 +322,60 @@ def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
     return out
 
 
-def cpu_cold_recovery(p, trials: int, threads, idle_ms: float):
-    """The same recovery on the CPU evaluator: after the same idle sleep, the
-    same one-row patch (written into the evaluator's columns), then one
-    placement; timed = patch + placement."""
+def cpu_cold_recovery(p, trials: int, threads, idle_ms: float, gaps_ms=COLD_GAPS_MS):
+    """The same recovery on the CPU evaluator, like for like with the GPU legs:
+    after the same idle sleep, the same one-row patch (written into the
+    evaluator's columns), the same gap (slept), then one placement; timed =
+    patch + placement, the gap excluded. Per gap, per thread count. (The
+    evaluator's pool threads spin between placements -- cpu_fast.c worker --
+    so its multi-thread legs start with hot workers: a CPU-favouring
+    baseline.)"""
+    from oracle import oracle as O
+    out = {}
+    for gap in gaps_ms:
+        legs = {}
+        for th in threads:
+            fc = O.FastCPU(th)
+            fc.prepare(p)
+            fc.run()
+            taints = fc.pk.arrs["taints"]
+            lat = []
+            for t in range(trials):
+                row = (t * 7919 + int(gap * 13)) % max(p.nodes.n_nodes, 1)
+                v = int(taints[row])
+                time.sleep((idle_ms + 10.0) * 1e-3)
+                t0 = time.perf_counter()
+                taints[row] = v
+                t1 = time.perf_counter()
+                if gap > 0:
+                    time.sleep(gap * 1e-3)
+                t2 = time.perf_counter()
+                fc.run()
+                t3 = time.perf_counter()
+                lat.append(((t1 - t0) + (t3 - t2)) * 1e6)
+            fc.close()
+            legs[f"{th}t"] = _pcts(lat)
+        out[f"gap_{gap:g}ms"] = legs
+    return out
+
+
+def cold_vs_cpu(cold, cpu):
+    """Per gap: the GPU cold p50/p99 beside the best like-for-like CPU leg's."""
+    out = {}
+    for g, legs in cpu.items():
+        if g not in cold:
+            continue
+        b50 = min(v["p50_us"] for v in legs.values())
+        b99 = min(v["p99_us"] for v in legs.values())
+        out[g] = {"gpu_p50_us": cold[g]["p50_us"], "gpu_p99_us": cold[g]["p99_us"], "best_cpu_p50_us": b50,
+                  "best_cpu_p99_us": b99, "p50_gpu_over_cpu_speedup": round(b50 / cold[g]["p50_us"], 3),
+                  "p99_gpu_over_cpu_speedup": round(b99 / cold[g]["p99_us"], 3)}
+    return out
+
+
+def cpu_patched_step(p, threads, seconds: float):
+    """The CPU counterpart of patched_step_us: one row written into the
+    evaluator's columns, then one placement, back to back (µs per step)."""
     from oracle import oracle as O
     out = {}
     for th in threads:
@@ -332,17 +383,16 @@ def cpu_cold_recovery(p, trials: int, threads, idle_ms: float):
         fc.prepare(p)
         fc.run()
         taints = fc.pk.arrs["taints"]
-        lat = []
-        for t in range(trials):
-            row = (t * 7919) % max(p.nodes.n_nodes, 1)
-            v = int(taints[row])
-            time.sleep((idle_ms + 10.0) * 1e-3)
-            t0 = time.perf_counter()
-            taints[row] = v
+        n, t0 = 0, time.perf_counter()
+        while True:
+            row = (n * 7919) % max(p.nodes.n_nodes, 1)
+            taints[row] = taints[row]
             fc.run()
-            lat.append((time.perf_counter() - t0) * 1e6)
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+        out[f"{th}t"] = round((time.perf_counter() - t0) * 1e6 / n, 2)
         fc.close()
-        out[f"{th}t"] = _pcts(lat)
     return out
 
 
@@ -497,6 +547,7 @@ def main() -> None:
     barrier(world)
     torch.cuda.synchronize()
     call()
+    eng.timing(reset=True)  # the library's own phase clocks of the timed calls (host side, always on)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         call()
@@ -505,6 +556,7 @@ def main() -> None:
     barrier(world)
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, world)
+    tphase = eng.timing(reset=True)
     placed = int((call.assign >= 0).sum())
     value = placed * args.steps * world / elapsed
 
@@ -532,6 +584,26 @@ def main() -> None:
     # from memory instead of their LDS copies); not the timed loop
     patched = round(patched_step_us(eng, p, max(200, args.steps * 5)), 3) if shape == 3 else None
     eng.service_stop()
+    # the host-link floor: host -> device -> host through pinned memory with
+    # the service's polling, and where the timed host-API step's time went
+    floor = eng.link_floor(2000) if rank == 0 else None
+    step_us = elapsed * 1e6 / args.steps
+    n_calls = max(int(tphase.host_calls), 1)
+    breakdown = None
+    if floor is not None and shape == 3:
+        pre = tphase.svc_pre_us / n_calls
+        ans = tphase.svc_answer_us / n_calls
+        lib_us = (tphase.host_prep_us + tphase.host_wait_us) / n_calls
+        dev = svc["request_us_device"] if svc else None
+        breakdown = {"host_api_step_us": round(step_us, 2), "library_us": round(lib_us, 2),
+                     "outside_library_us": round(step_us - lib_us, 2),
+                     "svc_pre_us": round(pre, 2), "svc_answer_us": round(ans, 2),
+                     "link_floor_p50_us": round(floor[0], 2), "device_request_us": dev,
+                     "answer_beyond_floor_and_device_us": round(ans - floor[0] - dev, 2) if dev else None,
+                     "note": "means over the timed calls (jsp_timing, host clock): svc_pre = library entry of the "
+                             "service path to the request post, svc_answer = post to the answer's last entry; the "
+                             "floor is jsp_engine_link_floor's median round trip; device_request = the service's "
+                             "in-kernel request time (stamps on, a separate leg)"}
 
     # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
     step, out = device_step(p)
@@ -584,15 +656,22 @@ def main() -> None:
     idle_ms = float(os.environ.get("JSP_SERVICE_IDLE_MS", "50"))
     if cold2 is not None and world == 1 and args.cpu_seconds > 0:
         cold2["cpu"] = cpu_cold_recovery(p, max(10, args.cold_trials // 2), sorted({1, 2, cpu_threads()}), idle_ms)
-        cold2["cpu_note"] = ("oracle/cpu_fast.c after the same idle sleep: the same one-row patch written into its "
-                             "columns, then one placement; timed = patch + placement")
-        best = min(v["p99_us"] for v in cold2["cpu"].values())
-        cold2["gpu_p99_over_best_cpu_p99"] = {k: round(best / v["p99_us"], 3) for k, v in cold2.items()
-                                              if k.startswith("gap_")}
+        cold2["cpu_note"] = ("oracle/cpu_fast.c like for like: the same idle sleep, the same one-row patch written into "
+                             "its columns, the same slept gap, then one placement; timed = patch + placement, the gap "
+                             "excluded")
+        cold2["vs_cpu"] = cold_vs_cpu(cold2, cold2["cpu"])
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
     cpu = None
     T = cpu_threads()
+    cpu_patched = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0 and patched is not None:
+        legs_p = cpu_patched_step(p, sorted({1, 2, T}), min(2.0, args.cpu_seconds / 6))
+        best_p = min(legs_p.values())
+        cpu_patched = {"legs_us": legs_p, "best_us": best_p, "gpu_patched_step_us": patched,
+                       "gpu_over_best_cpu": round(best_p / patched, 3),
+                       "note": "oracle/cpu_fast.c: the same one-row write into its columns, then one placement, "
+                               "back to back (the CPU side of patched_step_us)"}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle import oracle as O
         legs = []
@@ -667,8 +746,9 @@ def main() -> None:
                 line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
                 line["host_api_cold_recovery"] = cold_recovery_latency(eng, pc, args.cold_trials // 2)
                 if line["host_api_cold_recovery"] is not None and world == 1 and args.cpu_seconds > 0:
-                    line["host_api_cold_recovery"]["cpu"] = cpu_cold_recovery(
-                        pc, max(10, args.cold_trials // 4), sorted({1, 2, T}), idle_ms)
+                    cc = line["host_api_cold_recovery"]
+                    cc["cpu"] = cpu_cold_recovery(pc, max(10, args.cold_trials // 4), sorted({1, 2, T}), idle_ms)
+                    cc["vs_cpu"] = cold_vs_cpu(cc, cc["cpu"])
             eng.service_stop()
             if world == 1 and args.cpu_seconds > 0:
                 from oracle import oracle as O
@@ -839,11 +919,18 @@ def main() -> None:
                          "LDS between requests (no row traffic); patched_step_us times one row patched before "
                          "each call (rows reloaded from memory)",
             "patched_step_us": patched,
+            "cpu_patched_step": cpu_patched,
+            "host_link_floor_us": {"p50": round(floor[0], 2), "p99": round(floor[1], 2), "mean": round(floor[2], 2)}
+            if floor else None,
+            "host_api_breakdown": breakdown,
             "p50_recovery_us": lat2["p50_us"] if lat2 else None,
             "p99_recovery_us": lat2["p99_us"] if lat2 else None,
             "p99_recovery_leg": "warm: 1000 seeded trial snapshots, each uploaded untimed (the upload restarts the "
                                 "service and returns once it polls), then jsp_place on host wall; the realistic "
                                 "cold recovery is cold_recovery",
+            "p99_cold_recovery_us": {g: v["p99_us"] for g, v in cold2.items() if g.startswith("gap_")} if cold2 else None,
+            "p99_cold_recovery_best_cpu_us": {g: v["best_cpu_p99_us"] for g, v in cold2.get("vs_cpu", {}).items()}
+            if cold2 else None,
             "recovery_trials": lat2["n"] if lat2 else 0,
             "cold_recovery": cold2,
             "cpu_baseline": cpu,

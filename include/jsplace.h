@@ -313,6 +313,13 @@ int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
 int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
                            uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub,
                            size_t scrub_bytes, double* out_us);
+/* The host-link floor (ABI v6): `iters` host -> device -> host round trips
+ * through pinned memory with the resident service's polling (four device
+ * waves a quarter of a round trip apart poll a request word; the first to
+ * see request i writes an ack the host spins on). out_us[0] median, [1]
+ * p99, [2] mean, microseconds. Every host-API request pays this at least
+ * once; the bench reports it beside the host-API latency. */
+int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

@@ -2583,6 +2583,53 @@ int jsp_engine_service_stop(jsp_engine* e) {
     return svc_stop(e);
 }
 
+int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us) {
+    if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: probe a shard engine");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (iters == 0 || iters > 100000) return set_err(JSP_EINVAL, "iters %u out of range [1,100000]", iters);
+    if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
+    HostBuf box;
+    HIP_TRY(box.reserve(512));
+    uint32_t* req = box.as<uint32_t>();
+    uint32_t* ack = req + 32;  // four ack words, 64 B apart, on lines of their own
+    std::memset(box.p, 0, 512);
+    hipStream_t s = e->stream;
+    if (int rc = use_engine_stream(e)) return rc;
+    const uint32_t warm = std::min<uint32_t>(50, iters);
+    const uint32_t n = iters + warm;
+    HIP_TRY(jsp::launch_link_probe(req, ack, n, 100000000ull, s));  // a wave waits <= 1 s per request
+    auto acked = [&](uint32_t i) {
+        for (int w = 0; w < 4; ++w)
+            if (__atomic_load_n(ack + 16 * w, __ATOMIC_ACQUIRE) >= i) return true;
+        return false;
+    };
+    std::vector<double> us;
+    us.reserve(iters);
+    int rc = JSP_OK;
+    for (uint32_t i = 1; i <= n && rc == JSP_OK; ++i) {
+        const auto t0 = std::chrono::steady_clock::now();
+        __atomic_store_n(req, i, __ATOMIC_RELEASE);
+        while (!acked(i)) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(500)) {
+                rc = set_err(JSP_EHIP, "host-link probe: request %u not answered within 500 ms", i);
+                break;
+            }
+        }
+        if (i > warm) us.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    if (rc != JSP_OK) __atomic_store_n(req, n, __ATOMIC_RELEASE);  // let every wave finish
+    HIP_TRY(hipStreamSynchronize(s));
+    if (rc != JSP_OK) return rc;
+    std::sort(us.begin(), us.end());
+    double sum = 0;
+    for (double x : us) sum += x;
+    out_us[0] = us[us.size() / 2];
+    out_us[1] = us[std::min(us.size() - 1, (size_t)(0.99 * us.size()))];
+    out_us[2] = sum / us.size();
+    return JSP_OK;
+}
+
 int jsp_engine_set_timing(jsp_engine* e, int enable) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 2, enable); }

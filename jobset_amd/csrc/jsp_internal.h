@@ -320,6 +320,9 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 void set_launch_stop(hipEvent_t ev);
 void set_launch_start(hipEvent_t ev);  // the next launch's start event (then cleared)
 bool launch_stop_used();
+// host-link floor probe (instrumentation): four polling waves answer request
+// numbers 1..n of *req in ack[16 w] (pinned host memory)
+hipError_t launch_link_probe(const uint32_t* req, uint32_t* ack, uint32_t n, uint64_t wait_ticks, hipStream_t s);
 // read-only cache scrub of `bytes` (instrumentation: cold-cache timings)
 hipError_t launch_scrub(const void* p, size_t bytes, uint32_t* sink, hipStream_t s);
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);

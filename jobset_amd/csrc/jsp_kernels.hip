@@ -3605,6 +3605,32 @@ __global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst
         dst[i] += src[i];
 }
 
+// ----------------------------------------------------------------- host-link floor (instrumentation)
+// jsp_engine_link_floor: the dispatcher's polling alone -- lane 0 of four
+// waves a quarter of a round trip apart, system-scope loads of one request
+// word in pinned host memory -- answering request number i with an ack word
+// of its own in pinned memory, which the host spins on: the host -> device ->
+// host round trip every host-API request pays at least once. Every wave gives
+// up after wait_ticks without a request, so the grid always drains.
+__global__ __launch_bounds__(256) void link_probe_kernel(const uint32_t* req, uint32_t* ack, uint32_t n,
+                                                         uint64_t wait_ticks) {
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (lane != 0) return;
+    const uint64_t ts = wall_clock64();
+    while (wall_clock64() - ts < (uint64_t)w * kSvcStaggerTicks) __builtin_amdgcn_s_sleep(1);
+    for (uint32_t i = 1; i <= n; ++i) {
+        const uint64_t t0 = wall_clock64();
+        uint32_t q = 0;
+        while (true) {
+            asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(q) : "v"(req) : "memory");
+            if (q >= i) break;
+            if (wall_clock64() - t0 > wait_ticks) return;
+        }
+        i = q;
+        __hip_atomic_store(ack + 16u * w, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // ----------------------------------------------------------------- cache scrub (instrumentation)
 // Reads n16 16-byte words (a buffer larger than the Infinity Cache), so the
 // next launch finds its bytes in HBM only; nothing is dirtied. The sum goes
@@ -3936,6 +3962,11 @@ hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStrea
     if (n == 0) return hipSuccess;
     const size_t blocks = std::min<size_t>(1024, (n / 4 + 255) / 256 + 1);
     jsp_launch(add_u32_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, src, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_link_probe(const uint32_t* req, uint32_t* ack, uint32_t n, uint64_t wait_ticks, hipStream_t s) {
+    jsp_launch(link_probe_kernel, dim3(1), dim3(256), 0, s, req, ack, n, wait_ticks);
     return hipGetLastError();
 }
 

@@ -255,6 +255,13 @@ class Engine:
                                                scrub or None, scrub_bytes, _p(out)))
         return float(out[0]), float(out[1])
 
+    def link_floor(self, iters: int = 2000) -> Tuple[float, float, float]:
+        """Host -> device -> host round trip through pinned memory with the
+        resident service's polling (jsp_engine_link_floor): (p50, p99, mean) us."""
+        out = np.zeros(3, dtype=np.float64)
+        check(self._lib.jsp_engine_link_floor(self._h, int(iters), _p(out)))
+        return float(out[0]), float(out[1]), float(out[2])
+
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
