@@ -799,6 +799,12 @@ def main() -> None:
         tally_med, tally_mean = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, tally_loop)
         tally_loop_us = event_loop_us(tally_fn, tally_loop, stream)
         tally_us = tally_mean
+        # a third, tracer-free measure: the kernel's own span (first wave start
+        # -> last wave end, device clock stamps per wave; jsp_tally_device_spans)
+        try:
+            span_med, span_mean = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(), L4, tally_loop)
+        except Exception:  # noqa: BLE001 -- another tally shape (sharded ranks): no span
+            span_med = span_mean = None
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
         # cold: the library's read-only sweep of the 512 MiB buffer before each launch, dispatch events
@@ -819,6 +825,16 @@ def main() -> None:
                         "note": "device span of one three-launch step (first dispatch start -> last dispatch end, "
                                 "dispatch-packet events, engine stream)"}
             del rc4t, rl4t, a4t
+        host_step = None
+        if world == 1:  # the same step through the host API (jsp_place: run list in, assign[] back in host memory)
+            call4 = eng.host_placer(*job_runs(p4.job_class))
+            for _ in range(5):
+                call4()
+            t0h = time.perf_counter()
+            for _ in range(steps4):
+                call4()
+            host_step = round((time.perf_counter() - t0h) * 1e6 / steps4, 2)
+            assert np.array_equal(call4.assign, sp.assign()), "host API differs from the device path on cfg4"
         copy_ceiling = None
         if world == 1:  # achievable streaming rate: a cold copy of the same byte count
             src = torch.empty(tb4 // 2 // 16 * 4, dtype=torch.int32, device="cuda").fill_(1)
@@ -854,6 +870,12 @@ def main() -> None:
                 "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
                 "placed": placed4, "tally_us": round(tally_us, 2), "tally_median_us": round(tally_med, 2),
                 "tally_event_loop_us": round(tally_loop_us, 2),
+                "tally_span_us": round(span_mean, 2) if span_mean else None,
+                "tally_span_median_us": round(span_med, 2) if span_med else None,
+                "tally_span_vs_events": round(span_mean / tally_mean, 3) if span_mean else None,
+                "tally_measure": "tally_us (events on the dispatch packets); tally_span_us is the kernel's own "
+                                 "first-wave-start -> last-wave-end span from per-wave clock stamps (no tracer, no "
+                                 "dispatch overhead), reported beside it as the cross-check",
                 "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
                               "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
                               "around 200 ctypes-issued launches (includes host submit gaps)",
@@ -867,6 +889,7 @@ def main() -> None:
                              "median of the dispatch-packet events; cold_dirty: torch writes the buffer before each "
                              "launch (events around it), so the launch's misses pay its write-backs",
                 "step_device": step_dev,
+                "host_api_step_us": host_step,
                 "copy_ceiling_same_bytes": copy_ceiling,
                 "tally_traffic": pmc_traffic(("tally_wave",), 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
@@ -879,6 +902,8 @@ def main() -> None:
         barrier(world)
         if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
             cfg4["device_set"] = device_set_leg(p4, sp.assign(), max(20, args.steps))
+            if host_step and "us_per_step" in cfg4["device_set"]:
+                cfg4["device_set"]["over_single_device_host_api"] = round(cfg4["device_set"]["us_per_step"] / host_step, 3)
             torch.cuda.set_device(local)  # the rank's own device for the barrier (the library restores it too)
         barrier(world)
 

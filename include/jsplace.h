@@ -320,6 +320,15 @@ int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uin
  * p99, [2] mean, microseconds. Every host-API request pays this at least
  * once; the bench reports it beside the host-API latency. */
 int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us);
+/* The tally's in-kernel span (ABI v6): `iters` back-to-back launches of the
+ * one-tile wave tally with per-wave stamps of the device's 100 MHz clock
+ * (every wave's start, and its end once its stores drained); per launch the
+ * span from the first wave's start to the last wave's end -- a third measure
+ * beside the dispatch-packet events and a kernel trace, with no tracer and no
+ * dispatch overhead in it. out_us[0] median, [1] mean. JSP_ESTATE when the
+ * snapshot's tally runs another shape. */
+int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+                           double* out_us);
 int jsp_engine_set_timing(jsp_engine* e, int enable);
 int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
 void* jsp_engine_stream(jsp_engine* e);

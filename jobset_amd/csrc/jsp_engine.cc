@@ -600,10 +600,9 @@ uint32_t tally_wave_grid(jsp_engine* e) {
 // Whether the wave tally can fold the feasibility words into itself (the
 // three-launch shape on the engine's own unsharded tallies): at most 4
 // classes (one wave pass), all at the leaf level, wave tiles available.
-bool fold_ok(jsp_engine* e) {
-    if (e->C < 1 || e->C > 4 || e->n_wtiles == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total ||
-        e->hooks.tally_block)
-        return false;
+bool fold_ok(jsp_engine* e, bool shard = false) {
+    if (e->C < 1 || e->C > 4 || e->n_wtiles == 0 || e->hooks.tally_block) return false;
+    if (!shard && (e->leaf_begin != 0 || e->n_leaves != e->L_total)) return false;
     for (const auto& c : e->cls_h)
         if (c.level + 1 != e->K) return false;
     return (uint64_t)(e->C + 1) * e->L_total * 4 < (1ull << 31);
@@ -611,10 +610,14 @@ bool fold_ok(jsp_engine* e) {
 
 // The tally alone (three-launch shape, jsp_tally_device): the wave-tile
 // kernel when every leaf fits a wave tile, else the workgroup-block kernel.
-int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s, bool fold = false) {
+// fold_feas (null: none): the wave tally sets the leaf classes' feasibility
+// words there (fold_ok's shape; a shard of a device set folds into the words
+// of the set's assigning engine)
+int tally_impl(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, hipStream_t s,
+               uint64_t* fold_feas = nullptr) {
     jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
-    if (fold) {
-        a.feas_fold = e->feas.as<uint64_t>();
+    if (fold_feas) {
+        a.feas_fold = fold_feas;
         a.fold_nw = (e->L_total + 63) / 64;
     }
     if (e->n_blocks == 0) return JSP_OK;
@@ -788,7 +791,9 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
     e->last_shape = fused_ok(e) ? 1 : 0;
     if (e->last_shape == 0) {
         const bool fold = fold_ok(e);
-        if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s, fold)) return rc;
+        if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s,
+                                fold ? e->feas.as<uint64_t>() : nullptr))
+            return rc;
         return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_run_class, d_run_len,
                            n_runs, J, d_assign, s, fold);
     }
@@ -2331,6 +2336,49 @@ int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
                       [&](hipStream_t s) { return tally_impl(e, d_cap, d_occ, ld, s); });
 }
 
+int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+                           double* out_us) {
+    if (int rc = check_engine(e)) return rc;
+    if (e->multi) return set_err(JSP_ESTATE, "device-set engine: time its shard engines");
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (!d_occ || (e->C > 0 && !d_cap)) return set_err(JSP_EINVAL, "output buffer is NULL");
+    if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    if (iters == 0 || iters > 1024) return set_err(JSP_EINVAL, "iters %u out of range [1,1024]", iters);
+    if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
+    if (e->n_wtiles == 0 || e->C < 1 || e->C > 4 || tally_wave_grid(e) != 0 || e->hooks.tally_block)
+        return set_err(JSP_ESTATE, "the span probe times the one-tile wave tally; this snapshot runs another shape");
+    if (int rc = check_launch_error(e)) return rc;
+    hipStream_t s = e->stream;
+    if (int rc = use_engine_stream(e)) return rc;
+    const size_t per = (size_t)2 * e->n_wtiles;
+    DevBuf st;
+    HIP_TRY(st.reserve(per * iters * 8));
+    for (uint32_t i = 0; i < iters; ++i) {
+        jsp::TallyArgs a = tally_args(e, d_cap, d_occ, ld);
+        a.wstamps = st.as<unsigned long long>() + per * i;
+        HIP_TRY(jsp::launch_tally_wave(a, e->wtiles.as<uint4>(), e->n_wtiles, e->n_leaves, 0, s));
+    }
+    std::vector<unsigned long long> h(per * iters);
+    HIP_TRY(hipMemcpyAsync(h.data(), st.p, per * iters * 8, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    std::vector<double> us(iters);
+    double sum = 0.0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        unsigned long long lo = ~0ull, hi = 0;
+        for (size_t k = 0; k < per; k += 2) {
+            lo = std::min(lo, h[per * i + k]);
+            hi = std::max(hi, h[per * i + k + 1]);
+        }
+        us[i] = (double)(hi - lo) / 100.0;  // 100 MHz ticks
+        sum += us[i];
+    }
+    std::sort(us.begin(), us.end());
+    out_us[0] = us[iters / 2];
+    out_us[1] = sum / iters;
+    return check_launch_error(e);
+}
+
 int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
                            uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub, size_t scrub_bytes,
                            double* out_us) {
@@ -2582,6 +2630,52 @@ int jsp_engine_service_stop(jsp_engine* e) {
     e->wake_job = false;   // nor a wake still queued (its patch lands through patch_wait)
     return svc_stop(e);
 }
+
+}  // extern "C"
+
+// ---- internal entry points of the device-set engine (jsp_multi.h)
+bool jspi_fold_ok(jsp_engine* e) {
+    std::lock_guard<std::mutex> g(e->mu);
+    return e->have_cls && e->have_snap && fold_ok(e, true);
+}
+
+uint64_t* jspi_feas(jsp_engine* e, uint32_t* words) {
+    std::lock_guard<std::mutex> g(e->mu);
+    if (words) *words = e->feas_words;
+    return e->feas.as<uint64_t>();
+}
+
+int jspi_tally(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint64_t* fold_feas) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (ld < e->L_total) return set_err(JSP_EINVAL, "ld %u < total leaves %u", ld, e->L_total);
+    if (fold_feas && !fold_ok(e, true)) return set_err(JSP_ESTATE, "this shard cannot fold its feasibility");
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, e->stream)) return rc;
+    const int rc = tally_impl(e, d_cap, d_occ, ld, e->stream, fold_feas);
+    if (int lr = leave_stream(e, e->stream)) return lr;
+    return rc;
+}
+
+int jspi_assign(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld, const uint32_t* run_class,
+                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, bool folded) {
+    if (int rc = check_engine(e)) return rc;
+    std::lock_guard<std::mutex> g(e->mu);
+    if (int rc = ready(e, true)) return rc;
+    if (int rc = check_launch_error(e)) return rc;
+    if (int rc = enter_stream(e, e->stream)) return rc;
+    const int rc = assign_impl(e, d_cap, d_occ, ld, run_class, run_len, n_runs, J, assign, e->stream, folded);
+    if (int lr = leave_stream(e, e->stream)) return lr;
+    return rc;
+}
+
+int jspi_check(jsp_engine* e) {
+    std::lock_guard<std::mutex> g(e->mu);
+    return check_launch_error(e);
+}
+
+extern "C" {
 
 int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us) {
     if (int rc = check_engine(e)) return rc;

@@ -78,6 +78,10 @@ struct TallyArgs {
     // range, then an OR of its bits), so no feasibility launch follows. Null: off.
     uint64_t* feas_fold;
     uint32_t fold_nw;
+    // In-kernel span of the one-tile wave tally (jsp_tally_device_spans):
+    // lane 0 of every wave stores {its start, its end after its stores
+    // drained} (100 MHz clock) at [2 t, 2 t + 1] for wave tile t. Null: off.
+    unsigned long long* wstamps;
 };
 
 // Single-launch kernels run an oversubscribed grid (n_blocks + kSpareBlocks

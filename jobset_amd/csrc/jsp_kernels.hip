@@ -916,6 +916,7 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave1_kernel(TallyArgs a,
 #else
     const uint4 bt = tiles[t];
 #endif
+    const uint64_t t_in = a.wstamps ? wall_clock64() : 0ull;
     const JSP_CONST DevClass* k_cls = (const JSP_CONST DevClass*)(a.cls + a.c0);
     JSP_LDS uint32_t* s_pre = lds_ptr(lds + wid * nv * kWaveTileRows);
     const WaveRsrc rs{make_rsrc(a.labels, (uint32_t)W * a.npad * 8u), make_rsrc(a.taints, a.npad * 4u),
@@ -929,6 +930,13 @@ __global__ __launch_bounds__(kTallyThreads) void tally_wave1_kernel(TallyArgs a,
     wave_eval<W, R, NV>(a, k_cls, s_pre, bt, lane, A, sums);
     wave_store<NV>(a, cap_r, occ_r, bt, lane, sums);
     if (a.feas_fold) wave_fold<NV>(a, k_cls, bt, lane, sums);
+    if (a.wstamps) {  // the span probe: this wave's start and end (its stores drained)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+            a.wstamps[2 * t] = t_in;
+            a.wstamps[2 * t + 1] = wall_clock64();
+        }
+    }
 }
 
 // ----------------------------------------------------------------- feasibility
@@ -2998,7 +3006,9 @@ __device__ void service_apply_micro(const ServiceArgs& v, const TallyArgs& a, co
     if (t < m * rw) {
         const uint32_t r = t / rw, k = t - r * rw;
         const uint32_t row = s_w[r * rw], val = s_w[t];
-        if (k >= 1 && k <= 2u * W) {
+        if (k == 0u || row >= a.npad) {
+            // the row id itself
+        } else if (k <= 2u * W) {
             if (fl & kPatchLab) {
                 uint32_t* lab =
                     reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(a.labels) + (size_t)((k - 1) >> 1) * a.npad + row);

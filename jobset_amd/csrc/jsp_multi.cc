@@ -29,7 +29,7 @@ typedef int (*AllReduceFn)(const void*, void*, size_t, int, int, ncclComm_t, hip
 typedef int (*GroupFn)();
 typedef int (*DestroyFn)(ncclComm_t);
 typedef const char* (*ErrStrFn)(int);
-constexpr int kNcclInt32 = 2, kNcclSum = 0;
+constexpr int kNcclInt32 = 2, kNcclUint64 = 5, kNcclSum = 0;
 
 struct Rccl {
     void* so = nullptr;
@@ -112,6 +112,27 @@ struct DevMem {
     T* as() const { return static_cast<T*>(p); }
 };
 
+// pinned, device-mapped host memory (run lists in, assign[] out: the kernels
+// read and write it in place, no copy launches)
+struct PinMem {
+    void* p = nullptr;
+    size_t bytes = 0;
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    hipError_t reserve(size_t n) {
+        if (p && n <= bytes) return hipSuccess;
+        release();
+        hipError_t e = hipHostMalloc(&p, n ? n : 16, hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) bytes = n ? n : 16;
+        return e;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
 }  // namespace
 
 struct Multi {
@@ -132,11 +153,20 @@ struct Multi {
     // snapshot partition
     uint32_t N = 0, W = 0, R = 0;
     std::vector<uint32_t> r0, r1;      // per shard: global row range
-    std::vector<DevMem> local;         // per shard: its [C+1][L] tallies (zero outside its columns)
-    std::vector<DevMem> red;           // per group: the combined tallies
-    DevMem d_runs, d_assign;           // on shard 0's device
-    std::vector<int32_t> h_assign;
+    // per group: its shards' [C+1][L] tallies, each shard writing only its own
+    // leaf columns (every other column stays zero); with several devices the
+    // all-reduce sums them into `sum` (out of place: `red` keeps its zeros)
+    std::vector<DevMem> red, sum;
+    // folded feasibility (every class at the leaf level, <= 4 classes): per
+    // group its shards' bits of the [C][ceil(L/64)] words (zero elsewhere);
+    // one device: the assigning engine's own words, no all-reduce
+    bool fold = false;
+    bool leaf_classes = false;
+    std::vector<DevMem> fl_local, fl_sum;
+    PinMem h_runs, h_assign;           // run list in, assign[] out (pinned)
 };
+
+int reset_buffers(Multi* m);
 
 int create(const int* ids, int n, Multi** out) {
     *out = nullptr;
@@ -171,7 +201,9 @@ int create(const int* ids, int n, Multi** out) {
         m->group_of.push_back(g);
     }
     m->red.resize(m->gdev.size());
-    m->local.resize(n);
+    m->sum.resize(m->gdev.size());
+    m->fl_local.resize(m->gdev.size());
+    m->fl_sum.resize(m->gdev.size());
     if (m->gdev.size() > 1) {
         if (int rc = load_rccl(&m->rccl)) {
             destroy(m);
@@ -199,10 +231,10 @@ void destroy(Multi* m) {
         (void)hipSetDevice(m->dev[i]);
         (void)hipEventDestroy(m->ev[i]);
     }
-    for (auto& b : m->local) b.release();
-    for (auto& b : m->red) b.release();
-    m->d_runs.release();
-    m->d_assign.release();
+    for (auto* v : {&m->red, &m->sum, &m->fl_local, &m->fl_sum})
+        for (auto& b : *v) b.release();
+    m->h_runs.release();
+    m->h_assign.release();
     for (jsp_engine* e : m->sh) jsp_engine_destroy(e);
     delete m;
 }
@@ -303,13 +335,35 @@ int snapshot_upload(Multi* m, const jsp_nodes* nd) {
     m->W = W;
     m->R = R;
     m->have_snap = true;
-    if (m->have_cls) {  // new leaf columns per shard: zero the tally buffers again
-        for (int s = 0; s < m->n; ++s) {
-            MHIP(hipSetDevice(m->dev[s]));
-            MHIP(hipMemset(m->local[s].p, 0, m->local[s].bytes));
+    if (m->have_cls) MTRY(reset_buffers(m));  // new leaf columns per shard
+    return JSP_OK;
+}
+
+// The per-group buffers for the current snapshot and classes, zeroed: every
+// shard rewrites only its own columns and feasibility bits, so the others
+// stay zero from here on. The fold is on when every shard can fold.
+int reset_buffers(Multi* m) {
+    const size_t words = (size_t)(m->C + 1) * std::max<uint32_t>(m->L, 1);
+    m->fold = m->leaf_classes;
+    for (jsp_engine* e : m->sh) m->fold = m->fold && jspi_fold_ok(e);
+    uint32_t fw = 0;
+    uint64_t* f0 = jspi_feas(m->sh[0], &fw);
+    const bool multi = m->gdev.size() > 1;
+    for (size_t k = 0; k < m->gdev.size(); ++k) {
+        MHIP(m->red[k].reserve(m->gdev[k], words * 4));
+        MHIP(hipMemset(m->red[k].p, 0, words * 4));
+        if (multi) MHIP(m->sum[k].reserve(m->gdev[k], words * 4));
+        if (m->fold && multi) {
+            MHIP(m->fl_local[k].reserve(m->gdev[k], (size_t)std::max<uint32_t>(fw, 1) * 8));
+            MHIP(hipMemset(m->fl_local[k].p, 0, m->fl_local[k].bytes));
+            if (k != (size_t)m->group_of[0]) MHIP(m->fl_sum[k].reserve(m->gdev[k], (size_t)std::max<uint32_t>(fw, 1) * 8));
         }
     }
-    return JSP_OK;
+    if (m->fold && !multi) {  // the shards fold straight into the assigning engine's words
+        MHIP(hipSetDevice(m->dev[0]));
+        MHIP(hipMemset(f0, 0, (size_t)std::max<uint32_t>(fw, 1) * 8));
+    }
+    return JSP_OK;  // hipMemset returns once the bytes are set (no device-wide wait: a resident service runs)
 }
 
 // the shard holding global row `row` (r0 ascending; empty shards skipped)
@@ -358,13 +412,10 @@ int classes_upload(Multi* m, const jsp_job_class* classes, uint32_t C) {
     m->have_cls = false;
     for (jsp_engine* e : m->sh) MTRY(jsp_classes_upload(e, classes, C));
     m->C = C;
-    const size_t words = (size_t)(C + 1) * std::max<uint32_t>(m->L, 1);
-    for (int s = 0; s < m->n; ++s) {
-        MHIP(m->local[s].reserve(m->dev[s], words * 4));
-        MHIP(hipMemset(m->local[s].p, 0, words * 4));
-    }
-    for (size_t k = 0; k < m->gdev.size(); ++k) MHIP(m->red[k].reserve(m->gdev[k], words * 4));
+    m->leaf_classes = C >= 1;
+    for (uint32_t c = 0; c < C; ++c) m->leaf_classes &= classes[c].level + 1 == m->K;
     m->have_cls = true;
+    if (m->have_snap) MTRY(reset_buffers(m));
     return JSP_OK;
 }
 
@@ -386,31 +437,41 @@ int place(Multi* m, const uint32_t* run_class, const uint32_t* run_len, uint32_t
     if (J > 0 && !assign_out) return jsp_internal_set_err(JSP_EINVAL, "assign_out is NULL");
     const uint32_t L = m->L, C = m->C;
     const size_t words = (size_t)(C + 1) * L;
-    // 1. every shard tallies its leaf columns on its own stream
+    const bool multi = m->gdev.size() > 1;
+    const int g0 = m->group_of[0];
+    uint32_t fw = 0;
+    uint64_t* f0 = jspi_feas(m->sh[0], &fw);
+    // 1. every shard tallies straight into its device's buffer (its own leaf
+    //    columns) on its own stream -- shards of one device run side by side
+    //    -- folding its leaves' feasibility bits when every class is a leaf class
     for (int s = 0; s < m->n; ++s) {
-        uint32_t* b = m->local[s].as<uint32_t>();
-        MTRY(jsp_tally_device(m->sh[s], b, b + (size_t)C * L, L, jsp_engine_stream(m->sh[s])));
+        const int k = m->group_of[s];
+        uint32_t* b = m->red[k].as<uint32_t>();
+        uint64_t* fb = !m->fold ? nullptr : multi ? m->fl_local[k].as<uint64_t>() : f0;
+        MTRY(jspi_tally(m->sh[s], b, b + (size_t)C * L, L, fb));
     }
-    // 2. per device: the group's sum into its combined buffer, on the leader's stream
-    for (size_t k = 0; k < m->gdev.size(); ++k) {
-        const int lead = m->glead[k];
-        hipStream_t ls = static_cast<hipStream_t>(jsp_engine_stream(m->sh[lead]));
-        MHIP(hipSetDevice(m->gdev[k]));
-        MHIP(hipMemcpyAsync(m->red[k].p, m->local[lead].p, words * 4, hipMemcpyDeviceToDevice, ls));
-        for (int s = 0; s < m->n; ++s) {
-            if (m->group_of[s] != (int)k || s == lead) continue;
-            MHIP(hipEventRecord(m->ev[s], static_cast<hipStream_t>(jsp_engine_stream(m->sh[s]))));
-            MHIP(hipStreamWaitEvent(ls, m->ev[s], 0));
-            MHIP(jsp::launch_add_u32(m->red[k].as<uint32_t>(), m->local[s].as<uint32_t>(), words, ls));
-        }
+    // 2. per device: the group's leader waits for its other shards (an event each)
+    for (int s = 0; s < m->n; ++s) {
+        const int lead = m->glead[m->group_of[s]];
+        if (s == lead) continue;
+        MHIP(hipSetDevice(m->dev[s]));
+        MHIP(hipEventRecord(m->ev[s], static_cast<hipStream_t>(jsp_engine_stream(m->sh[s]))));
+        MHIP(hipStreamWaitEvent(static_cast<hipStream_t>(jsp_engine_stream(m->sh[lead])), m->ev[s], 0));
     }
-    // 3. between devices: one SUM all-reduce of the combined tallies over RCCL
-    if (m->gdev.size() > 1) {
+    // 3. between devices: one group of SUM all-reduces over RCCL, out of place
+    //    (each device's own buffers keep their zeros): the tallies, and the
+    //    folded feasibility words (disjoint bits: their sum is their OR) into
+    //    the assigning engine's words
+    const uint32_t* tallies = m->red[g0].as<uint32_t>();
+    if (multi) {
         if (m->rccl.group_start() != 0) return jsp_internal_set_err(JSP_EHIP, "ncclGroupStart failed");
         for (size_t k = 0; k < m->gdev.size(); ++k) {
             MHIP(hipSetDevice(m->gdev[k]));
-            const int r = m->rccl.all_reduce(m->red[k].p, m->red[k].p, words, kNcclInt32, kNcclSum, m->comm[k],
-                                             static_cast<hipStream_t>(jsp_engine_stream(m->sh[m->glead[k]])));
+            hipStream_t ls = static_cast<hipStream_t>(jsp_engine_stream(m->sh[m->glead[k]]));
+            int r = m->rccl.all_reduce(m->red[k].p, m->sum[k].p, words, kNcclInt32, kNcclSum, m->comm[k], ls);
+            if (r == 0 && m->fold)
+                r = m->rccl.all_reduce(m->fl_local[k].p, (int)k == g0 ? (void*)f0 : m->fl_sum[k].p, fw, kNcclUint64,
+                                       kNcclSum, m->comm[k], ls);
             if (r != 0) {
                 (void)m->rccl.group_end();
                 return jsp_internal_set_err(JSP_EHIP, "ncclAllReduce failed: %s", m->rccl.err(r));
@@ -418,27 +479,30 @@ int place(Multi* m, const uint32_t* run_class, const uint32_t* run_len, uint32_t
         }
         const int r = m->rccl.group_end();
         if (r != 0) return jsp_internal_set_err(JSP_EHIP, "ncclGroupEnd failed: %s", m->rccl.err(r));
+        tallies = m->sum[g0].as<uint32_t>();
     }
-    // 4. feasibility + assignment on shard 0 (the leader of its device group)
+    // 4. the assignment on shard 0 (the leader of its device group): the run
+    //    list read and assign[] written in pinned memory by the kernels
     jsp_engine* e0 = m->sh[0];
     hipStream_t s0 = static_cast<hipStream_t>(jsp_engine_stream(e0));
-    const int d0 = m->dev[0];
-    MHIP(m->d_runs.reserve(d0, (size_t)std::max<uint32_t>(n_runs, 1) * 8));
-    MHIP(m->d_assign.reserve(d0, (size_t)std::max<uint32_t>(J, 1) * 4));
-    MHIP(hipSetDevice(d0));
-    uint32_t* dr = m->d_runs.as<uint32_t>();
+    MHIP(m->h_runs.reserve((size_t)std::max<uint32_t>(n_runs, 1) * 8));
+    MHIP(m->h_assign.reserve((size_t)std::max<uint32_t>(J, 1) * 4));
+    uint32_t* hr = m->h_runs.as<uint32_t>();
     if (n_runs > 0) {
-        MHIP(hipMemcpyAsync(dr, run_class, (size_t)n_runs * 4, hipMemcpyHostToDevice, s0));
-        MHIP(hipMemcpyAsync(dr + n_runs, run_len, (size_t)n_runs * 4, hipMemcpyHostToDevice, s0));
+        std::memcpy(hr, run_class, (size_t)n_runs * 4);
+        std::memcpy(hr + n_runs, run_len, (size_t)n_runs * 4);
     }
-    const uint32_t* red0 = m->red[m->group_of[0]].as<uint32_t>();
-    MTRY(jsp_assign_device(e0, red0, red0 + (size_t)C * L, L, dr, dr + n_runs, n_runs, J, m->d_assign.as<int32_t>(), s0));
-    MHIP(hipSetDevice(d0));
-    if (J > 0) MHIP(hipMemcpyAsync(assign_out, m->d_assign.p, (size_t)J * 4, hipMemcpyDeviceToHost, s0));
-    if (tally_out && C > 0) MHIP(hipMemcpyAsync(tally_out, red0, (size_t)C * L * 4, hipMemcpyDeviceToHost, s0));
-    if (occ_out) MHIP(hipMemcpyAsync(occ_out, red0 + (size_t)C * L, (size_t)L * 4, hipMemcpyDeviceToHost, s0));
+    MTRY(jspi_assign(e0, tallies, tallies + (size_t)C * L, L, hr, hr + n_runs, n_runs, J, m->h_assign.as<int32_t>(),
+                     m->fold));
+    MHIP(hipSetDevice(m->dev[0]));
+    if (tally_out && C > 0) MHIP(hipMemcpyAsync(tally_out, tallies, (size_t)C * L * 4, hipMemcpyDeviceToHost, s0));
+    if (occ_out) MHIP(hipMemcpyAsync(occ_out, tallies + (size_t)C * L, (size_t)L * 4, hipMemcpyDeviceToHost, s0));
+    // everything above is ordered before this stream's end (events, the
+    // all-reduce group on the leaders' streams): one wait, then every shard's
+    // error word without another synchronisation
     MHIP(hipStreamSynchronize(s0));
-    for (int s = 0; s < m->n; ++s) MTRY(jsp_engine_check(m->sh[s]));
+    if (J > 0) std::memcpy(assign_out, m->h_assign.p, (size_t)J * 4);
+    for (int s = 0; s < m->n; ++s) MTRY(jspi_check(m->sh[s]));
     if (stats) {
         uint32_t placed = 0;
         for (uint32_t j = 0; j < J; ++j) placed += assign_out[j] >= 0;

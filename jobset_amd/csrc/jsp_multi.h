@@ -2,12 +2,14 @@
 // (SURVEY.md §8b "one per device set", §8e): one process (the Go manager,
 // main.go:161-190, builds one engine) drives several GPUs. The node rows are
 // sharded by whole level-0 domains over one shard engine per listed device;
-// each shard tallies its leaf columns of a zero-initialised [C+1][L] buffer,
-// the buffers are SUM-combined -- by RCCL all-reduce over xGMI between
-// distinct devices (ncclCommInitAll in this process, one group call), by an
-// on-device add between shards that share a device -- and the first shard
-// runs the deterministic feasibility + assignment on the sums. Integer sums
-// make the result bit-exact for any device set (tests/test_multi_gpu.py).
+// the shards of one device tally straight into their own (disjoint) leaf
+// columns of that device's zero-initialised [C+1][L] buffer -- and, for leaf
+// classes, fold their leaves' feasibility bits into the feasibility words --
+// the devices' buffers are SUM-combined by one RCCL all-reduce group over
+// xGMI (ncclCommInitAll in this process; the words' bits are disjoint, so a
+// sum is their OR), and the first shard runs the deterministic assignment.
+// Integer sums make the result bit-exact for any device set
+// (tests/test_multi_gpu.py).
 #pragma once
 #include <stdint.h>
 
@@ -44,3 +46,16 @@ int n_devices(const Multi* m);  // distinct devices (RCCL ranks)
 
 // error reporting of the engine (jsp_last_error), for the device-set module
 int jsp_internal_set_err(int code, const char* fmt, ...);
+
+// Internal entry points of a shard engine (jsp_engine.cc), on its own stream:
+// whether it can fold its leaf classes' feasibility into its tally; its
+// feasibility words (and their count); a tally that folds into `fold_feas`
+// (null: none); the assignment on given tallies (folded: the feasibility
+// words are already in the engine's own buffer); a non-blocking check of its
+// launches' error word.
+bool jspi_fold_ok(jsp_engine* e);
+uint64_t* jspi_feas(jsp_engine* e, uint32_t* words);
+int jspi_tally(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint64_t* fold_feas);
+int jspi_assign(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld, const uint32_t* run_class,
+                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, bool folded);
+int jspi_check(jsp_engine* e);

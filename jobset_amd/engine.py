@@ -255,6 +255,13 @@ class Engine:
                                                scrub or None, scrub_bytes, _p(out)))
         return float(out[0]), float(out[1])
 
+    def tally_device_spans(self, d_cap: int, d_occ: int, ld: int, iters: int) -> Tuple[float, float]:
+        """In-kernel span of the one-tile wave tally (first wave start -> last
+        wave end, device clock; jsp_tally_device_spans): (median, mean) us."""
+        out = np.zeros(2, dtype=np.float64)
+        check(self._lib.jsp_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
+        return float(out[0]), float(out[1])
+
     def link_floor(self, iters: int = 2000) -> Tuple[float, float, float]:
         """Host -> device -> host round trip through pinned memory with the
         resident service's polling (jsp_engine_link_floor): (p50, p99, mean) us."""

@@ -85,6 +85,7 @@ SIGNATURES = [
     ("jsp_tally_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, ctypes.c_size_t, vp]),
     ("jsp_place_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, u32, vp, ctypes.c_size_t, vp]),
     ("jsp_engine_link_floor", ctypes.c_int, [vp, u32, vp]),
+    ("jsp_tally_device_spans", ctypes.c_int, [vp, vp, vp, u32, u32, vp]),
     ("jsp_engine_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
     ("jsp_engine_stream", vp, [vp]),
