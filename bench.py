@@ -437,7 +437,8 @@ def device_set_leg(p4, ref_assign, steps: int):
             sh, nd = ds.shards()
             exact = bool(np.array_equal(call.assign, ref_assign))
             return {"device_ids": ids, "shards": sh, "devices": nd,
-                    "combine": "RCCL all-reduce (ncclCommInitAll in this process)" if nd > 1 else "on-device add",
+                    "combine": "RCCL all-reduce, out of place (ncclCommInitAll in this process)" if nd > 1
+                    else "one device buffer, each shard writes its own leaf columns and feasibility bits (no add)",
                     "us_per_step": round(us, 1), "placed": int((call.assign >= 0).sum()),
                     "placements_per_s": round(int((call.assign >= 0).sum()) / (us * 1e-6), 1),
                     "bit_exact_vs_single_device": exact, "steps": steps,
@@ -802,9 +803,10 @@ def main() -> None:
         # a third, tracer-free measure: the kernel's own span (first wave start
         # -> last wave end, device clock stamps per wave; jsp_tally_device_spans)
         try:
-            span_med, span_mean = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(), L4, tally_loop)
+            span_med, span_mean, empty_us = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(), L4,
+                                                                         tally_loop)
         except Exception:  # noqa: BLE001 -- another tally shape (sharded ranks): no span
-            span_med = span_mean = None
+            span_med = span_mean = empty_us = None
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
         # cold: the library's read-only sweep of the 512 MiB buffer before each launch, dispatch events
@@ -873,9 +875,12 @@ def main() -> None:
                 "tally_span_us": round(span_mean, 2) if span_mean else None,
                 "tally_span_median_us": round(span_med, 2) if span_med else None,
                 "tally_span_vs_events": round(span_mean / tally_mean, 3) if span_mean else None,
-                "tally_measure": "tally_us (events on the dispatch packets); tally_span_us is the kernel's own "
-                                 "first-wave-start -> last-wave-end span from per-wave clock stamps (no tracer, no "
-                                 "dispatch overhead), reported beside it as the cross-check",
+                "tally_empty_grid_event_us": round(empty_us, 2) if empty_us else None,
+                "tally_span_plus_empty_vs_events": round((span_mean + empty_us) / tally_mean, 3) if span_mean else None,
+                "tally_measure": "tally_us (events on the dispatch packets) is the figure used; tally_span_us is the "
+                                 "kernel's own first-wave-start -> last-wave-end span from per-wave clock stamps (no "
+                                 "tracer), and tally_empty_grid_event_us the events' time for an empty launch of the "
+                                 "same grid: span + empty ~ events is the cross-check",
                 "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
                               "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
                               "around 200 ctypes-issued launches (includes host submit gaps)",

@@ -297,7 +297,9 @@ int jsp_engine_service_stop(jsp_engine* e);
 /* With timing on: the last service request's 100 MHz device-clock stamps, 8
  * per tile (0 request seen, 1 after the acquire, 2 tallied, 3 feasible count
  * scanned, 4 look-back done, 5 assign[] drained; 6-7 unused). Copies up to
- * cap/8 tiles; *n_tiles = how many (0 when no timed request is held). */
+ * cap/8 tiles; *n_tiles = how many (0 when no timed request is held). When
+ * cap leaves room for one more row after all the tiles, it receives the
+ * dispatcher's {0 request seen in the mailbox, 1 bell rung} (ABI v6). */
 int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles);
 /* Device time of `iters` back-to-back steps on the engine stream (the bench's
  * kernel-time legs): each step carries a start event on its first dispatch and
@@ -325,7 +327,9 @@ int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us);
  * (every wave's start, and its end once its stores drained); per launch the
  * span from the first wave's start to the last wave's end -- a third measure
  * beside the dispatch-packet events and a kernel trace, with no tracer and no
- * dispatch overhead in it. out_us[0] median, [1] mean. JSP_ESTATE when the
+ * dispatch overhead in it. out_us[0] median, [1] mean; out_us[2] the median
+ * dispatch-event time of an empty launch of the same grid (what events on the
+ * dispatch packets add to a kernel's own span). JSP_ESTATE when the
  * snapshot's tally runs another shape. */
 int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
                            double* out_us);

@@ -3,6 +3,8 @@
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
+#include <pthread.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -986,7 +988,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     }
     const unsigned long long lkey = ((unsigned long long)nb << 40) | ((unsigned long long)v.groups << 32) |
                                     ((unsigned long long)v.cpg << 8) | (unsigned)shape;
-    const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3;
+    const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3 + jsp::kSvcClkSlots;  // + the dispatcher's clk row
     if (v.layout_key != lkey || !v.words.p || nw * 4 > v.words.bytes) {
         if (shape == 3) {
             const size_t sb = (size_t)n_tiles * (v.cpg + 1) * jsp::kSplitSlot * 8;
@@ -1050,6 +1052,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;
     a.clk = e->timing && (shape == 2 || shape == 3) ? w + n_tiles + 3 : nullptr;
+    a.n_tiles = n_tiles;
     a.spin_limit = e->spin_limit;
     a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
     a.ready = ready;
@@ -1421,6 +1424,16 @@ void run_wake(jsp_engine* e) {
 }
 
 void waker_main(jsp_engine* e) {
+    // The waker runs only on an idle core (SCHED_IDLE): woken by a patch call,
+    // a normal-priority waker could preempt the caller on the caller's own core
+    // (CFS wake-up preemption) and put the whole restart inside the patch call
+    // it exists to keep short. If no core is idle, the next placement runs the
+    // wake itself (run_wake in svc_place).
+    {
+        sched_param sp{};
+        sp.sched_priority = 0;
+        (void)pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
+    }
     (void)hipSetDevice(e->device);
     for (;;) {
         {
@@ -2376,6 +2389,36 @@ int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
     std::sort(us.begin(), us.end());
     out_us[0] = us[iters / 2];
     out_us[1] = sum / iters;
+    // the same grid empty, timed by events on its dispatch packets: what the
+    // events add to a kernel's own span
+    const uint32_t grid = (e->n_wtiles + jsp::kTallyWaves - 1) / jsp::kTallyWaves;
+    std::vector<EvPair> ev(iters);
+    for (auto& p : ev) {
+        HIP_TRY(hipEventCreate(&p.a));
+        HIP_TRY(hipEventCreate(&p.b));
+    }
+    int rc = JSP_OK;
+    for (uint32_t i = 0; i < iters && rc == JSP_OK; ++i) {
+        jsp::set_launch_start(ev[i].a);
+        jsp::set_launch_stop(ev[i].b);
+        if (jsp::launch_empty(grid, s) != hipSuccess) rc = set_err(JSP_EHIP, "empty launch failed");
+        jsp::set_launch_start(nullptr);
+        jsp::set_launch_stop(nullptr);
+    }
+    if (rc == JSP_OK && hipStreamSynchronize(s) != hipSuccess) rc = set_err(JSP_EHIP, "empty launches failed");
+    std::vector<double> eu(iters, 0.0);
+    for (uint32_t i = 0; i < iters && rc == JSP_OK; ++i) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ev[i].a, ev[i].b) != hipSuccess) rc = set_err(JSP_EHIP, "event time failed");
+        eu[i] = ms * 1e3;
+    }
+    for (auto& p : ev) {
+        (void)hipEventDestroy(p.a);
+        (void)hipEventDestroy(p.b);
+    }
+    if (rc) return rc;
+    std::sort(eu.begin(), eu.end());
+    out_us[2] = eu[iters / 2];
     return check_launch_error(e);
 }
 
@@ -2616,7 +2659,9 @@ int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_
     if (!v.clk || !v.words.p) return JSP_OK;
     const uint32_t n = std::min<uint32_t>(cap / jsp::kSvcClkSlots, v.nb);
     if (n > 0 && !out) return set_err(JSP_EINVAL, "out is NULL");
-    std::memcpy(out, v.words.as<uint32_t>() + v.nb + 3, (size_t)n * jsp::kSvcClkSlots * 4);
+    // the tiles' rows, then (room permitting) the dispatcher's {request seen, bell rung}
+    const uint32_t rows = n == v.nb && cap / jsp::kSvcClkSlots > v.nb ? n + 1 : n;
+    std::memcpy(out, v.words.as<uint32_t>() + v.nb + 3, (size_t)rows * jsp::kSvcClkSlots * 4);
     *n_tiles = n;
     return JSP_OK;
 }

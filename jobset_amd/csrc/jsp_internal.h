@@ -241,7 +241,9 @@ struct ServiceArgs {
     uint32_t* stats;                    // host-mapped [2]: runs (1), placed
     uint32_t* done;                     // host-mapped [n_blocks]: seq of the last answered request
     uint32_t* err;                      // host-mapped: a tile whose look-back timed out writes its epoch
-    uint32_t* clk;                      // host-mapped [kSvcClkSlots n_blocks] 100 MHz phase stamps, or null
+    uint32_t* clk;                      // host-mapped [kSvcClkSlots (n_tiles + 1)] 100 MHz phase stamps, or null:
+                                        //   a row per tile, then the dispatcher's {request seen, bell rung}
+    uint32_t n_tiles;                   // tiles of the grid (the dispatcher's clk row follows theirs)
     uint32_t spin_limit;
     unsigned long long idle_ticks;      // 100 MHz ticks without a request before a workgroup leaves
     uint32_t* ready;                    // host-mapped: the dispatcher writes gen once it polls
@@ -327,6 +329,8 @@ bool launch_stop_used();
 // host-link floor probe (instrumentation): four polling waves answer request
 // numbers 1..n of *req in ack[16 w] (pinned host memory)
 hipError_t launch_link_probe(const uint32_t* req, uint32_t* ack, uint32_t n, uint64_t wait_ticks, hipStream_t s);
+// an empty launch of `grid` 256-thread workgroups (instrumentation)
+hipError_t launch_empty(uint32_t grid, hipStream_t s);
 // read-only cache scrub of `bytes` (instrumentation: cold-cache timings)
 hipError_t launch_scrub(const void* p, size_t bytes, uint32_t* sink, hipStream_t s);
 hipError_t launch_tally(const TallyArgs& a, hipStream_t s);

@@ -3083,11 +3083,18 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                     if (lane == 0) won = atomicCAS(s_p + 0, 0u, q) == 0u ? 1u : 0u;
                     if (__builtin_amdgcn_readlane((int)won, 0) == 0) break;
                     const bool patch = (jw & kReqPatch) != 0u || m > 0u;
+                    const uint32_t t_seen = (uint32_t)wall_clock64();
                     if (!patch && lane == 0) {
                         // ring at once: nothing to apply first
                         const unsigned long long mm = ((unsigned long long)jw << 32) | q;
                         if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    if (v.clk && lane == 0) {  // timing on: the dispatcher's row after the tiles' (seen, rung)
+                        uint32_t* dc = v.clk + kSvcClkSlots * v.n_tiles;
+                        __hip_atomic_store(dc, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        __hip_atomic_store(dc + 1, patch ? 0u : (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
                     }
                     // the host learns that a request with a patch was taken (a
                     // later request then need not carry the patch again)
@@ -3136,6 +3143,9 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
                 if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (v.clk)
+                    __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles + 1, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         seq = q;
@@ -3641,6 +3651,11 @@ __global__ __launch_bounds__(256) void link_probe_kernel(const uint32_t* req, ui
     }
 }
 
+// An empty kernel (instrumentation): the dispatch-event time of a launch of
+// a given grid that does nothing -- the packet and workgroup-dispatch
+// overhead that dispatch events add to a kernel's own span.
+__global__ __launch_bounds__(256) void empty_kernel() {}
+
 // ----------------------------------------------------------------- cache scrub (instrumentation)
 // Reads n16 16-byte words (a buffer larger than the Infinity Cache), so the
 // next launch finds its bytes in HBM only; nothing is dirtied. The sum goes
@@ -3977,6 +3992,11 @@ hipError_t launch_add_u32(uint32_t* dst, const uint32_t* src, size_t n, hipStrea
 
 hipError_t launch_link_probe(const uint32_t* req, uint32_t* ack, uint32_t n, uint64_t wait_ticks, hipStream_t s) {
     jsp_launch(link_probe_kernel, dim3(1), dim3(256), 0, s, req, ack, n, wait_ticks);
+    return hipGetLastError();
+}
+
+hipError_t launch_empty(uint32_t grid, hipStream_t s) {
+    jsp_launch(empty_kernel, dim3(grid), dim3(256), 0, s);
     return hipGetLastError();
 }
 

@@ -255,12 +255,13 @@ class Engine:
                                                scrub or None, scrub_bytes, _p(out)))
         return float(out[0]), float(out[1])
 
-    def tally_device_spans(self, d_cap: int, d_occ: int, ld: int, iters: int) -> Tuple[float, float]:
+    def tally_device_spans(self, d_cap: int, d_occ: int, ld: int, iters: int) -> Tuple[float, float, float]:
         """In-kernel span of the one-tile wave tally (first wave start -> last
-        wave end, device clock; jsp_tally_device_spans): (median, mean) us."""
-        out = np.zeros(2, dtype=np.float64)
+        wave end, device clock; jsp_tally_device_spans): (median, mean) us,
+        and the dispatch-event time of an empty launch of the same grid."""
+        out = np.zeros(3, dtype=np.float64)
         check(self._lib.jsp_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
-        return float(out[0]), float(out[1])
+        return float(out[0]), float(out[1]), float(out[2])
 
     def link_floor(self, iters: int = 2000) -> Tuple[float, float, float]:
         """Host -> device -> host round trip through pinned memory with the
@@ -285,10 +286,16 @@ class Engine:
     def service_clock(self) -> np.ndarray:
         """The last timed service request's per-tile 100 MHz stamps [tiles, 8]
         (jsp_engine_service_clock); empty when none is held."""
-        out = np.zeros(256 * 8, dtype=np.uint32)
+        return self.service_clock_rows()[0]
+
+    def service_clock_rows(self) -> Tuple[np.ndarray, np.ndarray]:
+        """(the tiles' stamps [tiles, 8], the dispatcher's row [8]: 0 request
+        seen in the mailbox, 1 bell rung) of the last timed service request."""
+        out = np.zeros(257 * 8, dtype=np.uint32)
         n = ctypes.c_uint32(0)
         check(self._lib.jsp_engine_service_clock(self._h, _p(out), out.shape[0], ctypes.byref(n)))
-        return out[:n.value * 8].reshape(n.value, 8)
+        k = n.value
+        return out[:k * 8].reshape(k, 8), out[k * 8:(k + 1) * 8]
 
     # ---------------------------------------------------------------- webhook / reconciler batches
     def resolve_leader_domains(self, leader_rows: np.ndarray, levels: np.ndarray) -> np.ndarray:

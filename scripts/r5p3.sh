@@ -1,0 +1,16 @@
+#!/bin/bash
+# full GPU suite (micro-patches, device-set step, span probe), patched-step probe,
+# cold probe A/B (waker vs inline), driver bench
+out=gpurun_out/r5/${1:-p3}
+mkdir -p $out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --durations=10 > $out/pytest_gpu.log 2>&1 || { tail -60 $out/pytest_gpu.log; exit 2; }
+tail -2 $out/pytest_gpu.log
+timeout -k 10 120 python tools/patched_probe.py 400 > $out/patched_probe.txt 2>&1 || exit 3
+cat $out/patched_probe.txt | grep -v amdgpu.ids
+for i in 1 2; do
+  timeout -k 10 120 python tools/cold_probe4.py 30 > $out/cold4_product_$i.txt 2>&1 || exit 3
+  JSP_LIB_PATH=$PWD/tools/bin/ab_inlinewake/libjsplace.so timeout -k 10 120 python tools/cold_probe4.py 30 > $out/cold4_inline_$i.txt 2>&1 || exit 3
+done
+cat $out/cold4_*.txt | grep -v amdgpu.ids
+timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench_driver.json 2> $out/bench.err || { tail -20 $out/bench.err; exit 4; }
+tail -c 300 $out/bench_driver.json

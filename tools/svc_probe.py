@@ -37,15 +37,20 @@ def main():
                 call()
                 walls.append((time.perf_counter() - t0) * 1e6)
                 if timed:
-                    c = eng.service_clock().astype(np.int64)
+                    c, d = eng.service_clock_rows()
+                    c, d = c.astype(np.int64), d.astype(np.int64)
                     ref = c[:, 0].min()
-                    phases.append([(c[:, k].max() - ref) * 10 for k in (0, 1, 6, 7, 2, 3, 4, 5)])
+                    # the dispatcher's row: request seen in the mailbox, bell rung (relative to the first tile)
+                    ds = (d[0] - ref) * 10 if d[0] else 0
+                    dr = (d[1] - ref) * 10 if d[1] else 0
+                    phases.append([ds, dr] + [(c[:, k].max() - ref) * 10 for k in (0, 1, 6, 7, 2, 3, 4, 5)])
             w = np.array(walls)
             line = f"cfg{cfg} timing={'on ' if timed else 'off'} patched={int(patched)}: wall p50 {np.median(w):.2f} us p99 {np.percentile(w, 99):.2f}"
             if timed:
                 ph = np.median(np.array(phases), axis=0)
                 line += " | device (ns from first tile seeing the request, slowest tile): " + " ".join(
-                    f"{n} {v:.0f}" for n, v in zip(("seen", "bcast", "rowpass", "leafpass", "tally", "scan", "lookback", "drained"), ph))
+                    f"{n} {v:.0f}" for n, v in zip(("disp_seen", "disp_rung", "seen", "bcast", "rowpass", "leafpass",
+                                                     "tally", "scan", "lookback", "drained"), ph))
             print(line, flush=True)
         eng.set_timing(False)
     eng.close()
