@@ -875,12 +875,12 @@ def main() -> None:
                 "tally_span_us": round(span_mean, 2) if span_mean else None,
                 "tally_span_median_us": round(span_med, 2) if span_med else None,
                 "tally_span_vs_events": round(span_mean / tally_mean, 3) if span_mean else None,
-                "tally_empty_grid_event_us": round(empty_us, 2) if empty_us else None,
+                "tally_empty_launch_event_us": round(empty_us, 2) if empty_us else None,
                 "tally_span_plus_empty_vs_events": round((span_mean + empty_us) / tally_mean, 3) if span_mean else None,
                 "tally_measure": "tally_us (events on the dispatch packets) is the figure used; tally_span_us is the "
                                  "kernel's own first-wave-start -> last-wave-end span from per-wave clock stamps (no "
-                                 "tracer), and tally_empty_grid_event_us the events' time for an empty launch of the "
-                                 "same grid: span + empty ~ events is the cross-check",
+                                 "tracer), and tally_empty_launch_event_us the events' time for an empty one-workgroup "
+                                 "launch: span + empty ~ events is the cross-check",
                 "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
                               "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
                               "around 200 ctypes-issued launches (includes host submit gaps)",

@@ -3,8 +3,6 @@
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
 #include <emmintrin.h>
 #include <hip/hip_runtime.h>
-#include <pthread.h>
-#include <sched.h>
 
 #include <algorithm>
 #include <chrono>
@@ -1424,16 +1422,9 @@ void run_wake(jsp_engine* e) {
 }
 
 void waker_main(jsp_engine* e) {
-    // The waker runs only on an idle core (SCHED_IDLE): woken by a patch call,
-    // a normal-priority waker could preempt the caller on the caller's own core
-    // (CFS wake-up preemption) and put the whole restart inside the patch call
-    // it exists to keep short. If no core is idle, the next placement runs the
-    // wake itself (run_wake in svc_place).
-    {
-        sched_param sp{};
-        sp.sched_priority = 0;
-        (void)pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
-    }
+    // Normal priority: at SCHED_IDLE (measured, profiles/r05) a waker
+    // preempted while it held the engine lock stalled the next placement by
+    // milliseconds (a 5.2 ms cold-recovery p99 on a shared host).
     (void)hipSetDevice(e->device);
     for (;;) {
         {
@@ -2389,9 +2380,9 @@ int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
     std::sort(us.begin(), us.end());
     out_us[0] = us[iters / 2];
     out_us[1] = sum / iters;
-    // the same grid empty, timed by events on its dispatch packets: what the
-    // events add to a kernel's own span
-    const uint32_t grid = (e->n_wtiles + jsp::kTallyWaves - 1) / jsp::kTallyWaves;
+    // an empty one-workgroup launch timed by events on its dispatch packet:
+    // the fixed cost events add to a kernel's own span
+    const uint32_t grid = 1;  // the launch's fixed packet and completion cost (a grid's dispatch overlaps its work)
     std::vector<EvPair> ev(iters);
     for (auto& p : ev) {
         HIP_TRY(hipEventCreate(&p.a));

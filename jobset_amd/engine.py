@@ -258,7 +258,7 @@ class Engine:
     def tally_device_spans(self, d_cap: int, d_occ: int, ld: int, iters: int) -> Tuple[float, float, float]:
         """In-kernel span of the one-tile wave tally (first wave start -> last
         wave end, device clock; jsp_tally_device_spans): (median, mean) us,
-        and the dispatch-event time of an empty launch of the same grid."""
+        and the dispatch-event time of an empty one-workgroup launch."""
         out = np.zeros(3, dtype=np.float64)
         check(self._lib.jsp_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
         return float(out[0]), float(out[1]), float(out[2])
