@@ -255,6 +255,16 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t n_c
  * occ_out (nullable) [n_leaves_total]: rows covered by other exclusive jobs. */
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);
+/* `iters` jsp_place calls back to back, timed in C (ABI v6): what a cgo
+ * caller's loop sees, with no interpreter between the calls (the bench's
+ * host-API steps). With n_patch > 0, each call is preceded by a one-row
+ * jsp_snapshot_patch of the taint column (row patch_rows[i % n_patch] set to
+ * patch_taints[i % n_patch]: a watch event between recoveries). out_us[0]
+ * total wall, [1] median and [2] p99 per step, microseconds; assign_out holds
+ * the last call's answer. */
+int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                   int32_t* assign_out, uint32_t iters, const uint32_t* patch_rows, const uint32_t* patch_taints,
+                   uint32_t n_patch, double* out_us);
 /* Same with one class id per job (run-length encoded on the host). */
 int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
                    int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);

@@ -2536,6 +2536,32 @@ launch_path:
     return JSP_OK;
 }
 
+int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                   int32_t* assign_out, uint32_t iters, const uint32_t* patch_rows, const uint32_t* patch_taints,
+                   uint32_t n_patch, double* out_us) {
+    if (iters == 0 || iters > 1000000) return set_err(JSP_EINVAL, "iters %u out of range [1,1000000]", iters);
+    if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
+    if (n_patch > 0 && (!patch_rows || !patch_taints)) return set_err(JSP_EINVAL, "patch rows / taints are NULL");
+    std::vector<double> us(iters);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto tp = t0;
+    for (uint32_t i = 0; i < iters; ++i) {
+        if (n_patch > 0) {
+            const uint32_t k = i % n_patch;
+            if (int rc = jsp_snapshot_patch(e, patch_rows + k, 1, nullptr, patch_taints + k, nullptr, nullptr)) return rc;
+        }
+        if (int rc = jsp_place(e, run_class, run_len, n_runs, assign_out, nullptr, nullptr, nullptr)) return rc;
+        const auto t = std::chrono::steady_clock::now();
+        us[i] = std::chrono::duration<double, std::micro>(t - tp).count();
+        tp = t;
+    }
+    out_us[0] = std::chrono::duration<double, std::micro>(tp - t0).count();
+    std::sort(us.begin(), us.end());
+    out_us[1] = us[iters / 2];
+    out_us[2] = us[std::min<size_t>(iters - 1, (size_t)(0.99 * iters))];
+    return JSP_OK;
+}
+
 int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs, int32_t* assign_out,
                    uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (n_jobs > 0 && !job_class) return set_err(JSP_EINVAL, "job_class is NULL");

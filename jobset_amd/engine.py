@@ -189,9 +189,23 @@ class Engine:
             if r:
                 check(r)
             return st
+        loop_out = np.zeros(3, dtype=np.float64)
+
+        def loop(iters: int, patch_rows: Optional[np.ndarray] = None,
+                 patch_taints: Optional[np.ndarray] = None) -> Tuple[float, float, float]:
+            """`iters` calls back to back timed in C (jsp_place_loop), each
+            after a one-row taint patch when rows are given: total, median and
+            p99 per step, microseconds."""
+            pr = None if patch_rows is None else np.ascontiguousarray(patch_rows, dtype=np.uint32)
+            pt = None if patch_taints is None else np.ascontiguousarray(patch_taints, dtype=np.uint32)
+            check(self._lib.jsp_place_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
+                                           int(iters), _p(pr), _p(pt), 0 if pr is None else int(pr.shape[0]),
+                                           loop_out.ctypes.data))
+            return float(loop_out[0]), float(loop_out[1]), float(loop_out[2])
         call.assign = assign[:J]
         call.stats = st
-        call.keep = (rc, rl, assign)
+        call.loop = loop
+        call.keep = (rc, rl, assign, loop_out)
         return call
 
     def host_patcher(self, rows: np.ndarray, labels: Optional[np.ndarray] = None,

@@ -397,3 +397,29 @@ int jspf_run(jspf_ctx* x, int32_t* assign, uint32_t* cap_out, uint32_t* occ_out)
     if (occ_out) memcpy(occ_out, x->occ, sizeof(uint32_t) * x->L);
     return placed;
 }
+
+/* Timed loops (the bench's CPU legs, timed in C like the engine's
+ * jsp_place_loop, so that no Python call overhead sits in either figure):
+ * `iters` placements back to back; with rows (nrows > 0), row rows[i % nrows]
+ * of the taint column rewritten before each (a watch event's one-row patch,
+ * the same write the engine's patched step makes). Returns the wall time in
+ * microseconds. */
+#include <time.h>
+static double now_us(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec * 1e6 + (double)ts.tv_nsec * 1e-3;
+}
+
+double jspf_run_loop(jspf_ctx* x, int32_t* assign, uint32_t iters, const uint32_t* rows, uint32_t nrows) {
+    uint32_t* taints = (uint32_t*)x->p->taints;
+    const double t0 = now_us();
+    for (uint32_t i = 0; i < iters; ++i) {
+        if (nrows > 0) {
+            const uint32_t r = rows[i % nrows];
+            __atomic_store_n(taints + r, __atomic_load_n(taints + r, __ATOMIC_RELAXED), __ATOMIC_RELEASE);
+        }
+        (void)jspf_run(x, assign, NULL, NULL);
+    }
+    return now_us() - t0;
+}
