@@ -91,7 +91,7 @@ tools/bin/valu_rate: tools/valu_rate.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
 
-# A/B builds of the kernels with one build flag (tools/ab_probe.py loads them
+# A/B builds of the kernels with one build flag (a probe loads them
 # through JSP_LIB_PATH): tools/ablib/<name>/libjsplace.so
 AB_FLAGS_fakedesc = -DJSP_AB_FAKE_DESC
 tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
@@ -101,7 +101,7 @@ tools/ablib/%/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o 
 tools/bin/block_probe: tools/block_probe.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
-# A/B build: the service's row/leaf-pass stamps carry the shader clock (tools/dbg_clk.py)
+# A/B build: the service's row/leaf-pass stamps carry the shader clock (diagnostic)
 tools/bin/ab_clk/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
 	@mkdir -p build/ab_clk tools/bin/ab_clk
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_CLKFREQ -c -o build/ab_clk/k.o jobset_amd/csrc/jsp_kernels.hip

@@ -214,15 +214,15 @@ def cpu_threads() -> int:
 
 
 def time_cpu(fc, seconds: float):
-    """µs per placement of the prepared FastCPU over a bounded sample."""
+    """µs per placement of the prepared FastCPU over a bounded sample, the
+    placements timed in C (jspf_run_loop, batches of 64) like the GPU's
+    host-API loop (jsp_place_loop): no interpreter between the calls."""
     fc.run()
-    n, t0 = 0, time.perf_counter()
-    while True:
-        fc.run()
-        n += 1
-        dt = time.perf_counter() - t0
-        if dt >= seconds:
-            return dt * 1e6 / n, n, dt
+    n, tot = 0, 0.0
+    while tot < seconds * 1e6:
+        tot += fc.run_loop(64)
+        n += 64
+    return tot / n, n, tot * 1e-6
 
 
 def host_api_latency(eng, p, trials: int, trial_fn=None):
@@ -382,36 +382,36 @@ def cpu_patched_step(p, threads, seconds: float):
         fc = O.FastCPU(th)
         fc.prepare(p)
         fc.run()
-        taints = fc.pk.arrs["taints"]
-        n, t0 = 0, time.perf_counter()
-        while True:
-            row = (n * 7919) % max(p.nodes.n_nodes, 1)
-            taints[row] = taints[row]
-            fc.run()
-            n += 1
-            if time.perf_counter() - t0 >= seconds:
-                break
-        out[f"{th}t"] = round((time.perf_counter() - t0) * 1e6 / n, 2)
+        rows = np.array([(i * 7919) % max(p.nodes.n_nodes, 1) for i in range(16)], dtype=np.uint32)
+        n, tot = 0, 0.0
+        while tot < seconds * 1e6:
+            tot += fc.run_loop(64, rows)  # timed in C, like the GPU leg
+            n += 64
+        out[f"{th}t"] = round(tot / n, 2)
         fc.close()
     return out
 
 
 def patched_step_us(eng, p, steps: int):
     """Host-API steps with one row patched before each placement (a watch
-    event between recoveries): the resident tiles reload their rows from
-    memory instead of their LDS copies. µs per (patch + place)."""
+    event between recoveries): the patch rides in the next request
+    (micro-patch) and the resident tiles apply it before they answer. µs per
+    (patch + place), timed in C (jsp_place_loop with patch rows), and the
+    same steps from a Python loop (two ctypes calls each) beside it."""
     from jobset_amd.snapshot import job_runs
     call = eng.host_placer(*job_runs(p.job_class))
-    rows = [np.array([(i * 7919) % p.nodes.n_nodes], dtype=np.uint32) for i in range(16)]
-    patches = [eng.host_patcher(r, taints=p.nodes.taints[r]) for r in rows]
-    for i in range(20):
-        patches[i % 16]()
-        call()
+    rows = np.array([(i * 7919) % p.nodes.n_nodes for i in range(16)], dtype=np.uint32)
+    taints = np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)
+    call.loop(20, rows, taints)
+    tot, med, p99 = call.loop(steps, rows, taints)
+    patches = [eng.host_patcher(rows[i:i + 1], taints=taints[i:i + 1]) for i in range(16)]
     t0 = time.perf_counter()
     for i in range(steps):
         patches[i % 16]()
         call()
-    return (time.perf_counter() - t0) * 1e6 / steps
+    py = (time.perf_counter() - t0) * 1e6 / steps
+    return {"mean_us": round(tot / steps, 3), "p50_us": round(med, 2), "p99_us": round(p99, 2),
+            "python_loop_us": round(py, 3)}
 
 
 def device_set_leg(p4, ref_assign, steps: int):
@@ -430,10 +430,7 @@ def device_set_leg(p4, ref_assign, steps: int):
             call = ds.host_placer(*job_runs(p4.job_class))
             for _ in range(3):
                 call()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                call()
-            us = (time.perf_counter() - t0) * 1e6 / steps
+            us = call.loop(steps)[0] / steps  # timed in C (jsp_place_loop), like the single-device leg
             sh, nd = ds.shards()
             exact = bool(np.array_equal(call.assign, ref_assign))
             return {"device_ids": ids, "shards": sh, "devices": nd,
@@ -442,7 +439,7 @@ def device_set_leg(p4, ref_assign, steps: int):
                     "us_per_step": round(us, 1), "placed": int((call.assign >= 0).sum()),
                     "placements_per_s": round(int((call.assign >= 0).sum()) / (us * 1e-6), 1),
                     "bit_exact_vs_single_device": exact, "steps": steps,
-                    "note": "host API (jsp_place): run list in, assign[] back in host memory"}
+                    "note": "host API (jsp_place): run list in, assign[] back in host memory; timed in C"}
     except Exception as ex:  # noqa: BLE001 -- reported in the line, never hidden
         return {"device_ids": ids, "error": str(ex)}
 
@@ -550,8 +547,9 @@ def main() -> None:
     call()
     eng.timing(reset=True)  # the library's own phase clocks of the timed calls (host side, always on)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        call()
+    # the K timed jsp_place calls, issued from C (jsp_place_loop) as a cgo
+    # caller's loop would: no interpreter between them
+    _, loop_p50, loop_p99 = call.loop(args.steps)
     eng.service_stop()
     torch.cuda.synchronize()
     barrier(world)
@@ -583,7 +581,12 @@ def main() -> None:
 
     # one row patched before each call (the resident tiles reload their rows
     # from memory instead of their LDS copies); not the timed loop
-    patched = round(patched_step_us(eng, p, max(200, args.steps * 5)), 3) if shape == 3 else None
+    patched = patched_step_us(eng, p, max(200, args.steps * 5)) if shape == 3 else None
+    # the same K steps from a Python loop (one ctypes call each), beside the C-timed value
+    t0p = time.perf_counter()
+    for _ in range(args.steps):
+        call()
+    py_step_us = (time.perf_counter() - t0p) * 1e6 / args.steps
     eng.service_stop()
     # the host-link floor: host -> device -> host through pinned memory with
     # the service's polling, and where the timed host-API step's time went
@@ -669,10 +672,10 @@ def main() -> None:
     if rank == 0 and world == 1 and args.cpu_seconds > 0 and patched is not None:
         legs_p = cpu_patched_step(p, sorted({1, 2, T}), min(2.0, args.cpu_seconds / 6))
         best_p = min(legs_p.values())
-        cpu_patched = {"legs_us": legs_p, "best_us": best_p, "gpu_patched_step_us": patched,
-                       "gpu_over_best_cpu": round(best_p / patched, 3),
+        cpu_patched = {"legs_us": legs_p, "best_us": best_p, "gpu_patched_step_us": patched["mean_us"],
+                       "gpu_over_best_cpu": round(best_p / patched["mean_us"], 3),
                        "note": "oracle/cpu_fast.c: the same one-row write into its columns, then one placement, "
-                               "back to back (the CPU side of patched_step_us)"}
+                               "back to back, timed in C (jspf_run_loop; the CPU side of patched_step_us)"}
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         from oracle import oracle as O
         legs = []
@@ -832,10 +835,7 @@ def main() -> None:
             call4 = eng.host_placer(*job_runs(p4.job_class))
             for _ in range(5):
                 call4()
-            t0h = time.perf_counter()
-            for _ in range(steps4):
-                call4()
-            host_step = round((time.perf_counter() - t0h) * 1e6 / steps4, 2)
+            host_step = round(call4.loop(steps4)[0] / steps4, 2)  # timed in C (jsp_place_loop)
             assert np.array_equal(call4.assign, sp.assign()), "host API differs from the device path on cfg4"
         copy_ceiling = None
         if world == 1:  # achievable streaming rate: a cold copy of the same byte count
@@ -895,6 +895,7 @@ def main() -> None:
                              "launch (events around it), so the launch's misses pay its write-backs",
                 "step_device": step_dev,
                 "host_api_step_us": host_step,
+                "host_api_note": "jsp_place calls back to back, timed in C (jsp_place_loop)",
                 "copy_ceiling_same_bytes": copy_ceiling,
                 "tally_traffic": pmc_traffic(("tally_wave",), 4) if world == 1 else None,
                 "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
@@ -944,6 +945,12 @@ def main() -> None:
                          "note": "avg_us / median_us: events on the dispatch packets of back-to-back launches "
                                  "(jsp_place_device_timed, the engine stream); event_loop_us: HIP events around "
                                  "ctypes-issued launches. Latency-bound: one launch moving 0.43 MB; DESIGN.md §8"},
+            "timed_loop": "the K timed steps are jsp_place calls issued and timed from C (jsp_place_loop), as a cgo "
+                          "caller's loop would issue them; the same K steps from a Python loop (one ctypes call "
+                          "each) are python_loop_us_per_step",
+            "python_loop_us_per_step": round(py_step_us, 3),
+            "host_api_step_p50_us": round(loop_p50, 3),
+            "host_api_step_p99_us": round(loop_p99, 3),
             "service": svc,
             "rows_note": "the timed loop places the same snapshot repeatedly: the resident tiles keep their rows in "
                          "LDS between requests (no row traffic); patched_step_us times one row patched before "

@@ -25,8 +25,7 @@ out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
 med, mean = e.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 50)
 e.check()
 assert np.array_equal(out.cpu().numpy(), a)
-print(f"device step (fold={os.environ.get('JSP_FEAS_FOLD', '1')}, level={os.environ.get('JSP_ASSIGN_LEVEL', '1')}): "
-      f"median {med:.2f} us mean {mean:.2f} us", flush=True)
+print(f"device step: median {med:.2f} us mean {mean:.2f} us", flush=True)
 L = p.topology.n_leaves
 cap = torch.zeros((len(p.classes) + 1, L), dtype=torch.int32, device="cuda")
 s = torch.cuda.current_stream().cuda_stream

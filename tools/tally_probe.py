@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """cfg4 tally (1M rows, C=4) warm and cold per workgroup chunk count
-(JSP_BLOCK_CHUNKS, read at snapshot upload): back-to-back HIP-event rate and
+(the block_chunks test hook, read at snapshot upload): back-to-back HIP-event rate and
 the median of single launches after a 512 MiB scrub. Diagnostic only."""
 import os
 import sys
@@ -21,7 +21,7 @@ def main():
     scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")
     tb = bench.tally_bytes(p)
     for ch in (1, 2, 3, 4):
-        os.environ["JSP_BLOCK_CHUNKS"] = str(ch)
+        os.environ["JSP_TEST_HOOKS"] = f"block_chunks={ch}"
         eng.load(p)
         fn = lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), L, stream)  # noqa: E731
         for _ in range(10):
