@@ -2,9 +2,12 @@
 // the C ABI of include/jsplace.h over HIP device buffers and the kernels of
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
 #include <emmintrin.h>
+#include <pthread.h>
+#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -276,6 +279,12 @@ struct jsp_engine {
     std::mutex wake_mu;
     std::condition_variable wake_cv;
     bool wake_ring = false, wake_quit = false;
+    // a ring is delivered after the caller releases mu (wake_notify), with the
+    // waker kept off the ringing thread's CPU (waker_cpus = the process's
+    // CPUs at the waker's creation; waker_excl = the CPU it is kept off)
+    std::atomic<bool> wake_notify{false};
+    cpu_set_t waker_cpus;
+    std::atomic<int> waker_excl{-1};
     jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
@@ -1441,12 +1450,16 @@ void waker_main(jsp_engine* e) {
 // The waker thread, created with the engine's first service (thread creation
 // costs ~100 us, which must never land in a recovery's patch call).
 void start_waker(jsp_engine* e) {
-    if (!e->waker.joinable()) e->waker = std::thread(waker_main, e);
+    if (e->waker.joinable()) return;
+    CPU_ZERO(&e->waker_cpus);
+    if (sched_getaffinity(0, sizeof e->waker_cpus, &e->waker_cpus) != 0) CPU_ZERO(&e->waker_cpus);
+    e->waker = std::thread(waker_main, e);
 }
 
-// Hand the wake to the waker thread. Called with mu held. (Diagnostic A/B
-// build tools/bin/ab_inlinewake, -DJSP_AB_INLINE_WAKE: the patch call runs the
-// wake itself; never the product library.)
+// Hand the wake to the waker thread. Called with mu held; the caller delivers
+// it (notify_waker) after releasing mu, so the waker never wakes into a held
+// lock. (Diagnostic A/B build tools/bin/ab_inlinewake, -DJSP_AB_INLINE_WAKE:
+// the patch call runs the wake itself; never the product library.)
 void ring_waker(jsp_engine* e) {
     e->wake_job = true;
 #ifdef JSP_AB_INLINE_WAKE
@@ -1458,6 +1471,27 @@ void ring_waker(jsp_engine* e) {
         std::lock_guard<std::mutex> l(e->wake_mu);
         e->wake_ring = true;
     }
+    e->wake_notify.store(true, std::memory_order_relaxed);
+}
+
+// Deliver a ring (mu not held). The waker is kept off the ringing thread's
+// CPU: woken there, it would preempt the caller (a fresh sleeper wins the
+// CPU) and run the service launch -- tens of microseconds -- inside the
+// caller's patch call. The affinity changes only when the caller's CPU does
+// (one syscall, then none). (A/B build tools/bin/ab_waker_anycpu,
+// -DJSP_AB_WAKER_ANYCPU: no affinity.)
+void notify_waker(jsp_engine* e) {
+    if (!e->wake_notify.exchange(false, std::memory_order_relaxed)) return;
+#ifndef JSP_AB_WAKER_ANYCPU
+    const int cpu = sched_getcpu();
+    if (cpu >= 0 && cpu < CPU_SETSIZE && e->waker_excl.load(std::memory_order_relaxed) != cpu &&
+        CPU_ISSET(cpu, &e->waker_cpus) && CPU_COUNT(&e->waker_cpus) > 1) {
+        cpu_set_t m = e->waker_cpus;
+        CPU_CLR(cpu, &m);
+        if (pthread_setaffinity_np(e->waker.native_handle(), sizeof m, &m) == 0)
+            e->waker_excl.store(cpu, std::memory_order_relaxed);
+    }
+#endif
     e->wake_cv.notify_one();
 }
 
@@ -2074,12 +2108,27 @@ int jsp_snapshot_upload(jsp_engine* e, const jsp_nodes* nd) {
     return JSP_OK;
 }
 
+static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
+                                 const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner,
+                                 std::chrono::steady_clock::time_point t0);
+
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
                        const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner); }
     const auto t0 = std::chrono::steady_clock::now();
-    std::lock_guard<std::mutex> g(e->mu);
+    int rc;
+    {
+        std::lock_guard<std::mutex> g(e->mu);
+        rc = snapshot_patch_locked(e, rows, n, labels, taints, free_res, excl_owner, t0);
+    }
+    notify_waker(e);
+    return rc;
+}
+
+static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
+                                 const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner,
+                                 std::chrono::steady_clock::time_point t0) {
     if (!e->have_snap) return set_err(JSP_ESTATE, "no snapshot uploaded");
     if (n == 0) return JSP_OK;
     if (!rows) return set_err(JSP_EINVAL, "rows is NULL");
