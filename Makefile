@@ -122,9 +122,3 @@ tools/bin/ab_inlinewake/libjsplace.so: jobset_amd/csrc/jsp_engine.cc build/jsp_k
 	@mkdir -p build/ab_iw tools/bin/ab_inlinewake
 	$(HIPCC) $(HIPFLAGS) -DJSP_AB_INLINE_WAKE -x hip -c -o build/ab_iw/e.o jobset_amd/csrc/jsp_engine.cc
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/jsp_kernels.o build/ab_iw/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
-# A/B build: the waker thread may run on any CPU, the ringing caller's too
-# (tools/cold_probe4.py loads it through JSP_LIB_PATH)
-tools/bin/ab_waker_anycpu/libjsplace.so: jobset_amd/csrc/jsp_engine.cc build/jsp_kernels.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
-	@mkdir -p build/ab_wa tools/bin/ab_waker_anycpu
-	$(HIPCC) $(HIPFLAGS) -DJSP_AB_WAKER_ANYCPU -x hip -c -o build/ab_wa/e.o jobset_amd/csrc/jsp_engine.cc
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/jsp_kernels.o build/ab_wa/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

@@ -664,6 +664,19 @@ def main() -> None:
                              "its columns, the same slept gap, then one placement; timed = patch + placement, the gap "
                              "excluded")
         cold2["vs_cpu"] = cold_vs_cpu(cold2, cold2["cpu"])
+    # the same recovery with the service parked (JSP_SERVICE_PARKED: no idle
+    # exit, a dedicated GPU -- the GPU side of the CPU pool's spinning threads)
+    cold2p = None
+    if rank == 0 and args.cold_trials > 0:
+        eng.set_service(True, parked=True)
+        settled_place(eng, p.job_class)
+        cold2p = cold_recovery_latency(eng, p, args.cold_trials)
+        eng.service_stop()
+        eng.set_service(True)
+        cold2p["note"] = ("JSP_SERVICE_PARKED (the service never idles out): the same 60 ms sleep, one-row patch, gap "
+                          "and jsp_place; the patch rides in the request")
+        if cold2 is not None and "cpu" in cold2:
+            cold2p["vs_cpu"] = cold_vs_cpu(cold2p, cold2["cpu"])
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
     cpu = None
@@ -968,6 +981,9 @@ def main() -> None:
             "p99_cold_recovery_us": {g: v["p99_us"] for g, v in cold2.items() if g.startswith("gap_")} if cold2 else None,
             "p99_cold_recovery_best_cpu_us": {g: v["best_cpu_p99_us"] for g, v in cold2.get("vs_cpu", {}).items()}
             if cold2 else None,
+            "p99_cold_recovery_parked_us": {g: v["p99_us"] for g, v in cold2p.items() if g.startswith("gap_")}
+            if cold2p else None,
+            "cold_recovery_parked": cold2p,
             "recovery_trials": lat2["n"] if lat2 else 0,
             "cold_recovery": cold2,
             "cpu_baseline": cpu,

@@ -57,7 +57,7 @@
  * the engine's work) or, once visible, from the next call on the engine. No
  * timeout returns JSP_OK with a stale assign[].
  *
- * Environment: JSP_SERVICE=0 (no resident service), JSP_SERVICE_IDLE_MS
+ * Environment: JSP_SERVICE=0 (no resident service) / =parked, JSP_SERVICE_IDLE_MS
  * (its idle exit, default 50), JSP_RCCL_LIB (device sets) are the operational
  * switches; JSP_TEST_HOOKS is for tests only (jsp_engine.cc TestHooks).
  */
@@ -192,6 +192,13 @@ typedef struct jsp_timing {
 #define JSP_SERVICE_AUTO 1     /* default: the multi-class / multi-level shapes are answered by the split
                                   service -- resident tiles tally and hand back per-domain feasibility,
                                   the host walks (stats.fused = 5) */
+#define JSP_SERVICE_PARKED 2   /* AUTO without the idle exit (ABI v6): the service stays on the GPU
+                                  between requests however long the gap -- a dedicated GPU, where a
+                                  recovery hours after the last placement finds it polling (the
+                                  GPU analogue of a CPU pool whose threads spin). It leaves on
+                                  jsp_engine_service_stop, an upload, a mode change or destroy;
+                                  a device-wide synchronize needs the stop first. JSP_SERVICE=parked
+                                  in the environment selects it. */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);

@@ -2,8 +2,6 @@
 // the C ABI of include/jsplace.h over HIP device buffers and the kernels of
 // jsp_kernels.hip. See DESIGN.md for the data layout and the rules.
 #include <emmintrin.h>
-#include <pthread.h>
-#include <sched.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -279,12 +277,8 @@ struct jsp_engine {
     std::mutex wake_mu;
     std::condition_variable wake_cv;
     bool wake_ring = false, wake_quit = false;
-    // a ring is delivered after the caller releases mu (wake_notify), with the
-    // waker kept off the ringing thread's CPU (waker_cpus = the process's
-    // CPUs at the waker's creation; waker_excl = the CPU it is kept off)
+    // a ring is delivered after the caller releases mu (wake_notify)
     std::atomic<bool> wake_notify{false};
-    cpu_set_t waker_cpus;
-    std::atomic<int> waker_excl{-1};
     jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
@@ -839,6 +833,11 @@ double svc_idle_ms() {
     return ms;
 }
 
+// The engine's idle limit: JSP_SERVICE_PARKED never idles out (a dedicated
+// GPU; the service leaves on jsp_engine_service_stop, an upload or destroy).
+constexpr double kParkedIdleMs = 1e15;
+double idle_ms(const jsp_engine* e) { return e->svc_mode == JSP_SERVICE_PARKED ? kParkedIdleMs : svc_idle_ms(); }
+
 // Class groups of the split service's tiles: as the fused shape's (up to 4
 // groups of >= 2 classes, within 128 tiles), capped by the co-resident tile
 // limit.
@@ -1061,7 +1060,8 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     a.clk = e->timing && (shape == 2 || shape == 3) ? w + n_tiles + 3 : nullptr;
     a.n_tiles = n_tiles;
     a.spin_limit = e->spin_limit;
-    a.idle_ticks = (unsigned long long)(svc_idle_ms() * 1e5);  // 100 MHz
+    // 100 MHz ticks; parked: 2^62 (never reached, and twice it does not wrap)
+    a.idle_ticks = e->svc_mode == JSP_SERVICE_PARKED ? (1ull << 62) : (unsigned long long)(svc_idle_ms() * 1e5);
     a.ready = ready;
     a.gen = v.gen;
     v.err_ack = __atomic_load_n(w + n_tiles + 2, __ATOMIC_ACQUIRE);  // an earlier instance's error is not ours
@@ -1361,7 +1361,7 @@ bool svc_wake_wanted(jsp_engine* e) {
     auto& v = e->svc;
     if (!v.armed || !svc_ok(e)) return false;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
-    return !(v.running && since <= 0.5 * svc_idle_ms());
+    return !(v.running && since <= 0.5 * idle_ms(e));
 }
 
 // (Re)start the service without waiting for its dispatcher to poll. Long
@@ -1372,7 +1372,7 @@ bool svc_wake_wanted(jsp_engine* e) {
 int svc_restart_quiet(jsp_engine* e) {
     auto& v = e->svc;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
-    if (v.running && since > svc_idle_ms() + 5.0 && hipStreamQuery(v.stream) == hipSuccess) {
+    if (v.running && since > idle_ms(e) + 5.0 && hipStreamQuery(v.stream) == hipSuccess) {
         v.running = false;
         v.pending = 0;
         e->grave.flush();
@@ -1450,10 +1450,7 @@ void waker_main(jsp_engine* e) {
 // The waker thread, created with the engine's first service (thread creation
 // costs ~100 us, which must never land in a recovery's patch call).
 void start_waker(jsp_engine* e) {
-    if (e->waker.joinable()) return;
-    CPU_ZERO(&e->waker_cpus);
-    if (sched_getaffinity(0, sizeof e->waker_cpus, &e->waker_cpus) != 0) CPU_ZERO(&e->waker_cpus);
-    e->waker = std::thread(waker_main, e);
+    if (!e->waker.joinable()) e->waker = std::thread(waker_main, e);
 }
 
 // Hand the wake to the waker thread. Called with mu held; the caller delivers
@@ -1474,24 +1471,12 @@ void ring_waker(jsp_engine* e) {
     e->wake_notify.store(true, std::memory_order_relaxed);
 }
 
-// Deliver a ring (mu not held). The waker is kept off the ringing thread's
-// CPU: woken there, it would preempt the caller (a fresh sleeper wins the
-// CPU) and run the service launch -- tens of microseconds -- inside the
-// caller's patch call. The affinity changes only when the caller's CPU does
-// (one syscall, then none). (A/B build tools/bin/ab_waker_anycpu,
-// -DJSP_AB_WAKER_ANYCPU: no affinity.)
+// Deliver a ring (mu not held). Keeping the waker off the ringing thread's
+// CPU (an affinity change when the caller's CPU changed) was measured and
+// dropped: the affinity call costs the patch call 6-15 us at p50
+// (profiles/r05/probes/cold4_waker_affinity_ab.txt).
 void notify_waker(jsp_engine* e) {
     if (!e->wake_notify.exchange(false, std::memory_order_relaxed)) return;
-#ifndef JSP_AB_WAKER_ANYCPU
-    const int cpu = sched_getcpu();
-    if (cpu >= 0 && cpu < CPU_SETSIZE && e->waker_excl.load(std::memory_order_relaxed) != cpu &&
-        CPU_ISSET(cpu, &e->waker_cpus) && CPU_COUNT(&e->waker_cpus) > 1) {
-        cpu_set_t m = e->waker_cpus;
-        CPU_CLR(cpu, &m);
-        if (pthread_setaffinity_np(e->waker.native_handle(), sizeof m, &m) == 0)
-            e->waker_excl.store(cpu, std::memory_order_relaxed);
-    }
-#endif
     e->wake_cv.notify_one();
 }
 
@@ -1504,7 +1489,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     const auto now = std::chrono::steady_clock::now();
     const int shape = svc_shape(e);
     bool restart = !v.running || J > v.cap || v.clk != e->timing || v.blocks != e->n_blocks || v.shape != shape ||
-                   std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * svc_idle_ms();
+                   std::chrono::duration<double, std::milli>(now - v.last).count() > 0.5 * idle_ms(e);
     // the request's tiles must read the patched rows: a patch held back for
     // the running service rides on this request (its dispatcher applies it
     // before ringing the tiles); any other is waited for
@@ -1628,7 +1613,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
 bool svc_up(jsp_engine* e) {
     auto& v = e->svc;
     const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - v.last).count();
-    return v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    return v.running && since <= 0.5 * idle_ms(e) && svc_ok(e) && svc_shape(e) == v.shape;
 }
 
 // Merge n rows of one patch call (columns fl) into the held micro-patch: a
@@ -1834,7 +1819,9 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
     }
     std::memset(e->h_err.p, 0, 64);
     // operational: JSP_SERVICE=0 keeps the resident service off
-    if (const char* v = std::getenv("JSP_SERVICE")) e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF : JSP_SERVICE_AUTO;
+    if (const char* v = std::getenv("JSP_SERVICE"))
+        e->svc_mode = std::strcmp(v, "0") == 0 ? JSP_SERVICE_OFF
+                      : std::strcmp(v, "parked") == 0 ? JSP_SERVICE_PARKED : JSP_SERVICE_AUTO;
     e->hooks = read_hooks();
     // test hooks: CUs the service may count on (stands in for a smaller GPU
     // or a partition), the service's first request number (next to 2^30)
@@ -2190,7 +2177,7 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
     // a warm-up request; otherwise the patch kernel.
     const auto t1 = std::chrono::steady_clock::now();
     const double since = std::chrono::duration<double, std::milli>(t1 - v.last).count();
-    const bool up = v.running && since <= 0.5 * svc_idle_ms() && svc_ok(e) && svc_shape(e) == v.shape;
+    const bool up = v.running && since <= 0.5 * idle_ms(e) && svc_ok(e) && svc_shape(e) == v.shape;
     const bool wake = !up && svc_wake_wanted(e);
     // The delta into pinned staging, read in place. Patches for the service
     // of up to kPatchInlineRows rows go to its fixed inline buffer (layout
@@ -2703,7 +2690,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 1, mode); }
     std::lock_guard<std::mutex> g(e->mu);
-    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO)
+    if (mode != JSP_SERVICE_OFF && mode != JSP_SERVICE_AUTO && mode != JSP_SERVICE_PARKED)
         return set_err(JSP_EINVAL, "service mode %d", mode);
     if (mode != e->svc_mode) {  // the running service's shape may change
         e->svc.resume = false;

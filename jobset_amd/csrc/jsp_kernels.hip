@@ -3250,13 +3250,15 @@ __device__ bool service_xcc_vote(const ServiceArgs& v, uint32_t slot, uint32_t n
         uint32_t lo = 15u, hi = 0u;
         bool ok = true;
         const uint64_t t0 = wall_clock64();
+        // bounded by the idle limit, at most 50 ms (a parked service's is unbounded)
+        const uint64_t limit = v.idle_ticks < 5000000ull ? v.idle_ticks : 5000000ull;
         for (uint32_t base = 0; base < n && ok; base += 64) {
             const uint32_t i = base + lane;
             uint32_t x = 0;
             while (true) {
                 if (i < n) x = __hip_atomic_load(v.xcc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (__all(i >= n || (x >> 4) == tag)) break;
-                if (wall_clock64() - t0 > v.idle_ticks) {
+                if (wall_clock64() - t0 > limit) {
                     ok = false;
                     break;
                 }

@@ -287,10 +287,11 @@ class Engine:
     def set_fused(self, enable: bool) -> None:
         check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
-    def set_service(self, enable: bool) -> None:
+    def set_service(self, enable: bool, parked: bool = False) -> None:
         """Resident placement service for host-API placements
-        (jsp_engine_set_service; on by default)."""
-        mode = native.JSP_SERVICE_AUTO if enable else native.JSP_SERVICE_OFF
+        (jsp_engine_set_service; on by default). parked: it never idles out
+        (JSP_SERVICE_PARKED, a dedicated GPU)."""
+        mode = (native.JSP_SERVICE_PARKED if parked else native.JSP_SERVICE_AUTO) if enable else native.JSP_SERVICE_OFF
         check(self._lib.jsp_engine_set_service(self._h, mode))
 
     def service_stop(self) -> None:

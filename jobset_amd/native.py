@@ -55,7 +55,7 @@ class JspTiming(ctypes.Structure):
 
 
 JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
-JSP_SERVICE_OFF, JSP_SERVICE_AUTO = 0, 1
+JSP_SERVICE_OFF, JSP_SERVICE_AUTO, JSP_SERVICE_PARKED = 0, 1, 2
 
 
 # (name, restype, argtypes) — every entry point declared in include/jsplace.h

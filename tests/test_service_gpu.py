@@ -710,3 +710,44 @@ def test_micro_patches_ride_in_the_request(svc_engine, cfg, then):
     np.testing.assert_array_equal(got.assign, a)
     np.testing.assert_array_equal(got.cap, cap)
     np.testing.assert_array_equal(got.occ, occ)
+
+
+@pytest.mark.parametrize("cfg", [2, 5])
+def test_parked_service_survives_idle_gaps(svc_engine, cfg):
+    """JSP_SERVICE_PARKED: no idle exit. Gaps of several idle limits, a
+    one-row patch before each place (it rides in the request), an upload
+    (the service restarts parked), then a stop and a device-wide synchronize
+    that returns at once. Bit-exact against the oracle throughout."""
+    import torch
+    p = synth.CONFIGS[cfg]()
+    try:
+        svc_engine.set_service(True, parked=True)
+        svc_engine.load(p)
+        np.testing.assert_array_equal(warm(svc_engine, p.job_class).assign, O.place_c(p)[0])
+        svc_engine.timing(reset=True)
+        rng = np.random.default_rng(cfg)
+        for gap in (0.12, 0.2, 0.0, 0.15):
+            time.sleep(gap)
+            row = np.array([rng.integers(0, p.nodes.n_nodes)], dtype=np.uint32)
+            val = np.array([rng.integers(0, 4)], dtype=np.uint32)
+            svc_engine.patch_rows(row, taints=val)
+            p.nodes.taints[row] = val
+            got = svc_engine.place(p.job_class)
+            assert got.fused in (3, 5)
+            np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+        t = svc_engine.timing(reset=True)
+        assert t.svc_starts == 0, "a parked service never idles out"
+        assert t.svc_calls == 4
+        q = synth.CONFIGS[cfg](trial=1)
+        svc_engine.load(q)
+        time.sleep(0.12)
+        got = svc_engine.place(q.job_class)
+        assert got.fused in (3, 5)
+        np.testing.assert_array_equal(got.assign, O.place_c(q)[0])
+        svc_engine.service_stop()
+        t0 = time.perf_counter()
+        torch.cuda.synchronize()
+        assert time.perf_counter() - t0 < 1.0
+    finally:
+        svc_engine.service_stop()
+        svc_engine.set_service(True)

@@ -7,7 +7,8 @@ path before the request post (svc_pre: a queued wake, settling the warm-up
 request, patch bookkeeping) and from the post to the answer (svc_answer), the
 Python/ctypes remainder, and the second (warm) placement. The library is the
 product one, or another build through JSP_LIB_PATH (tools/bin/ab_inlinewake:
-the wake inside the patch call)."""
+the wake inside the patch call); a third argument "parked" keeps the
+service on the GPU through the idle period (JSP_SERVICE_PARKED)."""
 import os
 import sys
 import time
@@ -32,8 +33,11 @@ def wait(seconds, spin):
 
 trials = int(sys.argv[1]) if len(sys.argv) > 1 else 20
 cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 2
-tag = os.path.basename(os.path.dirname(os.environ.get("JSP_LIB_PATH", ""))) or "product"
+parked = len(sys.argv) > 3 and sys.argv[3] == "parked"  # JSP_SERVICE_PARKED: no idle exit
+tag = os.path.basename(os.path.dirname(os.environ.get("JSP_LIB_PATH", ""))) or ("parked" if parked else "product")
 e = Engine(0)
+if parked:
+    e.set_service(True, parked=True)
 p = synth.CONFIGS[cfg]()
 e.load(p)
 call = e.host_placer(*job_runs(p.job_class))
