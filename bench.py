@@ -273,18 +273,35 @@ def _pcts(lat):
 COLD_GAPS_MS = (0.0, 1.0, 10.0)
 
 
+def _recovery_rows(p, trials: int, gap: float):
+    rows = np.array([(t * 7919 + int(gap * 13)) % max(p.nodes.n_nodes, 1) for t in range(trials)], dtype=np.uint32)
+    return rows, np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)  # same values: the snapshot is unchanged
+
+
+def _recovery_line(out):
+    tot = out[:, 0] + out[:, 1]
+    line = _pcts(tot.tolist())
+    line.update({"patch_p50_us": _pcts(out[:, 0].tolist())["p50_us"], "patch_p99_us": _pcts(out[:, 0].tolist())["p99_us"],
+                 "place_p50_us": _pcts(out[:, 1].tolist())["p50_us"], "place_p99_us": _pcts(out[:, 1].tolist())["p99_us"],
+                 "gap_ms_p50": round(float(np.median(out[:, 2])) * 1e-3, 3)})
+    return line
+
+
 def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
     """The realistic recovery (failures are hours apart,
     keps/262-ConfigurableFailurePolicy/README.md:232-234): the resident
-    service has idle-exited (the host sleeps past JSP_SERVICE_IDLE_MS), a
+    service has idle-exited (the caller sleeps past JSP_SERVICE_IDLE_MS), a
     watch event patches one row (the failed job's node back to schedulable),
     then the recreate calls jsp_place. Timed: the patch call plus the place
-    call (host wall). Between them a gap: 0 (the place right behind the patch)
-    or the time the reconciler needs before it recreates -- the deletions
-    that produce the patches are foreground deletes whose completion triggers
-    the recreate (pkg/controllers/jobset_controller.go:553-576, 698-709), at
-    least one API-server round trip (1 and 10 ms here); the gap itself is not
-    counted. The patch wakes the service (jsp_snapshot_patch, ABI v5)."""
+    call. Between them a gap: 0 (the place right behind the patch) or the time
+    the reconciler needs before it recreates -- the deletions that produce the
+    patches are foreground deletes whose completion triggers the recreate
+    (pkg/controllers/jobset_controller.go:553-576, 698-709), at least one
+    API-server round trip (1 and 10 ms here); the gap itself is not counted.
+    The patch wakes the service (jsp_snapshot_patch, ABI v5). The trials run
+    in C (jsp_recovery_loop: sleep, patch, gap, place, each call timed by the
+    library's clock), as a cgo caller would make the calls -- no interpreter
+    waking up between them."""
     from jobset_amd.snapshot import job_runs
     if trials <= 0:
         return None
@@ -293,43 +310,27 @@ def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
     call()
     out = {}
     for gap in gaps_ms:
-        tot, pat, pla, gaps, shapes = [], [], [], [], {}
-        for t in range(trials):
-            row = np.array([(t * 7919 + int(gap * 13)) % max(p.nodes.n_nodes, 1)], dtype=np.uint32)
-            patch = eng.host_patcher(row, taints=p.nodes.taints[row])  # same value: the snapshot is unchanged
-            time.sleep((idle_ms + 10.0) * 1e-3)
-            t0 = time.perf_counter()
-            patch()
-            t1 = time.perf_counter()
-            if gap > 0:
-                time.sleep(gap * 1e-3)
-            t2 = time.perf_counter()
-            st = call()
-            t3 = time.perf_counter()
-            tot.append(((t1 - t0) + (t3 - t2)) * 1e6)
-            pat.append((t1 - t0) * 1e6)
-            pla.append((t3 - t2) * 1e6)
-            gaps.append((t2 - t1) * 1e3)
-            shapes[int(st.fused)] = shapes.get(int(st.fused), 0) + 1
-        line = _pcts(tot)
-        line.update({"patch_p50_us": _pcts(pat)["p50_us"], "patch_p99_us": _pcts(pat)["p99_us"],
-                     "place_p50_us": _pcts(pla)["p50_us"], "place_p99_us": _pcts(pla)["p99_us"],
-                     "gap_ms_p50": round(float(np.median(gaps)), 3),
-                     "shapes": {str(k): v for k, v in sorted(shapes.items())}})
+        rows, vals = _recovery_rows(p, trials, gap)
+        eng.timing(reset=True)
+        res = call.recovery(trials, (idle_ms + 10.0) * 1e3, gap * 1e3, rows, vals)
+        t = eng.timing(reset=True)
+        line = _recovery_line(res)
+        line["answered_by_service"] = f"{int(t.svc_calls)}/{trials}"
         out[f"gap_{gap:g}ms"] = line
     out["note"] = (f"service idle-exited (sleep {idle_ms + 10:.0f} ms), then a one-row patch (jsp_snapshot_patch) and, "
-                   "after the stated gap, jsp_place; timed = patch call + place call (host wall), the gap excluded")
+                   "after the stated gap, jsp_place; timed = patch call + place call, the gap excluded; trials issued "
+                   "and timed in C (jsp_recovery_loop)")
     return out
 
 
 def cpu_cold_recovery(p, trials: int, threads, idle_ms: float, gaps_ms=COLD_GAPS_MS):
-    """The same recovery on the CPU evaluator, like for like with the GPU legs:
-    after the same idle sleep, the same one-row patch (written into the
-    evaluator's columns), the same gap (slept), then one placement; timed =
-    patch + placement, the gap excluded. Per gap, per thread count. (The
-    evaluator's pool threads spin between placements -- cpu_fast.c worker --
-    so its multi-thread legs start with hot workers: a CPU-favouring
-    baseline.)"""
+    """The same recovery on the CPU evaluator, like for like with the GPU legs
+    and, like them, timed in C (jspf_recovery_loop): after the same idle
+    sleep, the same one-row patch (written into the evaluator's columns), the
+    same gap (slept), then one placement; timed = patch + placement, the gap
+    excluded. Per gap, per thread count. (The evaluator's pool threads spin
+    between placements -- cpu_fast.c worker -- so its multi-thread legs start
+    with hot workers: a CPU-favouring baseline.)"""
     from oracle import oracle as O
     out = {}
     for gap in gaps_ms:
@@ -338,23 +339,10 @@ def cpu_cold_recovery(p, trials: int, threads, idle_ms: float, gaps_ms=COLD_GAPS
             fc = O.FastCPU(th)
             fc.prepare(p)
             fc.run()
-            taints = fc.pk.arrs["taints"]
-            lat = []
-            for t in range(trials):
-                row = (t * 7919 + int(gap * 13)) % max(p.nodes.n_nodes, 1)
-                v = int(taints[row])
-                time.sleep((idle_ms + 10.0) * 1e-3)
-                t0 = time.perf_counter()
-                taints[row] = v
-                t1 = time.perf_counter()
-                if gap > 0:
-                    time.sleep(gap * 1e-3)
-                t2 = time.perf_counter()
-                fc.run()
-                t3 = time.perf_counter()
-                lat.append(((t1 - t0) + (t3 - t2)) * 1e6)
+            rows, vals = _recovery_rows(p, trials, gap)
+            res = fc.recovery_loop(trials, (idle_ms + 10.0) * 1e3, gap * 1e3, rows, vals)
             fc.close()
-            legs[f"{th}t"] = _pcts(lat)
+            legs[f"{th}t"] = _pcts((res[:, 0] + res[:, 1]).tolist())
         out[f"gap_{gap:g}ms"] = legs
     return out
 
@@ -662,7 +650,7 @@ def main() -> None:
         cold2["cpu"] = cpu_cold_recovery(p, max(10, args.cold_trials // 2), sorted({1, 2, cpu_threads()}), idle_ms)
         cold2["cpu_note"] = ("oracle/cpu_fast.c like for like: the same idle sleep, the same one-row patch written into "
                              "its columns, the same slept gap, then one placement; timed = patch + placement, the gap "
-                             "excluded")
+                             "excluded; timed in C (jspf_recovery_loop)")
         cold2["vs_cpu"] = cold_vs_cpu(cold2, cold2["cpu"])
     # the same recovery with the service parked (JSP_SERVICE_PARKED: no idle
     # exit, a dedicated GPU -- the GPU side of the CPU pool's spinning threads)

@@ -272,6 +272,15 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
 int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                    int32_t* assign_out, uint32_t iters, const uint32_t* patch_rows, const uint32_t* patch_taints,
                    uint32_t n_patch, double* out_us);
+/* The realistic recovery timed in C (ABI v6), `trials` times: the idle period
+ * (idle_us, slept -- or spun when spin != 0), a one-row taint patch
+ * (patch_rows[t % n_patch] := patch_taints[t % n_patch]; the failed job's
+ * node back to schedulable), the gap (gap_us: the reconciler's round trips
+ * between the deletions and the recreate), then jsp_place. out_us[3t] = the
+ * patch call, [3t+1] = the place call, [3t+2] = the gap as it passed (us). */
+int jsp_recovery_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                      int32_t* assign_out, uint32_t trials, double idle_us, double gap_us, int spin,
+                      const uint32_t* patch_rows, const uint32_t* patch_taints, uint32_t n_patch, double* out_us);
 /* Same with one class id per job (run-length encoded on the host). */
 int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
                    int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);

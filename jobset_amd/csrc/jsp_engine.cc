@@ -2598,6 +2598,45 @@ int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run
     return JSP_OK;
 }
 
+// The idle period or gap of jsp_recovery_loop: slept, or spun (a busy caller).
+static void recovery_wait(double us, bool spin) {
+    if (us <= 0.0) return;
+    const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(us);
+    if (!spin) {
+        std::this_thread::sleep_until(end);
+        return;
+    }
+    while (std::chrono::steady_clock::now() < end) __builtin_ia32_pause();
+}
+
+int jsp_recovery_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                      int32_t* assign_out, uint32_t trials, double idle_us, double gap_us, int spin,
+                      const uint32_t* patch_rows, const uint32_t* patch_taints, uint32_t n_patch, double* out_us) {
+    if (trials == 0 || trials > 100000) return set_err(JSP_EINVAL, "trials %u out of range [1,100000]", trials);
+    if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
+    if (!(idle_us >= 0.0 && idle_us <= 1e7 && gap_us >= 0.0 && gap_us <= 1e7))
+        return set_err(JSP_EINVAL, "idle / gap out of range [0, 10 s]");
+    if (n_patch > 0 && (!patch_rows || !patch_taints)) return set_err(JSP_EINVAL, "patch rows / taints are NULL");
+    using clk = std::chrono::steady_clock;
+    const auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    for (uint32_t t = 0; t < trials; ++t) {
+        recovery_wait(idle_us, spin != 0);
+        const uint32_t k = n_patch ? t % n_patch : 0u;
+        const auto t0 = clk::now();
+        if (n_patch > 0)
+            if (int rc = jsp_snapshot_patch(e, patch_rows + k, 1, nullptr, patch_taints + k, nullptr, nullptr)) return rc;
+        const auto t1 = clk::now();
+        recovery_wait(gap_us, spin != 0);
+        const auto t2 = clk::now();
+        if (int rc = jsp_place(e, run_class, run_len, n_runs, assign_out, nullptr, nullptr, nullptr)) return rc;
+        const auto t3 = clk::now();
+        out_us[3 * t] = us(t0, t1);
+        out_us[3 * t + 1] = us(t2, t3);
+        out_us[3 * t + 2] = us(t1, t2);
+    }
+    return JSP_OK;
+}
+
 int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs, int32_t* assign_out,
                    uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (n_jobs > 0 && !job_class) return set_err(JSP_EINVAL, "job_class is NULL");

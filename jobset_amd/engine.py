@@ -191,6 +191,19 @@ class Engine:
             return st
         loop_out = np.zeros(3, dtype=np.float64)
 
+        def recovery(trials: int, idle_us: float, gap_us: float, patch_rows: np.ndarray, patch_taints: np.ndarray,
+                     spin: bool = False) -> np.ndarray:
+            """The cold recovery timed in C (jsp_recovery_loop): per trial the
+            idle wait, a one-row patch, the gap, jsp_place. [trials, 3] µs:
+            patch call, place call, gap."""
+            pr = np.ascontiguousarray(patch_rows, dtype=np.uint32)
+            pt = np.ascontiguousarray(patch_taints, dtype=np.uint32)
+            out = np.zeros((int(trials), 3), dtype=np.float64)
+            check(self._lib.jsp_recovery_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
+                                              int(trials), float(idle_us), float(gap_us), 1 if spin else 0, _p(pr),
+                                              _p(pt), int(pr.shape[0]), out.ctypes.data))
+            return out
+
         def loop(iters: int, patch_rows: Optional[np.ndarray] = None,
                  patch_taints: Optional[np.ndarray] = None) -> Tuple[float, float, float]:
             """`iters` calls back to back timed in C (jsp_place_loop), each
@@ -205,6 +218,7 @@ class Engine:
         call.assign = assign[:J]
         call.stats = st
         call.loop = loop
+        call.recovery = recovery
         call.keep = (rc, rl, assign, loop_out)
         return call
 

@@ -74,6 +74,8 @@ SIGNATURES = [
     ("jsp_place", ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
     ("jsp_place_jobs", ctypes.c_int, [vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
     ("jsp_place_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, u32, vp]),
+    ("jsp_recovery_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                         vp, vp, u32, vp]),
     ("jsp_tally_device", ctypes.c_int, [vp, vp, vp, u32, vp]),
     ("jsp_assign_device", ctypes.c_int, [vp, vp, vp, u32, vp, vp, u32, u32, vp, vp]),
     ("jsp_place_device", ctypes.c_int, [vp, vp, vp, u32, u32, vp, vp]),

@@ -423,3 +423,42 @@ double jspf_run_loop(jspf_ctx* x, int32_t* assign, uint32_t iters, const uint32_
     }
     return now_us() - t0;
 }
+
+/* The cold recovery timed in C, like the engine's jsp_recovery_loop: per
+ * trial the idle period (slept, or spun when spin != 0), a one-row write of
+ * vals[k] into the taint column (the watch event's patch), the gap, then one
+ * placement. out_us[3t] = the write, [3t+1] = the placement, [3t+2] = the gap
+ * as it passed. */
+static void wait_us(double us, int spin) {
+    if (us <= 0.0) return;
+    if (spin) {
+        const double end = now_us() + us;
+        while (now_us() < end) {
+        }
+        return;
+    }
+    struct timespec ts;
+    ts.tv_sec = (time_t)(us / 1e6);
+    ts.tv_nsec = (long)((us - (double)ts.tv_sec * 1e6) * 1e3);
+    while (nanosleep(&ts, &ts) != 0) {
+    }
+}
+
+void jspf_recovery_loop(jspf_ctx* x, int32_t* assign, uint32_t trials, double idle_us, double gap_us, int spin,
+                        const uint32_t* rows, const uint32_t* vals, uint32_t nrows, double* out_us) {
+    uint32_t* taints = (uint32_t*)x->p->taints;
+    for (uint32_t t = 0; t < trials; ++t) {
+        wait_us(idle_us, spin);
+        const uint32_t k = nrows ? t % nrows : 0u;
+        const double t0 = now_us();
+        if (nrows) __atomic_store_n(taints + rows[k], vals[k], __ATOMIC_RELEASE);
+        const double t1 = now_us();
+        wait_us(gap_us, spin);
+        const double t2 = now_us();
+        (void)jspf_run(x, assign, NULL, NULL);
+        const double t3 = now_us();
+        out_us[3 * t] = t1 - t0;
+        out_us[3 * t + 1] = t3 - t2;
+        out_us[3 * t + 2] = t2 - t1;
+    }
+}

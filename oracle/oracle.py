@@ -203,6 +203,10 @@ def fast_lib():
         f.jspf_run.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         f.jspf_run_loop.restype = ctypes.c_double
         f.jspf_run_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32]
+        f.jspf_recovery_loop.restype = None
+        f.jspf_recovery_loop.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_double,
+                                         ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32, ctypes.c_void_p]
         _fast = f
     return _fast
 
@@ -245,6 +249,18 @@ class FastCPU:
         r = None if rows is None else np.ascontiguousarray(rows, dtype=np.uint32)
         return float(self.lib.jspf_run_loop(self.h, _ptr(self.assign), int(iters), None if r is None else _ptr(r),
                                             0 if r is None else int(r.shape[0])))
+
+    def recovery_loop(self, trials: int, idle_us: float, gap_us: float, rows: np.ndarray, vals: np.ndarray,
+                      spin: bool = False) -> np.ndarray:
+        """The cold recovery timed in C (jspf_recovery_loop): per trial the
+        idle wait, a one-row taint write, the gap, one placement. Returns
+        [trials, 3] µs: write, placement, gap."""
+        r = np.ascontiguousarray(rows, dtype=np.uint32)
+        v = np.ascontiguousarray(vals, dtype=np.uint32)
+        out = np.zeros((int(trials), 3), dtype=np.float64)
+        self.lib.jspf_recovery_loop(self.h, _ptr(self.assign), int(trials), float(idle_us), float(gap_us),
+                                    1 if spin else 0, _ptr(r), _ptr(v), int(r.shape[0]), _ptr(out))
+        return out
 
     def close(self) -> None:
         if self.h:

@@ -751,3 +751,24 @@ def test_parked_service_survives_idle_gaps(svc_engine, cfg):
     finally:
         svc_engine.service_stop()
         svc_engine.set_service(True)
+
+
+@pytest.mark.parametrize("parked", [False, True])
+def test_recovery_loop_answers_exactly(svc_engine, parked):
+    """jsp_recovery_loop (the bench's C-timed cold recovery): idle sleeps past
+    the idle limit, one-row patches with the rows' own values, gaps; every
+    call succeeds, the last answer is the oracle's, and each trial's three
+    times are sane."""
+    p = synth.config2()
+    try:
+        svc_engine.set_service(True, parked=parked)
+        svc_engine.load(p)
+        call = svc_engine.host_placer(*job_runs(p.job_class))
+        call()
+        rows = np.array([(t * 7919) % p.nodes.n_nodes for t in range(4)], dtype=np.uint32)
+        out = call.recovery(4, 70_000.0, 1_000.0, rows, p.nodes.taints[rows])
+        np.testing.assert_array_equal(call.assign, O.place_c(p)[0])
+        assert out.shape == (4, 3) and (out[:, :2] > 0).all() and (out[:, 2] >= 900.0).all()
+    finally:
+        svc_engine.service_stop()
+        svc_engine.set_service(True)
