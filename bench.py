@@ -585,15 +585,17 @@ def main() -> None:
     if floor is not None and shape == 3:
         pre = tphase.svc_pre_us / n_calls
         ans = tphase.svc_answer_us / n_calls
+        first = tphase.svc_first_us / n_calls
         lib_us = (tphase.host_prep_us + tphase.host_wait_us) / n_calls
         dev = svc["request_us_device"] if svc else None
         breakdown = {"host_api_step_us": round(step_us, 2), "library_us": round(lib_us, 2),
                      "outside_library_us": round(step_us - lib_us, 2),
                      "svc_pre_us": round(pre, 2), "svc_answer_us": round(ans, 2),
+                     "svc_first_entry_us": round(first, 2), "first_to_last_entry_us": round(ans - first, 2),
                      "link_floor_p50_us": round(floor[0], 2), "device_request_us": dev,
                      "answer_beyond_floor_and_device_us": round(ans - floor[0] - dev, 2) if dev else None,
                      "note": "means over the timed calls (jsp_timing, host clock): svc_pre = library entry of the "
-                             "service path to the request post, svc_answer = post to the answer's last entry; the "
+                             "service path to the request post, svc_answer = post to the answer's last entry (svc_first_entry: to its first); the "
                              "floor is jsp_engine_link_floor's median round trip; device_request = the service's "
                              "in-kernel request time (stamps on, a separate leg)"}
 

@@ -162,6 +162,7 @@ typedef struct jsp_timing {
     double svc_pre_us;         /* service-answered jsp_place: entry of the service path to the request post
                                   (a queued wake, settling the previous request, patch bookkeeping) (ABI v6) */
     double svc_answer_us;      /* ... the request post to the answer's last entry seen (ABI v6) */
+    double svc_first_us;       /* ... the request post to its first answer entry seen (compaction service) */
     /* jsp_snapshot_patch (ABI v5), host wall clock, always accumulated */
     uint64_t patches;          /* patch calls with at least one row */
     double patch_us;           /* their host time (a waker-thread restart is not in it) */

@@ -334,6 +334,7 @@ struct jsp_engine {
         unsigned long long occ_key = ~0ull;   // (shape, LDS, grid) whose co-residency was last checked
         int occ_fit = 0;
         std::chrono::steady_clock::time_point last{};
+        std::chrono::steady_clock::time_point first_seen{};  // the current request's first answer entry (svc_wait_entries)
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
     Grave grave;  // buffers replaced while the service ran: freed when it stops
@@ -1226,6 +1227,7 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
     uint32_t i = 0, n = 0;
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
+        const uint32_t i0 = i;
         while (i < J) {
             const unsigned long long x = __atomic_load_n(a + i, __ATOMIC_ACQUIRE);
             if ((uint32_t)(x >> 32) != seq) break;
@@ -1233,6 +1235,7 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
             out[i++] = d;
             n += d >= 0 ? 1u : 0u;
         }
+        if (i0 == 0 && i > 0) v.first_seen = std::chrono::steady_clock::now();
         if (i == J) {
             *placed = n;
             return JSP_OK;
@@ -1562,6 +1565,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         break;
     }
     e->acc.svc_answer_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_post).count();
+    if (early && J > 0) e->acc.svc_first_us += std::chrono::duration<double, std::micro>(v.first_seen - t_post).count();
     if (v.clk && v.nb > 0) {
         // the request's device time: first tile saw it -> last tile drained
         const uint32_t* clk = v.words.as<uint32_t>() + v.nb + 3;

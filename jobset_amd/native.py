@@ -50,7 +50,7 @@ class JspTiming(ctypes.Structure):
                 ("host_post_us", ctypes.c_double), ("svc_calls", ctypes.c_uint64), ("svc_starts", ctypes.c_uint64),
                 ("svc_us", ctypes.c_double), ("svc_fallbacks", ctypes.c_uint64),
                 ("svc_ready_us", ctypes.c_double), ("svc_pre_us", ctypes.c_double),
-                ("svc_answer_us", ctypes.c_double), ("patches", ctypes.c_uint64), ("patch_us", ctypes.c_double),
+                ("svc_answer_us", ctypes.c_double), ("svc_first_us", ctypes.c_double), ("patches", ctypes.c_uint64), ("patch_us", ctypes.c_double),
                 ("wake_us", ctypes.c_double)]
 
 
