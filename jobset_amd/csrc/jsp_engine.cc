@@ -1522,7 +1522,8 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     }
     // the compaction answer is read from its tagged entries (timing on: the
     // done words, which carry the per-tile stamps)
-    const bool early = shape == 2 && J > 0 && !e->timing;
+    // (timing on too: the stamps are read once the tiles' done words are in)
+    const bool early = shape == 2 && J > 0;
     uint32_t seq = 0, n_early = 0;
     std::chrono::steady_clock::time_point t_post{};
     for (int attempt = 0;; ++attempt) {
@@ -1567,6 +1568,10 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     e->acc.svc_answer_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t_post).count();
     if (early && J > 0) e->acc.svc_first_us += std::chrono::duration<double, std::micro>(v.first_seen - t_post).count();
     if (v.clk && v.nb > 0) {
+        if (early) {  // the tiles' stamps land with their done words
+            v.pending = seq;
+            if (int rc = svc_settle(e)) return rc;
+        }
         // the request's device time: first tile saw it -> last tile drained
         const uint32_t* clk = v.words.as<uint32_t>() + v.nb + 3;
         const uint32_t ref = clk[0];

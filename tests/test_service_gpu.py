@@ -772,3 +772,35 @@ def test_recovery_loop_answers_exactly(svc_engine, parked):
     finally:
         svc_engine.service_stop()
         svc_engine.set_service(True)
+
+
+@pytest.mark.parametrize("rep", range(2))
+def test_patch_kernel_after_dispatcher_patches(svc_engine, rep):
+    """The round-4 red run (`snapshot patch 7 ended without its completion
+    word`): patches the dispatcher applies must not advance the
+    patch kernel's completion target. Dispatcher-applied, micro, waker-applied
+    and patch-kernel patches alternate on one engine -- with the service up,
+    idle-exited, switched off, and patched right at half the idle limit (the
+    posted-versus-idle-exit edge) -- and every later reader sees every patch."""
+    p = synth.config2()
+    svc_engine.load(p)
+    rng = np.random.default_rng(100 + rep)
+    warm(svc_engine, p.job_class)
+    for step in range(12):
+        mode = step % 4
+        if mode == 1:
+            time.sleep(0.08)  # idle-exited: the waker restarts it
+        elif mode == 2:
+            svc_engine.set_service(False)  # the patch kernel applies the next patch
+        elif mode == 3:
+            time.sleep(0.025)  # at half the idle limit: posted, or handed to the patch kernel
+        n = int(rng.choice([1, 3, 300, 5000]))
+        rows = np.sort(rng.choice(p.nodes.n_nodes, size=n, replace=False)).astype(np.uint32)
+        taints = rng.integers(0, 2, size=n).astype(np.uint32)
+        svc_engine.patch_rows(rows, taints=taints)
+        p.nodes.taints[rows] = taints
+        got = svc_engine.place(p.job_class)
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+        if mode == 2:
+            svc_engine.set_service(True)
+    svc_engine.sync()
