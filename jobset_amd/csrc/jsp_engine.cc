@@ -297,6 +297,7 @@ struct jsp_engine {
     // call records ev_last on it before returning, and later calls wait on
     // that engine-owned event (the caller may destroy its stream meanwhile).
     hipStream_t last_stream = nullptr;  // compared, never used after its call returned
+    bool foreign_pending = false;       // device-path work on a caller's stream not yet waited for (ev_last)
     bool have_last = false;
     bool last_foreign = false;          // the last call enqueued on a caller's stream
     hipEvent_t ev_switch = nullptr;     // recorded on the engine stream
@@ -424,6 +425,7 @@ int leave_stream(jsp_engine* e, hipStream_t s) {
     e->last_stream = s;
     e->have_last = true;
     e->last_foreign = s != e->stream;
+    e->foreign_pending = e->last_foreign;
     if (e->last_foreign && !launched) HIP_TRY(hipEventRecord(e->ev_last, s));
     return JSP_OK;
 }
@@ -2131,6 +2133,13 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
     for (uint32_t i = 0; i < n; ++i)
         if (rows[i] >= e->N) return set_err(JSP_EINVAL, "row %u out of range (%u rows)", rows[i], e->N);
     run_wake(e);  // an earlier patch's wake still queued: run it (that patch then goes to the service)
+    // A patch the service's dispatcher applies is not stream-ordered: device-
+    // path work still in flight on a caller's stream (it may be reading the
+    // rows) finishes first. (The patch kernel is ordered by the stream.)
+    if (e->foreign_pending) {
+        HIP_TRY(hipEventSynchronize(e->ev_last));
+        e->foreign_pending = false;
+    }
     const uint32_t fl = (labels ? jsp::kPatchLab : 0u) | (taints ? jsp::kPatchTaint : 0u) |
                         (free_res ? jsp::kPatchFree : 0u) | (excl_owner ? jsp::kPatchExcl : 0u);
     // A patch small enough to ride in the next request's line, while the
