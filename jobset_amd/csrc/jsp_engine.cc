@@ -152,6 +152,8 @@ struct TestHooks {
                                     //   write-through protocol a partition mode would run)
     uint32_t seq0 = 0;              // seq0=N: the service's first request number
     bool have_seq0 = false;
+    bool svc_entries = false;       // svc_entries=1: the compaction service answers with per-job entries
+                                    //   after a look-back instead of tile bitmaps (A/B)
 };
 
 TestHooks read_hooks() {
@@ -178,6 +180,7 @@ TestHooks read_hooks() {
         else if (k == "wait_us") h.wait_ticks = v * 100ull;
         else if (k == "cu_limit") h.cu_limit = (int)v;
         else if (k == "svc_xcd") h.svc_xcd = v != 0;
+        else if (k == "svc_entries") h.svc_entries = v != 0;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -312,6 +315,7 @@ struct jsp_engine {
         HostBuf box;     // request: [0] (J << 32) | seq, [1] (n_runs << 32) | seq; u32 [8] ready
         HostBuf words;   // done[nb] | stats[2] | err[1] | clk[kSvcClkSlots nb]
         HostBuf assign;  // [cap]
+        HostBuf bits;    // compaction: the bitmap answer, one 64-byte line per tile (ServiceArgs::bits)
         DevBuf granules; // compaction granules | bell, one 128-B line each after the granules | XCC votes
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
         HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
@@ -336,6 +340,7 @@ struct jsp_engine {
         int occ_fit = 0;
         std::chrono::steady_clock::time_point last{};
         std::chrono::steady_clock::time_point first_seen{};  // the current request's first answer entry (svc_wait_entries)
+        bool bitmap = false;  // compaction answers with tile bitmaps (ServiceArgs::bits)
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
     Grave grave;  // buffers replaced while the service ran: freed when it stops
@@ -1007,6 +1012,10 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
         }
         HIP_TRY(v.words.reserve(nw * 4));
         std::memset(v.words.p, 0, nw * 4);  // done words: seq 0 is never posted
+        if (shape == 2) {
+            HIP_TRY(v.bits.reserve((size_t)64 * std::max<uint32_t>(n_tiles, 1)));
+            std::memset(v.bits.p, 0, (size_t)64 * std::max<uint32_t>(n_tiles, 1));  // tags: seq 0 is never posted
+        }
         v.layout_key = lkey;
     }
     HIP_TRY(v.box.reserve(kBoxBytes));
@@ -1057,6 +1066,10 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     a.pods = e->cls_h[0].pods;
     a.seq0 = v.seq;
     a.assign = v.assign.as<int32_t>();
+    // the bitmap answer (test hook svc_entries=1: the per-job entries after a
+    // look-back, for A/B runs)
+    v.bitmap = shape == 2 && !e->hooks.svc_entries;
+    a.bits = v.bitmap ? v.bits.as<unsigned long long>() : nullptr;
     a.done = w;
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;
@@ -1255,6 +1268,60 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
                 }
                 *placed = n;
                 return JSP_OK;
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
+        }
+    }
+}
+
+// The compaction service's bitmap answer (ServiceArgs::bits): tile t's line
+// holds its leaves' feasibility as four 64-leaf words, each as two (seq << 32
+// | 32 bits) halves. Tiles own consecutive leaf ranges in leaf order, so job
+// j's domain is the j-th feasible leaf: the host takes the lines in tile
+// order as they arrive, bit by bit, and returns once J jobs have a leaf or
+// every tile has answered (the rest get -1). The tiles' done words then only
+// gate the next request (svc_settle). kSvcGone: the service left.
+int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_t* placed) {
+    auto& v = e->svc;
+    const unsigned long long* b = v.bits.as<unsigned long long>();
+    const uint32_t n = v.nb, base = e->leaf_begin;
+    const uint32_t* l0 = e->blk_l0.data();
+    uint32_t t = 0, j = 0;
+    QueryPacer qp;
+    for (uint64_t spins = 1;; ++spins) {
+        while (t < n && j < J) {
+            const unsigned long long* L = b + 8u * t;
+            unsigned long long x[8];
+            uint32_t bad = 0;
+            for (int k = 0; k < 8; ++k) {
+                x[k] = __atomic_load_n(L + k, __ATOMIC_ACQUIRE);
+                bad |= (uint32_t)(x[k] >> 32) ^ seq;
+            }
+            if (bad) break;
+            if (t == 0) v.first_seen = std::chrono::steady_clock::now();
+            const uint32_t d0 = base + l0[t];
+            for (uint32_t w = 0; w < 4 && j < J; ++w) {
+                uint64_t m = (x[2 * w] & 0xFFFFFFFFull) | (x[2 * w + 1] << 32);
+                while (m != 0ull && j < J) {
+                    out[j++] = (int32_t)(d0 + 64u * w + (uint32_t)__builtin_ctzll(m));
+                    m &= m - 1ull;
+                }
+            }
+            ++t;
+        }
+        if (t == n || j == J) {
+            *placed = j;
+            for (uint32_t i = j; i < J; ++i) out[i] = -1;
+            return JSP_OK;
+        }
+        if ((spins & 255) == 0 && qp.due()) {
+            const hipError_t q = hipStreamQuery(v.stream);
+            if (q == hipSuccess) {  // it left: only a line already complete counts
+                const unsigned long long* L = b + 8u * t;
+                uint32_t bad = 0;
+                for (int k = 0; k < 8; ++k) bad |= (uint32_t)(__atomic_load_n(L + k, __ATOMIC_ACQUIRE) >> 32) ^ seq;
+                if (bad) return kSvcGone;
+                continue;
             }
             if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
         }
@@ -1551,7 +1618,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             e->acc.svc_pre_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
         }
         svc_request(e, seq, jw, w2, micro);
-        const int rc = early ? svc_wait_entries(e, seq, J, assign_out, &n_early) : svc_wait(e, seq, J);
+        const int rc = !early ? svc_wait(e, seq, J)
+                       : v.bitmap ? svc_wait_bits(e, seq, J, assign_out, &n_early)
+                                  : svc_wait_entries(e, seq, J, assign_out, &n_early);
         if (rc == kSvcFailed) {
             v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
             (void)svc_stop(e);
@@ -1611,7 +1680,8 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         const unsigned long long* a = v.assign.as<unsigned long long>();
         for (uint32_t j = 0; j < J; ++j) assign_out[j] = (int32_t)(uint32_t)a[j];
     }
-    *placed = __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
+    // (the bitmap answer writes no stats: it runs this path only for J = 0)
+    *placed = v.bitmap ? 0u : __atomic_load_n(w + v.nb + 1, __ATOMIC_ACQUIRE);
     // the copy-out's share of the wait (jsp_timing.host_post_us on this path)
     e->acc.host_post_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - tc).count();
     e->acc.svc_calls += 1;

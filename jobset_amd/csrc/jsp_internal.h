@@ -266,6 +266,11 @@ struct ServiceArgs {
     const char* pstage;                 // host-mapped inline patch staging (kReqPatchInline)
     uint32_t* pdone;                    // host-mapped: the applied patch's seq
     uint32_t* taken;                    // host-mapped: the seq of the request the dispatcher took last
+    // compaction shape: the bitmap answer -- per tile one 64-byte line of its
+    // leaves' feasibility (four 64-leaf ballots, each as two (seq << 32 |
+    // 32 bits) halves); the host gives job j the j-th feasible leaf. null: the
+    // per-job (seq << 32 | domain) entries in `assign` after a look-back.
+    unsigned long long* bits;
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

@@ -2860,13 +2860,32 @@ __device__ __forceinline__ void compact_finish(const TallyArgs& a, uint32_t tile
     }
 }
 
-// One compaction tile: tally its leaves (sums in LDS), then compact_finish.
+// The bitmap answer of the resident service (ServiceArgs::bits): the tile's
+// feasible leaves (thread t: leaf l0 + t) as four 64-leaf wave ballots, each
+// sent as two tagged halves (tag << 32 | 32 bits: one atomic 8-byte store
+// each) into the tile's own 64-byte line of pinned host memory. The host takes
+// the tiles' lines in order and gives job j the j-th feasible leaf -- no
+// look-back between tiles, no per-job scatter, one line per tile on the link.
+__device__ __forceinline__ void bitmap_finish(uint32_t tile, bool ok, uint32_t tag, unsigned long long* bits) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t word = __ballot(ok);
+    if (lane < 2) {
+        const uint32_t half = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
+        __hip_atomic_store(bits + 8u * tile + 2u * (uint32_t)wid + (uint32_t)lane,
+                           ((unsigned long long)tag << 32) | half, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+static_assert(kTallyThreads == 256, "bitmap_finish: four waves, eight halves per tile line");
+
+// One compaction tile: tally its leaves (sums in LDS), then compact_finish
+// (or bitmap_finish when `bits` is given: the resident service).
 template <int W, int R, bool STAGED = false>
 __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, uint4 bt, uint32_t epoch, uint32_t pods,
                                              uint32_t J, uint32_t n_runs, unsigned long long* g, uint32_t spin_limit,
                                              int32_t* assign, uint32_t* stats, uint32_t* err, bool sys, uint32_t* lds,
                                              uint32_t* s_x, JSP_LDS uint32_t* clk = nullptr, JSP_LDS u32x4* row_cache = nullptr,
-                                             bool use_cache = false, uint32_t tag = 0, bool local = false) {
+                                             bool use_cache = false, uint32_t tag = 0, bool local = false,
+                                             unsigned long long* bits = nullptr) {
     const int tid = threadIdx.x;
     // ends with the leaf sums in LDS (acc[0] cap, acc[1] occ)
     tally_block<W, R, STAGED>(a, tile, lds, bt, clk, row_cache, use_cache);
@@ -2877,7 +2896,8 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     const uint32_t* s_acc = lds + tally_acc_off(1);
     const uint32_t nl = bt.y - bt.x;
     const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
-    compact_finish(a, tile, bt.x, ok, epoch, J, n_runs, g, spin_limit, assign, stats, err, sys, s_x, clk, tag, local);
+    if (bits) bitmap_finish(tile, ok, tag, bits);
+    else compact_finish(a, tile, bt.x, ok, epoch, J, n_runs, g, spin_limit, assign, stats, err, sys, s_x, clk, tag, local);
 }
 
 template <int W, int R>
@@ -3369,12 +3389,14 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
                                                 lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
             svc_stamp(clk, 2);
-            compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
-                           v.stats, v.err, true, s_x, clk, next, local);
+            if (v.bits) bitmap_finish(tile, ok, next, v.bits);
+            else compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
+                                v.stats, v.err, true, s_x, clk, next, local);
             cached = true;
         } else {
             compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
-                                     v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local);
+                                     v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local,
+                                     v.bits);
             cached = row_cache != nullptr;
         }
         signal_host_clk(v.done + tile, next, clk, clk_out);

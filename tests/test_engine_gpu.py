@@ -563,7 +563,9 @@ def test_lookback_timeout_is_reported(engine, monkeypatch):
     p = synth.config4()
     p.classes = [p.classes[0]]
     p.job_class = np.zeros(30_000, dtype=np.uint32)
-    monkeypatch.setenv("JSP_TEST_HOOKS", "lookback_spins=0")  # read at snapshot upload
+    # read at snapshot upload; svc_entries=1: a resident compaction service
+    # answers through its look-back too (the per-job entry form, A/B)
+    monkeypatch.setenv("JSP_TEST_HOOKS", "lookback_spins=0,svc_entries=1")
     engine.load(p)
     with pytest.raises(JspError) as ei:
         for _ in range(5):  # ~1000 tiles: some tile always finds a predecessor unpublished

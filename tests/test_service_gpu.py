@@ -582,7 +582,8 @@ def test_no_stall_when_buffers_grow_under_the_service(svc_engine):
     assert svc_engine.timing(reset=True).svc_starts == 0
 
 
-@pytest.mark.parametrize("hooks", ["", "svc_xcd=0", "block_chunks=2", "svc_xcd=0,block_chunks=2"])
+@pytest.mark.parametrize("hooks", ["", "svc_xcd=0", "block_chunks=2", "svc_xcd=0,block_chunks=2", "svc_entries=1",
+                                   "svc_xcd=0,svc_entries=1", "block_chunks=2,svc_entries=1"])
 def test_service_colocated_and_spread(monkeypatch, hooks):
     """The compaction service co-located on one XCD (plain bell and granule
     stores when every workgroup votes the same XCC id) and spread over the
