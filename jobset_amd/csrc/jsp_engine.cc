@@ -1289,6 +1289,10 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
     uint32_t t = 0, j = 0;
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
+        // touch every line still to come (independent loads: their misses
+        // overlap), so a line that has landed is in cache when its turn comes
+        // -- not one miss after another in tile order
+        for (uint32_t u = t + 1; u < n; ++u) __builtin_prefetch(b + 8u * u, 0, 3);
         while (t < n && j < J) {
             const unsigned long long* L = b + 8u * t;
             unsigned long long x[8];

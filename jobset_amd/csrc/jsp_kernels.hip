@@ -2866,14 +2866,19 @@ __device__ __forceinline__ void compact_finish(const TallyArgs& a, uint32_t tile
 // each) into the tile's own 64-byte line of pinned host memory. The host takes
 // the tiles' lines in order and gives job j the j-th feasible leaf -- no
 // look-back between tiles, no per-job scatter, one line per tile on the link.
-__device__ __forceinline__ void bitmap_finish(uint32_t tile, bool ok, uint32_t tag, unsigned long long* bits) {
+// The four ballots meet in LDS (s_w: 8 words) and wave 0's lanes 0-7 write the
+// line with one store instruction: one whole-line write to host memory
+// instead of four partial ones (each a read-modify-write there, and a
+// snoop of the host's polling copy).
+__device__ __forceinline__ void bitmap_finish(uint32_t tile, bool ok, uint32_t tag, unsigned long long* bits,
+                                              uint32_t* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t word = __ballot(ok);
-    if (lane < 2) {
-        const uint32_t half = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
-        __hip_atomic_store(bits + 8u * tile + 2u * (uint32_t)wid + (uint32_t)lane,
-                           ((unsigned long long)tag << 32) | half, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (lane < 2) s_w[2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
+    __syncthreads();
+    if (wid == 0 && lane < 8)
+        __hip_atomic_store(bits + 8u * tile + (uint32_t)lane, ((unsigned long long)tag << 32) | s_w[lane],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 static_assert(kTallyThreads == 256, "bitmap_finish: four waves, eight halves per tile line");
 
@@ -2896,7 +2901,7 @@ __device__ __forceinline__ void compact_tile(const TallyArgs& a, uint32_t tile, 
     const uint32_t* s_acc = lds + tally_acc_off(1);
     const uint32_t nl = bt.y - bt.x;
     const bool ok = (uint32_t)tid < nl && s_acc[tid] >= pods && s_acc[a.la + tid] == 0;
-    if (bits) bitmap_finish(tile, ok, tag, bits);
+    if (bits) bitmap_finish(tile, ok, tag, bits, s_x + 4);
     else compact_finish(a, tile, bt.x, ok, epoch, J, n_runs, g, spin_limit, assign, stats, err, sys, s_x, clk, tag, local);
 }
 
@@ -3389,7 +3394,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
                                                 lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
             svc_stamp(clk, 2);
-            if (v.bits) bitmap_finish(tile, ok, next, v.bits);
+            if (v.bits) bitmap_finish(tile, ok, next, v.bits, s_x + 4);
             else compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
                                 v.stats, v.err, true, s_x, clk, next, local);
             cached = true;
