@@ -1279,9 +1279,12 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
 // | 32 bits) halves. Tiles own consecutive leaf ranges in leaf order, so job
 // j's domain is the j-th feasible leaf: the host takes the lines in tile
 // order as they arrive, bit by bit, and returns once J jobs have a leaf or
-// every tile has answered (the rest get -1). The tiles' done words then only
-// gate the next request (svc_settle). kSvcGone: the service left.
-int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_t* placed) {
+// every tile has answered (the rest get -1). kSvcGone: the service left.
+// *all: every tile's line arrived -- each tile then has read its rows and
+// holds no state of this request that a patch or the next request could
+// disturb, so neither waits for the tiles' done words (svc_settle); after an
+// answer complete before its last tiles, they do.
+int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_t* placed, bool* all) {
     auto& v = e->svc;
     const unsigned long long* b = v.bits.as<unsigned long long>();
     const uint32_t n = v.nb, base = e->leaf_begin;
@@ -1315,6 +1318,7 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
         }
         if (t == n || j == J) {
             *placed = j;
+            *all = t == n;
             for (uint32_t i = j; i < J; ++i) out[i] = -1;
             return JSP_OK;
         }
@@ -1598,6 +1602,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     // (timing on too: the stamps are read once the tiles' done words are in)
     const bool early = shape == 2 && J > 0;
     uint32_t seq = 0, n_early = 0;
+    bool all_tiles = false;
     std::chrono::steady_clock::time_point t_post{};
     for (int attempt = 0;; ++attempt) {
         if (restart) {
@@ -1623,7 +1628,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         }
         svc_request(e, seq, jw, w2, micro);
         const int rc = !early ? svc_wait(e, seq, J)
-                       : v.bitmap ? svc_wait_bits(e, seq, J, assign_out, &n_early)
+                       : v.bitmap ? svc_wait_bits(e, seq, J, assign_out, &n_early, &all_tiles)
                                   : svc_wait_entries(e, seq, J, assign_out, &n_early);
         if (rc == kSvcFailed) {
             v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
@@ -1666,7 +1671,7 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         return JSP_OK;
     }
     if (early) {
-        v.pending = seq;
+        v.pending = all_tiles ? 0u : seq;
         *placed = n_early;
         e->acc.svc_calls += 1;
         return JSP_OK;
