@@ -1308,10 +1308,20 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
             if (t == 0) v.first_seen = std::chrono::steady_clock::now();
             const uint32_t d0 = base + l0[t];
             for (uint32_t w = 0; w < 4 && j < J; ++w) {
+                // run by run: feasible leaves come in long runs (a word of 64
+                // is the common case), each written by a loop that vectorizes
                 uint64_t m = (x[2 * w] & 0xFFFFFFFFull) | (x[2 * w + 1] << 32);
+                const int32_t dw = (int32_t)(d0 + 64u * w);
                 while (m != 0ull && j < J) {
-                    out[j++] = (int32_t)(d0 + 64u * w + (uint32_t)__builtin_ctzll(m));
-                    m &= m - 1ull;
+                    const uint32_t s0 = (uint32_t)__builtin_ctzll(m);
+                    const uint64_t sh = m >> s0;
+                    const uint32_t r = ~sh == 0ull ? 64u - s0 : (uint32_t)__builtin_ctzll(~sh);
+                    const uint32_t take = std::min(r, J - j);
+                    int32_t* o = out + j;
+                    const int32_t d = dw + (int32_t)s0;
+                    for (uint32_t k = 0; k < take; ++k) o[k] = d + (int32_t)k;
+                    j += take;
+                    m = s0 + r >= 64u ? 0ull : m & (~0ull << (s0 + r));
                 }
             }
             ++t;
