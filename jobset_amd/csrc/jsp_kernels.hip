@@ -3404,12 +3404,22 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
                                      v.bits);
             cached = row_cache != nullptr;
         }
-        signal_host_clk(v.done + tile, next, clk, clk_out);
+        if (v.bits && !clk_out) {
+            // bitmap answer: the done word only says this tile is past its
+            // row reads (svc_settle), so it follows the line without waiting
+            // for the line's host write to complete -- a write to host memory
+            // takes a link round trip to retire, and the tile polls the bell
+            // for the next request right away instead
+            if (threadIdx.x == 0) __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            signal_host_clk(v.done + tile, next, clk, clk_out);
+        }
         // The host may patch the snapshot before its next request (another
         // launch): drop this CU's L1 lines now, off the request path -- no
         // snapshot load happens until the next request, which the host posts
-        // after the patch has finished.
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        // after the patch has finished. The invalidate alone: an acquire fence
+        // would first wait for this tile's posted host stores (vmcnt(0)).
+        if (threadIdx.x == 0) asm volatile("buffer_inv sc1" ::: "memory");
         seq = next;
         __syncthreads();  // s_x[16..17] and the tally carve are rewritten by the next request
     }
@@ -3550,7 +3560,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         signal_host_clk(v.done + tile, next, clk, clk_out);
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
-        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (threadIdx.x == 0) asm volatile("buffer_inv sc1" ::: "memory");  // no wait for the done word's store
         seq = next;
         __syncthreads();  // s_x and the tally carve are rewritten by the next request
     }
