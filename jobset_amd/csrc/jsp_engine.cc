@@ -154,6 +154,7 @@ struct TestHooks {
     bool have_seq0 = false;
     bool svc_entries = false;       // svc_entries=1: the compaction service answers with per-job entries
                                     //   after a look-back instead of tile bitmaps (A/B)
+    uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
 };
 
 TestHooks read_hooks() {
@@ -181,6 +182,7 @@ TestHooks read_hooks() {
         else if (k == "cu_limit") h.cu_limit = (int)v;
         else if (k == "svc_xcd") h.svc_xcd = v != 0;
         else if (k == "svc_entries") h.svc_entries = v != 0;
+        else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -2688,7 +2690,13 @@ int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run
     std::vector<double> us(iters);
     const auto t0 = std::chrono::steady_clock::now();
     auto tp = t0;
+    const auto gap = std::chrono::nanoseconds(e->hooks.loop_gap_ns);
     for (uint32_t i = 0; i < iters; ++i) {
+        if (gap.count() > 0) {  // test hook: a caller that does other work between calls
+            const auto until = std::chrono::steady_clock::now() + gap;
+            while (std::chrono::steady_clock::now() < until) __builtin_ia32_pause();
+            tp = std::chrono::steady_clock::now();
+        }
         if (n_patch > 0) {
             const uint32_t k = i % n_patch;
             if (int rc = jsp_snapshot_patch(e, patch_rows + k, 1, nullptr, patch_taints + k, nullptr, nullptr)) return rc;
