@@ -455,6 +455,39 @@ def relaunch_with_torchrun(n: int) -> int:
     return subprocess.run(cmd).returncode
 
 
+def bind_to_gpu_node(device: int):
+    """Run this rank's threads on the CPUs of its GPU's NUMA node (the
+    numactl --cpunodebind a latency-bound deployment uses; Kubernetes' topology
+    manager gives a GPU pod the same with its single-numa-node policy): every
+    host-API call polls pinned host memory the GPU writes, and a thread on the
+    other socket pays the cross-socket coherence on each line. The CPU
+    baseline legs run under the same binding. Returns what was done (or why
+    not) for the bench line."""
+    import ctypes
+    import glob
+    try:
+        hip = ctypes.CDLL("libamdhip64.so")
+        buf = ctypes.create_string_buffer(64)
+        if hip.hipDeviceGetPCIBusId(buf, 64, device) != 0:
+            return {"bound": False, "why": "hipDeviceGetPCIBusId failed"}
+        bdf = buf.value.decode().lower()
+        node = int(open(f"/sys/bus/pci/devices/{bdf}/numa_node").read())
+    except (OSError, ValueError) as ex:
+        return {"bound": False, "why": str(ex)}
+    if node < 0:
+        return {"bound": False, "gpu": bdf, "why": "no NUMA node reported"}
+    allowed = os.sched_getaffinity(0)
+    local = set()
+    for c in allowed:
+        g = glob.glob(f"/sys/devices/system/cpu/cpu{c}/node*")
+        if g and int(os.path.basename(g[0])[4:]) == node:
+            local.add(c)
+    if not local:
+        return {"bound": False, "gpu": bdf, "gpu_numa_node": node, "why": "none of the allowed CPUs is on that node"}
+    os.sched_setaffinity(0, local)
+    return {"bound": True, "gpu": bdf, "gpu_numa_node": node, "cpus": len(local), "of_allowed": len(allowed)}
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -501,6 +534,7 @@ def main() -> None:
     from jobset_amd.engine import Engine
     from jobset_amd.snapshot import job_runs
 
+    binding = bind_to_gpu_node(local)  # before the engine allocates its pinned buffers and threads
     stream = torch.cuda.current_stream().cuda_stream
     eng = Engine(local)
 
@@ -948,6 +982,7 @@ def main() -> None:
                          "note": "avg_us / median_us: events on the dispatch packets of back-to-back launches "
                                  "(jsp_place_device_timed, the engine stream); event_loop_us: HIP events around "
                                  "ctypes-issued launches. Latency-bound: one launch moving 0.43 MB; DESIGN.md §8"},
+            "host_binding": binding,
             "timed_loop": "the K timed steps are jsp_place calls issued and timed from C (jsp_place_loop), as a cgo "
                           "caller's loop would issue them; the same K steps from a Python loop (one ctypes call "
                           "each) are python_loop_us_per_step",
