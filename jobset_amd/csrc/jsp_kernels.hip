@@ -3121,9 +3121,6 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                         __hip_atomic_store(dc + 1, patch ? 0u : (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_SYSTEM);
                     }
-                    // the host learns that a request with a patch was taken (a
-                    // later request then need not carry the patch again)
-                    if (patch && lane == 0) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                     if (lane == 1) {
                         s_p[1] = jw;
                         s_p[3] = w2;
@@ -3163,6 +3160,12 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                 else service_apply_patch(v, a);
                 if (threadIdx.x == 0) s_p[7] = pseq;
             }
+            // the host learns that a request with a patch was taken (a later
+            // request then need not carry the patch again). Stored after the
+            // apply: the apply waits for its own row stores (vmcnt), and a
+            // host store issued before them would put a link round trip into
+            // that wait
+            if (threadIdx.x == 0) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
                 const unsigned long long mm =
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
