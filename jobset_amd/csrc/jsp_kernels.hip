@@ -3059,7 +3059,8 @@ __device__ void service_apply_micro(const ServiceArgs& v, const TallyArgs& a, co
 
 // The dispatcher's LDS words (s_p): [0] claimed request seq [1] J word [2]
 // stop [3] second request word [4] micro rows [5] patch number [6] column
-// flags [7] last applied patch number [8 .. 8 + kMailboxPayload) micro words.
+// flags [7] last applied patch number [8 .. 8 + kMailboxPayload) micro words
+// [8 + kMailboxPayload] the request's seen stamp (timing on).
 __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const TallyArgs& a, uint32_t* s_p,
                                                  bool local = false) {
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3116,10 +3117,16 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                         else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     if (v.clk && lane == 0) {  // timing on: the dispatcher's row after the tiles' (seen, rung)
-                        uint32_t* dc = v.clk + kSvcClkSlots * v.n_tiles;
-                        __hip_atomic_store(dc, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        __hip_atomic_store(dc + 1, patch ? 0u : (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                        if (patch) {
+                            // written after the apply: a host store here would sit in
+                            // the apply's wait for its row stores
+                            s_p[8 + kMailboxPayload] = t_seen;
+                        } else {
+                            uint32_t* dc = v.clk + kSvcClkSlots * v.n_tiles;
+                            __hip_atomic_store(dc, t_seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                            __hip_atomic_store(dc + 1, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_SYSTEM);
+                        }
                     }
                     if (lane == 1) {
                         s_p[1] = jw;
@@ -3171,9 +3178,13 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
                 if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (v.clk)
-                    __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles + 1, (uint32_t)wall_clock64(), __ATOMIC_RELAXED,
+                if (v.clk) {
+                    const uint32_t t_rung = (uint32_t)wall_clock64();
+                    __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles, s_p[8 + kMailboxPayload], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles + 1, t_rung, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                }
             }
         }
         seq = q;
@@ -3881,7 +3892,7 @@ uint32_t service_row_cache_words(uint32_t la) { return (uint32_t)((compact_lds_b
 
 size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache) {
     // + the dispatcher's words past the compaction's (service_dispatch s_p: 8 + kMailboxPayload after s_x[16])
-    if (!row_cache) return compact_lds_bytes(la) + sizeof(uint32_t) * (8 + kMailboxPayload);
+    if (!row_cache) return compact_lds_bytes(la) + sizeof(uint32_t) * (8 + kMailboxPayload + 2);
     return sizeof(uint32_t) * service_row_cache_words(la) + (size_t)(2 * W + 2 + R) * 16 * kTallyThreads;
 }
 
