@@ -3024,37 +3024,38 @@ __device__ void service_apply_inline(const ServiceArgs& v, const TallyArgs& a, u
 // distinct); one thread per word stores it (agent scope: the tiles' sc1
 // reloads find it in L2), every store drains, and thread 0 publishes the
 // patch number. No host-link round trip beyond the request's own.
-__device__ void service_apply_micro(const ServiceArgs& v, const TallyArgs& a, const uint32_t* s_w, uint32_t m,
-                                    uint32_t fl, uint32_t pseq) {
+// A micro-patch's row stores (the rows ride in the request line, s_w). `plain`:
+// the co-located service -- plain stores that stay in this XCD's L2, where the
+// tiles' sc1 reloads find them, retired in an L2 round trip; otherwise
+// write-through (agent scope), which retires only once the memory side has the
+// data. Each thread stores one word; the barrier ends with every store retired.
+__device__ void service_micro_stores(const TallyArgs& a, const uint32_t* s_w, uint32_t m, uint32_t fl, bool plain) {
     const uint32_t W = (uint32_t)a.W, R = (uint32_t)a.R, rw = 3u + 2u * W + R;
     const uint32_t t = threadIdx.x;
     if (t < m * rw) {
         const uint32_t r = t / rw, k = t - r * rw;
         const uint32_t row = s_w[r * rw], val = s_w[t];
+        uint32_t* p = nullptr;
         if (k == 0u || row >= a.npad) {
             // the row id itself
         } else if (k <= 2u * W) {
-            if (fl & kPatchLab) {
-                uint32_t* lab =
-                    reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(a.labels) + (size_t)((k - 1) >> 1) * a.npad + row);
-                __hip_atomic_store(lab + ((k - 1) & 1u), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (fl & kPatchLab)
+                p = reinterpret_cast<uint32_t*>(const_cast<uint64_t*>(a.labels) + (size_t)((k - 1) >> 1) * a.npad + row) +
+                    ((k - 1) & 1u);
         } else if (k == 2u * W + 1u) {
-            if (fl & kPatchTaint)
-                __hip_atomic_store(const_cast<uint32_t*>(a.taints) + row, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (fl & kPatchTaint) p = const_cast<uint32_t*>(a.taints) + row;
         } else if (k < 2u * W + 2u + R) {
-            if (fl & kPatchFree)
-                __hip_atomic_store(const_cast<uint32_t*>(a.freer) + (size_t)(k - 2u * W - 2u) * a.npad + row, val,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (fl & kPatchFree) p = const_cast<uint32_t*>(a.freer) + (size_t)(k - 2u * W - 2u) * a.npad + row;
         } else if (k == 2u * W + 2u + R) {
-            if (fl & kPatchExcl)
-                __hip_atomic_store(const_cast<int32_t*>(a.excl) + row, (int32_t)val, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (fl & kPatchExcl) p = reinterpret_cast<uint32_t*>(const_cast<int32_t*>(a.excl)) + row;
+        }
+        if (p) {
+            if (plain) __hip_atomic_store(p, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else __hip_atomic_store(p, val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(v.pdone, pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // The dispatcher's LDS words (s_p): [0] claimed request seq [1] J word [2]
@@ -3161,18 +3162,15 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             // a patch this dispatcher applied already (carried again by a
             // request posted before its completion word came back) is not
             // applied twice; each apply ends with a barrier and the completion word
-            if (pseq != s_p[7]) {
-                if (m > 0u) service_apply_micro(v, a, s_p + 8, m, fl, pseq);
+            const bool fresh = pseq != s_p[7];
+            if (fresh) {
+                // a micro-patch on a co-located service: into this XCD's L2
+                // first (the tiles reload from there), written through for
+                // every other reader after the bell
+                if (m > 0u) service_micro_stores(a, s_p + 8, m, fl, local);
                 else if (jw & kReqPatchInline) service_apply_inline(v, a, nr);
                 else service_apply_patch(v, a);
-                if (threadIdx.x == 0) s_p[7] = pseq;
             }
-            // the host learns that a request with a patch was taken (a later
-            // request then need not carry the patch again). Stored after the
-            // apply: the apply waits for its own row stores (vmcnt), and a
-            // host store issued before them would put a link round trip into
-            // that wait
-            if (threadIdx.x == 0) __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
                 const unsigned long long mm =
                     ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
@@ -3185,6 +3183,20 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                     __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles + 1, t_rung, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                 }
+            }
+            if (fresh && m > 0u) {
+                if (local) service_micro_stores(a, s_p + 8, m, fl, false);  // in memory for every other reader
+                // its completion word: readers other than this service's
+                // tiles (launches, uploads, jsp_engine_sync) wait for it
+                if (threadIdx.x == 0) __hip_atomic_store(v.pdone, pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            if (threadIdx.x == 0) {
+                if (fresh) s_p[7] = pseq;
+                // the host learns that a request with a patch was taken (a
+                // later request then need not carry the patch again); after
+                // the stores, whose retirement waits would otherwise include
+                // this host store's link round trip
+                __hip_atomic_store(v.taken, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         seq = q;
