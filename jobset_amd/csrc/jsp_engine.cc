@@ -868,6 +868,9 @@ bool split_ok(jsp_engine* e) {
     if (e->fused_mode != JSP_FUSED_AUTO || e->n_blocks == 0 || e->leaf_begin != 0 || e->n_leaves != e->L_total)
         return false;
     const uint32_t g = split_groups(e);
+    // an upper class's records carry its domain in 20 bits (jsp_internal.h SplitArgs)
+    for (uint32_t c = 0; c < e->C; ++c)
+        if (e->cls_h[c].level + 1 < e->K && e->D[e->cls_h[c].level] >= jsp::kSplitMaxDomains) return false;
     return e->n_blocks * g <= kSvcMaxBlocks && (e->C + g - 1) / g <= (uint32_t)jsp::kTallyClasses && e->C > 0;
 }
 
@@ -1007,7 +1010,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3 + jsp::kSvcClkSlots;  // + the dispatcher's clk row
     if (v.layout_key != lkey || !v.words.p || nw * 4 > v.words.bytes) {
         if (shape == 3) {
-            const size_t sb = (size_t)n_tiles * (v.cpg + 1) * jsp::kSplitSlot * 8;
+            const size_t sb = (size_t)n_tiles * jsp::split_tile_words(v.cpg) * 8;
             HIP_TRY(v.split.reserve(sb));
             std::memset(v.split.p, 0, sb);
             e->walk.set_tiles(e->blk_l0, e->blk_l1, v.groups, v.cpg);
@@ -1348,6 +1351,33 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
     }
 }
 
+// The split service's answer (jsp_internal.h SplitArgs): every tile's lines and
+// records carry the request, so the host takes tile after tile as each has
+// arrived whole -- touching the lines still to come every few polls, so
+// their misses overlap -- with no done word in between. kSvcGone: the
+// service left.
+int svc_wait_split(jsp_engine* e, uint32_t seq) {
+    auto& v = e->svc;
+    const uint64_t* s = v.split.as<uint64_t>();
+    const uint32_t n = v.nb;
+    uint32_t t = 0;
+    QueryPacer qp;
+    for (uint64_t spins = 1;; ++spins) {
+        while (t < n && e->walk.tile_ready(s, t, seq)) ++t;
+        if (t == n) return JSP_OK;
+        if ((spins & 7) == 1)
+            for (uint32_t u = t + 1; u < n; ++u) e->walk.prefetch_tile(s, u);
+        if ((spins & 255) == 0 && qp.due()) {
+            const hipError_t q = hipStreamQuery(v.stream);
+            if (q == hipSuccess) {  // it left: only tiles already complete count
+                while (t < n && e->walk.tile_ready(s, t, seq)) ++t;
+                return t == n ? JSP_OK : kSvcGone;
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
+        }
+    }
+}
+
 // The request number after q. Never 0 (the done words' initial value) or
 // kSvcStop, and never a value whose low 30 bits are 0: the compaction tiles
 // tag their look-back granules with seq & 0x3FFFFFFF (0 -> 1), so 2^30 would
@@ -1639,7 +1669,9 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             e->acc.svc_pre_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
         }
         svc_request(e, seq, jw, w2, micro);
-        const int rc = !early ? svc_wait(e, seq, J)
+        // (the split shape, timing off and J > 0: its tagged lines; with the
+        // stamps on, the done words, which follow the stamps)
+        const int rc = !early ? (v.shape == 3 && !v.clk && J > 0 ? svc_wait_split(e, seq) : svc_wait(e, seq, J))
                        : v.bitmap ? svc_wait_bits(e, seq, J, assign_out, &n_early, &all_tiles)
                                   : svc_wait_entries(e, seq, J, assign_out, &n_early);
         if (rc == kSvcFailed) {

@@ -3467,23 +3467,28 @@ __device__ __forceinline__ uint32_t leaf_ancestor(uint32_t leaf, uint32_t level,
 }
 
 __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
-                                           uint32_t* lds, uint32_t* s_x) {
+                                           uint32_t seq, uint32_t* lds, uint32_t* s_x) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nc = (int)ag.nc;
     JSP_LDS const DevClass* cls_l = lds_ptr(reinterpret_cast<const DevClass*>(lds));
     JSP_LDS const uint32_t* s_acc = lds_ptr(lds + tally_acc_off(nc));
     JSP_LDS uint32_t* s_pre = lds_ptr(s_x + 16);
+    // the tile's lines, gathered here and written by one pass of stores
+    JSP_LDS uint32_t* s_line = lds_ptr(s_x + 16 + kTallyThreads);
+    const uint32_t n_line = 8u * (sp.cpg + 1u);
+    if ((uint32_t)tid < n_line) s_line[tid] = 0u;
+    __syncthreads();
     const uint32_t la = ag.la;
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
     const bool in = (uint32_t)tid < nl;
     const uint32_t K = sp.topo.K;
+    const unsigned long long rtag = (unsigned long long)split_rec_tag(seq) << 50;
     for (int c = 0; c < nc; ++c) {
         const uint32_t level = to_sgpr(cls_l[c].level), pods = to_sgpr(cls_l[c].pods);
         const uint32_t cap = in ? s_acc[c * la + tid] : 0u;
-        uint64_t* slot = out + (size_t)c * kSplitSlot + (size_t)wid * kSplitWave;
         if (level + 1 == K) {
             const uint64_t word = __ballot(in && cap >= pods);
-            if (lane == 0) __hip_atomic_store(slot, (unsigned long long)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane < 2) s_line[8 * c + 2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
         } else {
             const uint32_t v = cap < pods ? cap : pods;
             uint32_t total;
@@ -3491,7 +3496,7 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
             s_pre[tid] = incl;
             __syncthreads();
             bool last = false;
-            uint64_t rec = 0;
+            unsigned long long rec = 0;
             if (in) {
                 const uint32_t l = l0 + (uint32_t)tid;
                 const uint32_t d = leaf_ancestor(l, level, sp.topo);
@@ -3499,23 +3504,24 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
                 last = (uint32_t)tid + 1 == nl || l + 1 == end;
                 const uint32_t first = (beg > l0 ? beg : l0) - l0;
                 const uint32_t partial = incl - (first > 0 ? s_pre[first - 1] : 0u);
-                rec = ((uint64_t)d << 32) | partial;
+                rec = rtag | ((unsigned long long)d << 30) | partial;
             }
             const uint64_t m = __ballot(last);
-            if (last) __hip_atomic_store(slot + 1 + mbcnt64(m), (unsigned long long)rec, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_SYSTEM);
-            if (lane == 0)
-                __hip_atomic_store(slot, (unsigned long long)__popcll(m), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            uint64_t* recs = out + n_line + ((size_t)c * 4 + wid) * kSplitRecs;
+            if (last) __hip_atomic_store(recs + mbcnt64(m), rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (lane == 0) s_line[8 * c + 2 * wid] = (uint32_t)__popcll(m);
             __syncthreads();  // s_pre and the scan scratch are rewritten by the next upper class
         }
     }
     if (ag.do_occ) {
         const uint32_t o = in ? s_acc[nc * la + tid] : 0u;
         const uint64_t word = __ballot(in && o != 0u);
-        if (lane == 0)
-            __hip_atomic_store(out + (size_t)sp.cpg * kSplitSlot + (size_t)wid * kSplitWave, (unsigned long long)word,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (lane < 2) s_line[8 * sp.cpg + 2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
     }
+    __syncthreads();
+    if ((uint32_t)tid < n_line)
+        __hip_atomic_store(out + tid, ((unsigned long long)seq << 32) | s_line[tid], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 template <int W, int R>
@@ -3535,7 +3541,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     ag.do_occ = ft.do_occ;
     ag.cap_out = nullptr;  // the sums stay in LDS
     const uint4 bt = a.blk[ft.blk];
-    uint64_t* out = sp.out + (size_t)tile * (sp.cpg + 1) * kSplitSlot;
+    uint64_t* out = sp.out + (size_t)tile * split_tile_words(sp.cpg);
     uint32_t seq = v.seq0;
     // the tile's rows stay in LDS between requests (as the compaction
     // service's; bit 63 of the bell: the snapshot was patched since the
@@ -3579,11 +3585,18 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
 #ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 2);
 #endif
-        split_emit(ag, sp, bt, out, lds, s_x);
+        split_emit(ag, sp, bt, out, next, lds, s_x);
 #ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 4);
 #endif
-        signal_host_clk(v.done + tile, next, clk, clk_out);
+        if (!clk_out) {
+            // the tagged lines are the answer; the done word only says this
+            // tile is past its row reads, so it follows without waiting for
+            // the lines' host writes to retire
+            if (threadIdx.x == 0) __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            signal_host_clk(v.done + tile, next, clk, clk_out);
+        }
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
         if (threadIdx.x == 0) asm volatile("buffer_inv sc1" ::: "memory");  // no wait for the done word's store
@@ -3865,7 +3878,9 @@ hipError_t launch_service(const TallyArgs& a, const ServiceArgs& v, hipStream_t 
 }
 
 size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
-    return sizeof(uint32_t) * ((size_t)tally_lds_words((int)cpg, (int)cpg + 1, (int)la) + 16 + kTallyThreads + 4);
+    // + s_x: [0..16) seq and scan scratch, [16, 16 + 256) prefixes, then the tile's line words
+    return sizeof(uint32_t) * ((size_t)tally_lds_words((int)cpg, (int)cpg + 1, (int)la) + 16 + kTallyThreads +
+                               8 * ((size_t)cpg + 1) + 4);
 }
 
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la) { return (uint32_t)((split_lds_bytes(cpg, la) + 15) / 16 * 4); }

@@ -39,6 +39,11 @@ public:
     // read one by one in the walk, the misses cost cfg3 ~3.9 us, cfg5 ~7.4 us).
     void prefetch_tile(const uint64_t* slots, uint32_t t) const;
 
+    // Tile t's answer to request seq has arrived whole: every entry of its
+    // lines carries seq and every record its wave counts carries the
+    // request's record tag (jsp_internal.h SplitArgs).
+    bool tile_ready(const uint64_t* slots, uint32_t t, uint32_t seq) const;
+
     // The feasibility bitmaps of the last request (tests / diagnostics):
     // words [woff[c], woff[c+1]) of class c.
     const std::vector<uint64_t>& feas() const { return feas_; }

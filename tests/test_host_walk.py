@@ -16,7 +16,24 @@ import pytest
 from jobset_amd import native, synth
 from oracle import oracle as O
 
-SLOT_WAVE, SLOT = 65, 4 * 65   # jsp_internal.h kSplitWave / kSplitSlot
+SPLIT_RECS = 64                 # jsp_internal.h kSplitRecs
+SEQ = 7                         # the request number the emulated tiles tag their answer with
+
+
+def tile_words(cpg):
+    """jsp_internal.h split_tile_words: (cpg + 1) lines of 8, then records."""
+    return 8 * (cpg + 1) + 4 * SPLIT_RECS * cpg
+
+
+def rec_tag(seq):
+    """jsp_internal.h split_rec_tag."""
+    return seq % 16383 + 1
+
+
+def put_word(slots, line, w, word, seq=SEQ):
+    """Wave w's ballot as the two tagged halves of a tile line."""
+    slots[line + 2 * w] = (seq << 32) | (word & 0xFFFFFFFF)
+    slots[line + 2 * w + 1] = (seq << 32) | (word >> 32)
 CHUNK_ROWS, MAX_BLK_LEAVES = 1024, 256
 
 
@@ -54,6 +71,9 @@ def ancestor(topo, leaf, level):
 
 
 def emulate_tiles(p, cap, occ):
+    """The split service's tiles (place_split_service_kernel split_emit), in
+    numpy: per tile, its tagged lines (ballots or record counts, occupancy)
+    and its upper classes' tagged records."""
     topo = p.topology
     K = topo.n_levels
     C = len(p.classes)
@@ -61,19 +81,23 @@ def emulate_tiles(p, cap, occ):
     nb = len(b0)
     groups = split_groups(C, nb)
     cpg = (C + groups - 1) // groups
-    slots = np.zeros(nb * groups * (cpg + 1) * SLOT, dtype=np.uint64)
+    tw = tile_words(cpg)
+    slots = np.zeros(nb * groups * tw, dtype=np.uint64)
     for b in range(nb):
         l0, l1 = b0[b], b1[b]
         nl = l1 - l0
         for g in range(groups):
             t = b * groups + g
-            base_t = t * (cpg + 1) * SLOT
+            base_t = t * tw
+            for j in range(cpg + 1):  # every line is written, tagged
+                for w in range(4):
+                    put_word(slots, base_t + 8 * j, w, 0)
             for j in range(cpg):
                 c = g * cpg + j
                 if c >= C:
                     break
                 jc = p.classes[c]
-                base = base_t + j * SLOT
+                line = base_t + 8 * j
                 capc = cap[c, l0:l1].astype(np.int64)
                 if jc.level + 1 == K:
                     ok = capc >= jc.pods
@@ -83,7 +107,7 @@ def emulate_tiles(p, cap, occ):
                             li = 64 * w + i
                             if li < nl and ok[li]:
                                 word |= 1 << i
-                        slots[base + w * SLOT_WAVE] = word
+                        put_word(slots, line, w, word)
                 else:
                     fl = topo.first_leaf[jc.level]
                     incl = np.cumsum(np.minimum(capc, jc.pods))
@@ -95,20 +119,21 @@ def emulate_tiles(p, cap, occ):
                         if li == nl - 1 or leaf + 1 == end:
                             first = max(beg, l0) - l0
                             part = int(incl[li] - (incl[first - 1] if first > 0 else 0))
-                            recs[li // 64].append((d << 32) | part)
+                            recs[li // 64].append((rec_tag(SEQ) << 50) | (d << 30) | part)
                     for w in range(4):
-                        slots[base + w * SLOT_WAVE] = len(recs[w])
+                        slots[line + 2 * w] = (SEQ << 32) | len(recs[w])
+                        rb = base_t + 8 * (cpg + 1) + (j * 4 + w) * SPLIT_RECS
                         for i, r in enumerate(recs[w]):
-                            slots[base + w * SLOT_WAVE + 1 + i] = r
+                            slots[rb + i] = r
             if g == 0:
-                base = base_t + cpg * SLOT
+                line = base_t + 8 * cpg
                 for w in range(4):
                     word = 0
                     for i in range(64):
                         li = 64 * w + i
                         if li < nl and occ[l0 + li] != 0:
                             word |= 1 << i
-                    slots[base + w * SLOT_WAVE] = word
+                    put_word(slots, line, w, word)
     return slots, (b0, b1), groups, cpg
 
 

@@ -22,7 +22,8 @@ def main():
     eng = Engine(0)
     fl = eng.link_floor(2000)
     print(f"host-link floor (jsp_engine_link_floor): p50 {fl[0]:.2f} us p99 {fl[1]:.2f}", flush=True)
-    for cfg in (1, 2):
+    cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2]
+    for cfg in cfgs:
         p = synth.CONFIGS[cfg]()
         eng.load(p)
         call = eng.host_placer(*job_runs(p.job_class))
@@ -48,7 +49,7 @@ def main():
                     ds = (d[0] - ref) * 10 if d[0] else 0
                     dr = (d[1] - ref) * 10 if d[1] else 0
                     phases.append([ds, dr] + [(c[:, k].max() - ref) * 10 for k in (0, 1, 6, 7, 2, 3, 4, 5)])
-                    if d[0]:
+                    if d[0] and tm.svc_first_us > 0:
                         # host: post -> first / last answer entry; device: the
                         # dispatcher saw the request -> tile 0 / the last tile
                         # drained. The difference is the two host-link hops.
