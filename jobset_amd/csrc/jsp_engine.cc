@@ -320,6 +320,7 @@ struct jsp_engine {
         HostBuf bits;    // compaction: the bitmap answer, one 64-byte line per tile (ServiceArgs::bits)
         DevBuf granules; // compaction granules | bell, one 128-B line each after the granules | XCC votes
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
+        std::vector<uint8_t> split_ready;  // svc_wait_split: tiles whose answer has arrived
         HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
         HostBuf pstage;  // inline patch staging (kReqPatchInline, jsp_internal.h), sized at snapshot upload
         uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
@@ -1361,12 +1362,17 @@ int svc_wait_split(jsp_engine* e, uint32_t seq) {
     const uint64_t* s = v.split.as<uint64_t>();
     const uint32_t n = v.nb;
     uint32_t t = 0;
+    // per pass, every tile not yet seen whole is checked: the checks are
+    // independent, so their line misses overlap instead of following one
+    // another in tile order
+    std::vector<uint8_t>& ready = v.split_ready;
+    ready.assign(n, 0);
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
-        while (t < n && e->walk.tile_ready(s, t, seq)) ++t;
+        for (uint32_t u = t; u < n; ++u)
+            if (!ready[u]) ready[u] = e->walk.tile_ready(s, u, seq) ? 1 : 0;
+        while (t < n && ready[t]) ++t;
         if (t == n) return JSP_OK;
-        if ((spins & 7) == 1)
-            for (uint32_t u = t + 1; u < n; ++u) e->walk.prefetch_tile(s, u);
         if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {  // it left: only tiles already complete count

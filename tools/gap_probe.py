@@ -13,9 +13,11 @@ from jobset_amd.engine import Engine  # noqa: E402
 from jobset_amd.snapshot import job_runs  # noqa: E402
 
 extra = sys.argv[1] if len(sys.argv) > 1 else ""
-p = synth.config2()
+cfg = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+p = synth.CONFIGS[cfg]()
+print(f"cfg{cfg}", end=" ")
 print(f"hooks: {extra or '-'}; floor", end=" ", flush=True)
-for gap in (0, 500, 1000, 2000, 3000, 5000, 0):
+for gap in (0, 1000, 3000, 6000, 10000, 0):
     os.environ["JSP_TEST_HOOKS"] = ",".join(x for x in (extra, f"loop_gap_ns={gap}") if x)
     e = Engine(0)
     if gap == 0 and extra == "":
