@@ -155,6 +155,7 @@ struct TestHooks {
     bool svc_entries = false;       // svc_entries=1: the compaction service answers with per-job entries
                                     //   after a look-back instead of tile bitmaps (A/B)
     uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
+    uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
 };
 
 TestHooks read_hooks() {
@@ -183,6 +184,7 @@ TestHooks read_hooks() {
         else if (k == "svc_xcd") h.svc_xcd = v != 0;
         else if (k == "svc_entries") h.svc_entries = v != 0;
         else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
+        else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -320,7 +322,6 @@ struct jsp_engine {
         HostBuf bits;    // compaction: the bitmap answer, one 64-byte line per tile (ServiceArgs::bits)
         DevBuf granules; // compaction granules | bell, one 128-B line each after the granules | XCC votes
         HostBuf split;   // split shape: the tiles' feasibility slots (jsp_internal.h SplitArgs)
-        std::vector<uint8_t> split_ready;  // svc_wait_split: tiles whose answer has arrived
         HostBuf pdesc;   // the patch descriptor its dispatcher reads (kReqPatch)
         HostBuf pstage;  // inline patch staging (kReqPatchInline, jsp_internal.h), sized at snapshot upload
         uint32_t groups = 1, cpg = 1;  // split shape: class groups of its tiles
@@ -1362,17 +1363,16 @@ int svc_wait_split(jsp_engine* e, uint32_t seq) {
     const uint64_t* s = v.split.as<uint64_t>();
     const uint32_t n = v.nb;
     uint32_t t = 0;
-    // per pass, every tile not yet seen whole is checked: the checks are
-    // independent, so their line misses overlap instead of following one
-    // another in tile order
-    std::vector<uint8_t>& ready = v.split_ready;
-    ready.assign(n, 0);
+    if (e->hooks.wait_delay_ns) {  // diagnostic: let the answer land before reading it
+        const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(e->hooks.wait_delay_ns);
+        while (std::chrono::steady_clock::now() < until) __builtin_ia32_pause();
+    }
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
-        for (uint32_t u = t; u < n; ++u)
-            if (!ready[u]) ready[u] = e->walk.tile_ready(s, u, seq) ? 1 : 0;
-        while (t < n && ready[t]) ++t;
+        while (t < n && e->walk.tile_ready(s, t, seq)) ++t;
         if (t == n) return JSP_OK;
+        if ((spins & 7) == 1)
+            for (uint32_t u = t + 1; u < n; ++u) e->walk.prefetch_tile(s, u);
         if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {  // it left: only tiles already complete count

@@ -11,6 +11,8 @@ from jobset_amd import synth  # noqa: E402
 from jobset_amd.engine import Engine  # noqa: E402
 from jobset_amd.snapshot import job_runs  # noqa: E402
 
+if len(sys.argv) > 1:
+    os.environ["JSP_TEST_HOOKS"] = sys.argv[1]
 e = Engine(0)
 fl = e.link_floor(2000)
 print(f"floor p50 {fl[0]:.2f} us", flush=True)
