@@ -1012,7 +1012,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     const size_t nw = (size_t)(1 + jsp::kSvcClkSlots) * n_tiles + 3 + jsp::kSvcClkSlots;  // + the dispatcher's clk row
     if (v.layout_key != lkey || !v.words.p || nw * 4 > v.words.bytes) {
         if (shape == 3) {
-            const size_t sb = (size_t)n_tiles * jsp::split_tile_words(v.cpg) * 8;
+            const size_t sb = (size_t)n_tiles * jsp::split_tile_words(v.cpg, jsp::split_waves(e->blk_l0, e->blk_l1)) * 8;
             HIP_TRY(v.split.reserve(sb));
             std::memset(v.split.p, 0, sb);
             e->walk.set_tiles(e->blk_l0, e->blk_l1, v.groups, v.cpg);
@@ -1112,6 +1112,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     } else {
         sp.groups = v.groups;
         sp.cpg = v.cpg;
+        sp.nw = jsp::split_waves(e->blk_l0, e->blk_l1);
         sp.C = e->C;
         sp.out = v.split.as<uint64_t>();
         sp.topo = e->topo;

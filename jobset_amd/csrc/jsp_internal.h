@@ -279,22 +279,32 @@ struct ServiceArgs {
 // classes) or its partial capacity sums per upper-level domain (upper
 // classes), plus its leaves' occupancy bits -- through pinned host memory; the
 // host runs the O(J + C D / 64) walk.
-// Per tile, split_tile_words(cpg) u64, every one tagged with the request, so
-// its arrival is the signal (no done word, no store-retirement wait):
-// first (cpg + 1) 64-byte lines, line j for class slot j (j = cpg: the
-// leaves' occupancy), entries 2w and 2w + 1 for wave w = (seq << 32) | 32
-// bits -- the low and high halves of the ballot of leaves [64w, 64w + 64) of
-// the tile (a leaf-level class, the occupancy), or the wave's record count and
-// 0 (an upper class); then, per upper class slot j and wave w, kSplitRecs
-// records (split_rec_tag(seq) << 50) | (domain << 30) | partial clamped
-// capacity sum (< 2^30). Upper-level domains must number < 2^20 (split_ok).
+// Per tile, split_tile_words(cpg, nw) u64 (nw: the waves of the largest tile
+// that hold leaves, 64 leaves each), every one tagged with the request, so its
+// arrival is the signal (no done word, no store-retirement wait). First the
+// tile's lines: for class slot j (j = cpg: the leaves' occupancy) and wave
+// w < nw, entries 2 (j nw + w) and + 1 = (seq << 32) | 32 bits -- the low and
+// high halves of the ballot of leaves [64w, 64w + 64) of the tile (a
+// leaf-level class, the occupancy), or the wave's record count and 0 (an upper
+// class) -- rounded up to whole 64-byte lines: the host reads every line a
+// device write just invalidated, one miss each, so the layout is dense (cfg3:
+// one line per tile, not one per class and wave). Then, per upper class slot j
+// and wave w, kSplitRecs records (split_rec_tag(seq) << 50) | (domain << 30) |
+// partial clamped capacity sum (< 2^30). Upper-level domains must number
+// < 2^20 (split_ok).
 constexpr uint32_t kSplitRecs = 64;
 constexpr uint32_t kSplitMaxDomains = 1u << 20;
-__host__ __device__ constexpr uint32_t split_tile_words(uint32_t cpg) { return 8u * (cpg + 1u) + 4u * kSplitRecs * cpg; }
+__host__ __device__ constexpr uint32_t split_line_words(uint32_t cpg, uint32_t nw) {
+    return (2u * (cpg + 1u) * nw + 7u) & ~7u;
+}
+__host__ __device__ constexpr uint32_t split_tile_words(uint32_t cpg, uint32_t nw) {
+    return split_line_words(cpg, nw) + nw * kSplitRecs * cpg;
+}
 __host__ __device__ constexpr uint64_t split_rec_tag(uint32_t seq) { return (uint64_t)(seq % 16383u + 1u); }
 struct SplitArgs {
     uint32_t groups, cpg, C;
-    uint64_t* out;  // host-mapped [n_tiles][split_tile_words(cpg)]
+    uint32_t nw;    // waves of the largest tile that hold leaves (1..4)
+    uint64_t* out;  // host-mapped [n_tiles][split_tile_words(cpg, nw)]
     TopoDev topo;
 };
 

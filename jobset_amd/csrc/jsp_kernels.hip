@@ -3475,7 +3475,7 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
     JSP_LDS uint32_t* s_pre = lds_ptr(s_x + 16);
     // the tile's lines, gathered here and written by one pass of stores
     JSP_LDS uint32_t* s_line = lds_ptr(s_x + 16 + kTallyThreads);
-    const uint32_t n_line = 8u * (sp.cpg + 1u);
+    const uint32_t nw = sp.nw, n_line = split_line_words(sp.cpg, nw);
     if ((uint32_t)tid < n_line) s_line[tid] = 0u;
     __syncthreads();
     const uint32_t la = ag.la;
@@ -3488,7 +3488,8 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
         const uint32_t cap = in ? s_acc[c * la + tid] : 0u;
         if (level + 1 == K) {
             const uint64_t word = __ballot(in && cap >= pods);
-            if (lane < 2) s_line[8 * c + 2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
+            if (lane < 2 && (uint32_t)wid < nw)
+                s_line[2 * (c * nw + wid) + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
         } else {
             const uint32_t v = cap < pods ? cap : pods;
             uint32_t total;
@@ -3507,16 +3508,17 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
                 rec = rtag | ((unsigned long long)d << 30) | partial;
             }
             const uint64_t m = __ballot(last);
-            uint64_t* recs = out + n_line + ((size_t)c * 4 + wid) * kSplitRecs;
+            uint64_t* recs = out + n_line + ((size_t)c * nw + wid) * kSplitRecs;
             if (last) __hip_atomic_store(recs + mbcnt64(m), rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            if (lane == 0) s_line[8 * c + 2 * wid] = (uint32_t)__popcll(m);
+            if (lane == 0 && (uint32_t)wid < nw) s_line[2 * (c * nw + wid)] = (uint32_t)__popcll(m);
             __syncthreads();  // s_pre and the scan scratch are rewritten by the next upper class
         }
     }
     if (ag.do_occ) {
         const uint32_t o = in ? s_acc[nc * la + tid] : 0u;
         const uint64_t word = __ballot(in && o != 0u);
-        if (lane < 2) s_line[8 * sp.cpg + 2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
+        if (lane < 2 && (uint32_t)wid < nw)
+            s_line[2 * (sp.cpg * nw + wid) + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
     }
     __syncthreads();
     if ((uint32_t)tid < n_line)
@@ -3541,7 +3543,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     ag.do_occ = ft.do_occ;
     ag.cap_out = nullptr;  // the sums stay in LDS
     const uint4 bt = a.blk[ft.blk];
-    uint64_t* out = sp.out + (size_t)tile * split_tile_words(sp.cpg);
+    uint64_t* out = sp.out + (size_t)tile * split_tile_words(sp.cpg, sp.nw);
     uint32_t seq = v.seq0;
     // the tile's rows stay in LDS between requests (as the compaction
     // service's; bit 63 of the bell: the snapshot was patched since the

@@ -96,26 +96,34 @@ void HostWalk::set_tiles(const std::vector<uint32_t>& blk_l0, const std::vector<
     l1_ = blk_l1;
     groups_ = groups;
     cpg_ = cpg;
+    nw_ = split_waves(blk_l0, blk_l1);
+}
+
+uint32_t split_waves(const std::vector<uint32_t>& blk_l0, const std::vector<uint32_t>& blk_l1) {
+    uint32_t m = 1;
+    for (size_t b = 0; b < blk_l0.size() && b < blk_l1.size(); ++b) m = std::max(m, blk_l1[b] - blk_l0[b]);
+    return std::min<uint32_t>((m + 63) / 64, 4u);
 }
 
 void HostWalk::prefetch_tile(const uint64_t* slots, uint32_t t) const {
     const uint32_t b = t / groups_;
     if (b >= l0_.size()) return;
-    const uint64_t* s = slots + (size_t)t * split_tile_words(cpg_);
-    for (uint32_t j = 0; j <= cpg_; ++j) __builtin_prefetch(s + 8u * j, 0, 3);
+    const uint64_t* s = slots + (size_t)t * split_tile_words(cpg_, nw_);
+    const uint32_t n_line = split_line_words(cpg_, nw_);
+    for (uint32_t i = 0; i < n_line; i += 8) __builtin_prefetch(s + i, 0, 3);
     if (!any_upper_) return;
     const uint32_t nl = l1_[b] - l0_[b], g = t % groups_;
     for (uint32_t j = 0; j < cpg_; ++j) {
         const uint32_t c = g * cpg_ + j;
         if (c >= C_ || level_[c] + 1 == K_) continue;
         for (uint32_t w = 0; 64 * w < nl; ++w)
-            __builtin_prefetch(s + 8u * (cpg_ + 1) + ((size_t)j * 4 + w) * kSplitRecs, 0, 3);
+            __builtin_prefetch(s + n_line + ((size_t)j * nw_ + w) * kSplitRecs, 0, 3);
     }
 }
 
 bool HostWalk::tile_ready(const uint64_t* slots, uint32_t t, uint32_t seq) const {
-    const uint64_t* s = slots + (size_t)t * split_tile_words(cpg_);
-    const uint32_t n_line = 8u * (cpg_ + 1);
+    const uint64_t* s = slots + (size_t)t * split_tile_words(cpg_, nw_);
+    const uint32_t n_line = split_line_words(cpg_, nw_);
     uint32_t bad = 0;
     for (uint32_t i = 0; i < n_line; ++i) bad |= (uint32_t)(__atomic_load_n(s + i, __ATOMIC_ACQUIRE) >> 32) ^ seq;
     if (bad) return false;
@@ -127,8 +135,8 @@ bool HostWalk::tile_ready(const uint64_t* slots, uint32_t t, uint32_t seq) const
         const uint32_t c = g * cpg_ + j;
         if (c >= C_ || level_[c] + 1 == K_) continue;
         for (uint32_t w = 0; 64 * w < nl; ++w) {
-            const uint32_t n = std::min<uint32_t>((uint32_t)s[8 * j + 2 * w], kSplitRecs);
-            const uint64_t* r = s + n_line + ((size_t)j * 4 + w) * kSplitRecs;
+            const uint32_t n = std::min<uint32_t>((uint32_t)s[2 * (j * nw_ + w)], kSplitRecs);
+            const uint64_t* r = s + n_line + ((size_t)j * nw_ + w) * kSplitRecs;
             for (uint32_t i = 0; i < n; ++i)
                 if ((__atomic_load_n(r + i, __ATOMIC_ACQUIRE) >> 50) != rtag) return false;
         }
@@ -136,22 +144,24 @@ bool HostWalk::tile_ready(const uint64_t* slots, uint32_t t, uint32_t seq) const
     return true;
 }
 
-// A ballot word of a tile line: wave w's halves (low 32 bits of entries 2w, 2w + 1).
-static inline uint64_t line_word(const uint64_t* line, uint32_t w) {
-    return (line[2 * w] & 0xFFFFFFFFull) | (line[2 * w + 1] << 32);
+// A ballot word of a tile's lines: class slot j, wave w's halves (the low 32
+// bits of entries 2 (j nw + w) and + 1).
+static inline uint64_t line_word(const uint64_t* lines, uint32_t nw, uint32_t j, uint32_t w) {
+    const uint64_t* p = lines + 2 * (j * nw + w);
+    return (p[0] & 0xFFFFFFFFull) | (p[1] << 32);
 }
 
 void HostWalk::build_feasibility(const uint64_t* slots) {
-    const size_t tile_words = split_tile_words(cpg_);
-    const uint32_t n_line = 8u * (cpg_ + 1);
+    const size_t tile_words = split_tile_words(cpg_, nw_);
+    const uint32_t n_line = split_line_words(cpg_, nw_);
     const uint32_t nb = (uint32_t)l0_.size();
     // occupied leaves, from the group-0 tiles
     std::fill(occ_.begin(), occ_.end(), 0ull);
     for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t* s = slots + (size_t)(b * groups_) * tile_words + 8u * cpg_;
+        const uint64_t* s = slots + (size_t)(b * groups_) * tile_words;
         const uint32_t nl = l1_[b] - l0_[b];
         for (uint32_t w = 0; 64 * w < nl; ++w) {
-            const uint64_t x = line_word(s, w);
+            const uint64_t x = line_word(s, nw_, cpg_, w);
             if (x) or_bits(occ_.data(), l0_[b] + 64 * w, x);
         }
     }
@@ -174,10 +184,10 @@ void HostWalk::build_feasibility(const uint64_t* slots) {
         uint64_t* F = feas_.data() + woff_[c];
         if (k + 1 == K_) {
             for (uint32_t b = 0; b < nb; ++b) {
-                const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words + 8u * j;
+                const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words;
                 const uint32_t nl = l1_[b] - l0_[b];
                 for (uint32_t w = 0; 64 * w < nl; ++w) {
-                    const uint64_t x = line_word(s, w);
+                    const uint64_t x = line_word(s, nw_, j, w);
                     if (x) or_bits(F, l0_[b] + 64 * w, x);
                 }
             }
@@ -190,8 +200,8 @@ void HostWalk::build_feasibility(const uint64_t* slots) {
                 const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words;
                 const uint32_t nl = l1_[b] - l0_[b];
                 for (uint32_t w = 0; 64 * w < nl; ++w) {
-                    const uint32_t n = std::min<uint32_t>((uint32_t)s[8u * j + 2u * w], kSplitRecs);
-                    const uint64_t* q = s + n_line + ((size_t)j * 4 + w) * kSplitRecs;
+                    const uint32_t n = std::min<uint32_t>((uint32_t)s[2u * (j * nw_ + w)], kSplitRecs);
+                    const uint64_t* q = s + n_line + ((size_t)j * nw_ + w) * kSplitRecs;
                     for (uint32_t i = 0; i < n; ++i) {
                         const uint64_t r = q[i];
                         const uint32_t d = (uint32_t)(r >> 30) & (kSplitMaxDomains - 1u);

@@ -14,6 +14,10 @@
 
 namespace jsp {
 
+// The waves of the largest tally row block that hold leaves (64 leaves each,
+// at most 4): the split service's line layout (jsp_internal.h SplitArgs).
+uint32_t split_waves(const std::vector<uint32_t>& blk_l0, const std::vector<uint32_t>& blk_l1);
+
 class HostWalk {
 public:
     // topology: first_leaf per level (identity at the leaves), child_start
@@ -52,7 +56,7 @@ private:
     void build_feasibility(const uint64_t* slots);
     void take(uint32_t d, uint32_t k);
 
-    uint32_t K_ = 0, L_ = 0, C_ = 0, groups_ = 1, cpg_ = 1;
+    uint32_t K_ = 0, L_ = 0, C_ = 0, groups_ = 1, cpg_ = 1, nw_ = 1;
     uint32_t D_[kMaxLevels] = {0, 0, 0, 0};
     std::vector<uint32_t> fl_[kMaxLevels], cs_[kMaxLevels];
     std::vector<int32_t> par_[kMaxLevels];

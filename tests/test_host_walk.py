@@ -20,9 +20,14 @@ SPLIT_RECS = 64                 # jsp_internal.h kSplitRecs
 SEQ = 7                         # the request number the emulated tiles tag their answer with
 
 
-def tile_words(cpg):
-    """jsp_internal.h split_tile_words: (cpg + 1) lines of 8, then records."""
-    return 8 * (cpg + 1) + 4 * SPLIT_RECS * cpg
+def line_words(cpg, nw):
+    """jsp_internal.h split_line_words: 2 entries per (class slot, wave), whole lines."""
+    return (2 * (cpg + 1) * nw + 7) & ~7
+
+
+def tile_words(cpg, nw):
+    """jsp_internal.h split_tile_words: the lines, then nw x 64 records per class slot."""
+    return line_words(cpg, nw) + nw * SPLIT_RECS * cpg
 
 
 def rec_tag(seq):
@@ -30,10 +35,10 @@ def rec_tag(seq):
     return seq % 16383 + 1
 
 
-def put_word(slots, line, w, word, seq=SEQ):
-    """Wave w's ballot as the two tagged halves of a tile line."""
-    slots[line + 2 * w] = (seq << 32) | (word & 0xFFFFFFFF)
-    slots[line + 2 * w + 1] = (seq << 32) | (word >> 32)
+def put_word(slots, entry, word, seq=SEQ):
+    """A ballot as the two tagged halves at a tile's line entry."""
+    slots[entry] = (seq << 32) | (word & 0xFFFFFFFF)
+    slots[entry + 1] = (seq << 32) | (word >> 32)
 CHUNK_ROWS, MAX_BLK_LEAVES = 1024, 256
 
 
@@ -81,7 +86,9 @@ def emulate_tiles(p, cap, occ):
     nb = len(b0)
     groups = split_groups(C, nb)
     cpg = (C + groups - 1) // groups
-    tw = tile_words(cpg)
+    nw = min((max([1] + [b1[b] - b0[b] for b in range(nb)]) + 63) // 64, 4)  # jsp_walk split_waves
+    nlw = line_words(cpg, nw)
+    tw = tile_words(cpg, nw)
     slots = np.zeros(nb * groups * tw, dtype=np.uint64)
     for b in range(nb):
         l0, l1 = b0[b], b1[b]
@@ -89,25 +96,23 @@ def emulate_tiles(p, cap, occ):
         for g in range(groups):
             t = b * groups + g
             base_t = t * tw
-            for j in range(cpg + 1):  # every line is written, tagged
-                for w in range(4):
-                    put_word(slots, base_t + 8 * j, w, 0)
+            for e in range(0, nlw, 2):  # every line entry is written, tagged
+                put_word(slots, base_t + e, 0)
             for j in range(cpg):
                 c = g * cpg + j
                 if c >= C:
                     break
                 jc = p.classes[c]
-                line = base_t + 8 * j
                 capc = cap[c, l0:l1].astype(np.int64)
                 if jc.level + 1 == K:
                     ok = capc >= jc.pods
-                    for w in range(4):
+                    for w in range(nw):
                         word = 0
                         for i in range(64):
                             li = 64 * w + i
                             if li < nl and ok[li]:
                                 word |= 1 << i
-                        put_word(slots, line, w, word)
+                        put_word(slots, base_t + 2 * (j * nw + w), word)
                 else:
                     fl = topo.first_leaf[jc.level]
                     incl = np.cumsum(np.minimum(capc, jc.pods))
@@ -120,20 +125,19 @@ def emulate_tiles(p, cap, occ):
                             first = max(beg, l0) - l0
                             part = int(incl[li] - (incl[first - 1] if first > 0 else 0))
                             recs[li // 64].append((rec_tag(SEQ) << 50) | (d << 30) | part)
-                    for w in range(4):
-                        slots[line + 2 * w] = (SEQ << 32) | len(recs[w])
-                        rb = base_t + 8 * (cpg + 1) + (j * 4 + w) * SPLIT_RECS
+                    for w in range(nw):
+                        slots[base_t + 2 * (j * nw + w)] = (SEQ << 32) | len(recs[w])
+                        rb = base_t + nlw + (j * nw + w) * SPLIT_RECS
                         for i, r in enumerate(recs[w]):
                             slots[rb + i] = r
             if g == 0:
-                line = base_t + 8 * cpg
-                for w in range(4):
+                for w in range(nw):
                     word = 0
                     for i in range(64):
                         li = 64 * w + i
                         if li < nl and occ[l0 + li] != 0:
                             word |= 1 << i
-                    put_word(slots, line, w, word)
+                    put_word(slots, base_t + 2 * (cpg * nw + w), word)
     return slots, (b0, b1), groups, cpg
 
 
