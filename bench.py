@@ -843,10 +843,10 @@ def main() -> None:
         # a third, tracer-free measure: the kernel's own span (first wave start
         # -> last wave end, device clock stamps per wave; jsp_tally_device_spans)
         try:
-            span_med, span_mean, empty_us = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(), L4,
-                                                                         tally_loop)
+            span_med, span_mean, empty_us, period_us = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(),
+                                                                                    L4, tally_loop)
         except Exception:  # noqa: BLE001 -- another tally shape (sharded ranks): no span
-            span_med = span_mean = empty_us = None
+            span_med = span_mean = empty_us = period_us = None
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
         # cold: the library's read-only sweep of the 512 MiB buffer before each launch, dispatch events
@@ -913,11 +913,13 @@ def main() -> None:
                 "tally_span_median_us": round(span_med, 2) if span_med else None,
                 "tally_span_vs_events": round(span_mean / tally_mean, 3) if span_mean else None,
                 "tally_empty_launch_event_us": round(empty_us, 2) if empty_us else None,
-                "tally_span_plus_empty_vs_events": round((span_mean + empty_us) / tally_mean, 3) if span_mean else None,
-                "tally_measure": "tally_us (events on the dispatch packets) is the figure used; tally_span_us is the "
-                                 "kernel's own first-wave-start -> last-wave-end span from per-wave clock stamps (no "
-                                 "tracer), and tally_empty_launch_event_us the events' time for an empty one-workgroup "
-                                 "launch: span + empty ~ events is the cross-check",
+                "tally_period_us": round(period_us, 2) if period_us else None,
+                "tally_period_vs_events": round(period_us / tally_mean, 3) if period_us else None,
+                "tally_measure": "tally_us (events on the dispatch packets) is the figure used; tally_period_us is the "
+                                 "same back-to-back launches' period by the kernels' own clock (first wave to first "
+                                 "wave, per-wave stamps, no tracer): the cross-check; tally_span_us is the execution "
+                                 "part of it (first wave start -> last wave end), the rest the gap dispatch leaves "
+                                 "between launches; tally_empty_launch_event_us = an empty one-workgroup launch's events",
                 "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
                               "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
                               "around 200 ctypes-issued launches (includes host submit gaps)",

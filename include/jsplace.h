@@ -356,8 +356,11 @@ int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us);
  * beside the dispatch-packet events and a kernel trace, with no tracer and no
  * dispatch overhead in it. out_us[0] median, [1] mean; out_us[2] the median
  * dispatch-event time of an empty one-workgroup launch (the fixed cost events
- * on the dispatch packets add to a kernel's own span). JSP_ESTATE when the
- * snapshot's tally runs another shape. */
+ * on the dispatch packets add to a kernel's own span); out_us[3] the launches'
+ * period by the same clock (first wave of the first launch to first wave of
+ * the last, per launch: execution plus the gap dispatch leaves between
+ * back-to-back launches). JSP_ESTATE when the snapshot's tally runs another
+ * shape. */
 int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
                            double* out_us);
 int jsp_engine_set_timing(jsp_engine* e, int enable);

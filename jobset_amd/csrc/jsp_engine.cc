@@ -2552,6 +2552,7 @@ int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
     HIP_TRY(hipStreamSynchronize(s));
     std::vector<double> us(iters);
     double sum = 0.0;
+    unsigned long long lo0 = 0, lo_last = 0;
     for (uint32_t i = 0; i < iters; ++i) {
         unsigned long long lo = ~0ull, hi = 0;
         for (size_t k = 0; k < per; k += 2) {
@@ -2560,10 +2561,16 @@ int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
         }
         us[i] = (double)(hi - lo) / 100.0;  // 100 MHz ticks
         sum += us[i];
+        if (i == 0) lo0 = lo;
+        lo_last = lo;
     }
     std::sort(us.begin(), us.end());
     out_us[0] = us[iters / 2];
     out_us[1] = sum / iters;
+    // the launches' period by the kernels' own clock: first wave of launch 0
+    // to first wave of the last launch, per launch (execution + the gap the
+    // dispatch leaves between back-to-back launches)
+    out_us[3] = iters > 1 ? (double)(lo_last - lo0) / 100.0 / (iters - 1) : out_us[1];
     // an empty one-workgroup launch timed by events on its dispatch packet:
     // the fixed cost events add to a kernel's own span
     const uint32_t grid = 1;  // the launch's fixed packet and completion cost (a grid's dispatch overlaps its work)

@@ -283,13 +283,15 @@ class Engine:
                                                scrub or None, scrub_bytes, _p(out)))
         return float(out[0]), float(out[1])
 
-    def tally_device_spans(self, d_cap: int, d_occ: int, ld: int, iters: int) -> Tuple[float, float, float]:
+    def tally_device_spans(self, d_cap: int, d_occ: int, ld: int,
+                           iters: int) -> Tuple[float, float, float, float]:
         """In-kernel span of the one-tile wave tally (first wave start -> last
         wave end, device clock; jsp_tally_device_spans): (median, mean) us,
-        and the dispatch-event time of an empty one-workgroup launch."""
-        out = np.zeros(3, dtype=np.float64)
+        the dispatch-event time of an empty one-workgroup launch, and the
+        back-to-back launches' period by the kernels' own clock."""
+        out = np.zeros(4, dtype=np.float64)
         check(self._lib.jsp_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
-        return float(out[0]), float(out[1]), float(out[2])
+        return float(out[0]), float(out[1]), float(out[2]), float(out[3])
 
     def link_floor(self, iters: int = 2000) -> Tuple[float, float, float]:
         """Host -> device -> host round trip through pinned memory with the
