@@ -330,6 +330,10 @@ struct jsp_engine {
         int shape = 0;   // 2 compaction, 3 split
         bool clk = false;
         bool rows_dirty = true;  // a patch since the last request: its tiles reload their rows from memory
+        // a micro-patch since the last request: the request that carries it
+        // hands its rows to the resident tiles (the dispatcher's microbox), any
+        // other request reloads them (rows_dirty)
+        bool micro_dirty = false;
         uint32_t pending = 0;    // a compaction request answered early: its tiles' done words still to come
         bool resume = false;  // an upload stopped it: start it again once the engine is ready
         bool pending_ready = false;  // launched; the dispatcher's ready word not seen yet
@@ -1036,8 +1040,9 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     // request (patch_wait), so the launch need not wait for the engine's
     // streams.
     const size_t xbytes = ((size_t)4 * (nb + 1) + 127) & ~size_t(127);  // XCC vote words (co-located service)
-    if (gpad + 128 + xbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
-    HIP_TRY(v.granules.reserve(gpad + 128 + xbytes));
+    const size_t mbytes = (size_t)4 * (2 + jsp::kMailboxPayload);       // the microbox (not zeroed: seq-tagged)
+    if (gpad + 128 + xbytes + mbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
+    HIP_TRY(v.granules.reserve(gpad + 128 + xbytes + mbytes));
     const unsigned long long key = ((unsigned long long)nb << 8) | ((unsigned long long)n_tiles << 40) | (unsigned)shape;
     if (v.zero_key != key) {
         HIP_TRY(hipMemsetAsync(v.granules.p, 0, gpad + 128, v.stream));
@@ -1077,6 +1082,8 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     // look-back, for A/B runs)
     v.bitmap = shape == 2 && !e->hooks.svc_entries;
     a.bits = v.bitmap ? v.bits.as<unsigned long long>() : nullptr;
+    // the microbox: a micro-patch's rows for the co-located resident tiles
+    a.mbox = shape == 2 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 128 + xbytes) : nullptr;
     a.done = w;
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;
@@ -1411,6 +1418,9 @@ void patch_post_deferred(jsp_engine* e) {
     v.last = std::chrono::steady_clock::now();
     svc_request(e, seq, e->patch_bits | jsp::kReqPatchOnly, e->patch_nf, e->patch_micro);
     e->patch_req = seq;
+    // applied on its own: the next request's tiles reload the rows
+    v.rows_dirty |= v.micro_dirty;
+    v.micro_dirty = false;
 }
 
 int patch_wait(jsp_engine* e) {
@@ -1555,7 +1565,7 @@ void run_wake(jsp_engine* e) {
     e->patch_req = seq;
     e->patch_deferred = false;
     v.pending = seq;
-    v.rows_dirty = false;  // the warm-up loads the patched rows
+    v.rows_dirty = v.micro_dirty = false;  // the warm-up loads the patched rows
     e->acc.wake_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
 }
 
@@ -1667,10 +1677,13 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
         const uint32_t w2 = carry && (e->patch_bits & jsp::kReqPatchInline) ? e->patch_nf : n_runs;
         // the tiles keep their rows on chip: bit 31 of J tells them the
         // snapshot was patched since their previous request (J < 2^28)
-        const uint32_t jw = J | (v.rows_dirty ? jsp::kReqDirty : 0u) | (carry ? e->patch_bits : 0u);
+        // (a micro-patch carried here: the dispatcher hands its rows to the
+        // resident tiles, or marks the rows patched itself)
         const bool micro = carry && e->patch_micro;
+        const bool dirty = v.rows_dirty || (v.micro_dirty && !micro);
+        const uint32_t jw = J | (dirty ? jsp::kReqDirty : 0u) | (carry ? e->patch_bits : 0u);
         carry = false;  // a retry finds it applied, or applied by the patch kernel (patch_wait)
-        v.rows_dirty = false;
+        v.rows_dirty = v.micro_dirty = false;
         if (attempt == 0) {
             t_post = std::chrono::steady_clock::now();
             e->acc.svc_pre_us += std::chrono::duration<double, std::micro>(t_post - t_in).count();
@@ -2285,7 +2298,6 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
         if (int rc = svc_settle(e)) return rc;  // no tile may still be reading the rows of the last request
         if (int rc = patch_wait(e)) return rc;  // the staging buffer is free again
     }
-    e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     hipStream_t s = e->stream;
     auto& v = e->svc;
     if (!e->patch_ctr.p) {
@@ -2310,6 +2322,7 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
         }
     }
     if (micro) {
+        e->svc.micro_dirty = true;  // the resident tiles' on-chip row copies are stale
         if (int rc = micro_stage_kernel_form(e)) return rc;
         const auto t2 = std::chrono::steady_clock::now();
         e->acc.patches += 1;
@@ -2317,6 +2330,7 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
         return JSP_OK;
     }
     e->patch_micro = false;
+    e->svc.rows_dirty = true;  // the resident tiles' on-chip row copies are stale
     // Who applies it: the running service's dispatcher (posted at once; a
     // request that finds it not yet taken carries it again; whatever else
     // reads the rows first waits for it, patch_wait); after the service left,

@@ -186,6 +186,11 @@ struct PatchDesc {
 // n | column flags << 16.
 constexpr uint32_t kReqDirty = 1u << 31, kReqPatch = 1u << 30, kReqPatchOnly = 1u << 29,
                    kReqPatchInline = 1u << 28;
+// The bell's J word (the dispatcher's copy of the request): bit 31 the rows
+// changed (every tile reloads them), bit 30 the request's micro-patch rows
+// are in the microbox (ServiceArgs::mbox: the resident tiles take them from
+// there instead of reloading), bits 0..27 J.
+constexpr uint32_t kBellMicro = 1u << 30;
 // Inline patch staging (ServiceArgs::pstage, host-mapped, one fixed buffer per
 // service): a 64-B header {seq}, then rows[n], then (8-B aligned) the present
 // columns in the order labels [W][n] u64, taints [n], free [R][n], excl [n].
@@ -271,6 +276,10 @@ struct ServiceArgs {
     // 32 bits) halves); the host gives job j the j-th feasible leaf. null: the
     // per-job (seq << 32 | domain) entries in `assign` after a look-back.
     unsigned long long* bits;
+    // the co-located resident compaction: the dispatcher's copy of a
+    // micro-patch for its tiles, device memory {request seq, m | flags << 16,
+    // m rows of micro_row_words} (kBellMicro), or null
+    uint32_t* mbox;
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

@@ -3163,17 +3163,39 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             // request posted before its completion word came back) is not
             // applied twice; each apply ends with a barrier and the completion word
             const bool fresh = pseq != s_p[7];
+            // the resident co-located tiles take a micro-patch riding in a
+            // request with clean rows from the microbox (one L2 line) and
+            // patch their registers; the rows are written through after the bell
+            const bool mb = fresh && m > 0u && v.mbox != nullptr && v.resident != 0u && local &&
+                            (jw & (kReqDirty | kReqPatchOnly)) == 0u;
             if (fresh) {
-                // a micro-patch on a co-located service: into this XCD's L2
-                // first (the tiles reload from there), written through for
-                // every other reader after the bell
-                if (m > 0u) service_micro_stores(a, s_p + 8, m, fl, local);
-                else if (jw & kReqPatchInline) service_apply_inline(v, a, nr);
-                else service_apply_patch(v, a);
+                if (mb) {
+                    const uint32_t rw2 = m * rw;
+                    if (threadIdx.x < rw2)
+                        __hip_atomic_store(v.mbox + 2 + threadIdx.x, s_p[8 + threadIdx.x], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (threadIdx.x == 0) {
+                        __hip_atomic_store(v.mbox, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_store(v.mbox + 1, m | (fl << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    __syncthreads();
+                } else if (m > 0u) {
+                    // a micro-patch on a co-located service: into this XCD's L2
+                    // first (the tiles reload from there), written through for
+                    // every other reader after the bell
+                    service_micro_stores(a, s_p + 8, m, fl, local);
+                } else if (jw & kReqPatchInline) {
+                    service_apply_inline(v, a, nr);
+                } else {
+                    service_apply_patch(v, a);
+                }
             }
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
-                const unsigned long long mm =
-                    ((unsigned long long)(jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) << 32) | q;
+                // rows changed (and not handed over in the microbox): every tile reloads
+                const uint32_t bj = (jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) |
+                                    (mb ? kBellMicro : 0u) | (fresh && m > 0u && !mb ? kReqDirty : 0u);
+                const unsigned long long mm = ((unsigned long long)bj << 32) | q;
                 if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (v.clk) {
@@ -3185,7 +3207,7 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                 }
             }
             if (fresh && m > 0u) {
-                if (local) service_micro_stores(a, s_p + 8, m, fl, false);  // in memory for every other reader
+                if (local || mb) service_micro_stores(a, s_p + 8, m, fl, false);  // in memory for every other reader
                 // its completion word: readers other than this service's
                 // tiles (launches, uploads, jsp_engine_sync) wait for it
                 if (threadIdx.x == 0) __hip_atomic_store(v.pdone, pseq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3205,6 +3227,40 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
         __syncthreads();
         if (threadIdx.x == 0) s_p[0] = 0;
         __syncthreads();
+    }
+}
+
+// The micro-patch rows of this request from the microbox (ServiceArgs::mbox,
+// sc1 loads: L2 hits on the co-located service): thread t holds rows mine ..
+// mine + 3 in registers, and a patched row among them takes the columns the
+// patch carries (micro_row_words layout: row id, W label words as lo/hi
+// halves, taint, R free, excl).
+template <int W, int R>
+__device__ __forceinline__ void apply_microbox(const uint32_t* mb, uint32_t mine, RowRegs<W, R>& x) {
+    const uint32_t mf = __hip_atomic_load(mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t m = mf & 0xFFFFu, fl = mf >> 16;
+    constexpr uint32_t rw = 3u + 2u * W + R;
+    for (uint32_t r = 0; r < m && r * rw < kMailboxPayload; ++r) {
+        const uint32_t* p = mb + 2 + r * rw;
+        const uint32_t i = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - mine;
+        if (i >= 4u) continue;
+        uint32_t v[rw];
+#pragma unroll
+        for (uint32_t k = 1; k < rw; ++k) v[k] = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            if ((uint32_t)s != i) continue;
+            if (fl & kPatchLab) {
+#pragma unroll
+                for (int w = 0; w < W; ++w) x.lab[w][s] = ((uint64_t)v[2 + 2 * w] << 32) | v[1 + 2 * w];
+            }
+            if (fl & kPatchTaint) x.tn[s] = v[1 + 2 * W];
+            if (fl & kPatchFree) {
+#pragma unroll
+                for (int r2 = 0; r2 < R; ++r2) x.fr[r2][s] = v[2 + 2 * W + r2];
+            }
+            if (fl & kPatchExcl) x.ex[s] = (int32_t)v[2 + 2 * W + R];
+        }
     }
 }
 
@@ -3408,7 +3464,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
         __syncthreads();
         const uint32_t next = s_x[16], Jw = s_x[17];
         if (next == 0) return;
-        const uint32_t J = Jw & 0x7FFFFFFFu;
+        const uint32_t J = Jw & ~(kReqDirty | kBellMicro);
         const bool use_cache = cached && (Jw >> 31) == 0u;
         svc_stamp(clk, 1);
         const uint32_t epoch = next & 0x3FFFFFFFu;
@@ -3417,6 +3473,9 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
                 const uint32_t row = (bt.z & ~3u) + 4u * threadIdx.x;
                 load_rows<W, R, true>(a, row, row < bt.w && row + 3 >= bt.z, rows);
             }
+            // this request's micro-patch rows, from the microbox (their stores
+            // to memory may land after this tile's loads)
+            if (Jw & kBellMicro) apply_microbox<W, R>(v.mbox, (bt.z & ~3u) + 4u * threadIdx.x, rows);
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
                                                 lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
             svc_stamp(clk, 2);

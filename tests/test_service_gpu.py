@@ -713,6 +713,45 @@ def test_micro_patches_ride_in_the_request(svc_engine, cfg, then):
     np.testing.assert_array_equal(got.occ, occ)
 
 
+@pytest.mark.parametrize("cols", ["labels", "all"])
+def test_micro_patch_rows_from_the_microbox(svc_engine, cols):
+    """A one-row micro-patch carried by the next request of the co-located
+    resident service reaches its tiles through the dispatcher's microbox
+    (their rows stay in registers): label words copied from another row (the
+    row's feasibility flips), or every column at once; rows at the ends of
+    the snapshot and of the tiles' 4-row groups; bit-exact after each place."""
+    p = synth.config2()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused in (3, 5)
+    rng = np.random.default_rng(7 if cols == "labels" else 8)
+    N, R = p.nodes.n_nodes, p.nodes.free.shape[0]
+    picks = [0, 1, 3, 4, N - 1, N - 2] + [int(x) for x in rng.integers(0, N, size=10)]
+    for i, r in enumerate(picks):
+        row = np.array([r], dtype=np.uint32)
+        src = int(rng.integers(0, N))
+        lab = p.nodes.labels[:, [src]].copy()
+        if cols == "labels":
+            svc_engine.patch_rows(row, labels=lab)
+        else:
+            f = rng.integers(0, 200_000, size=(R, 1)).astype(np.uint32)
+            t = rng.integers(0, 2, size=1).astype(np.uint32)
+            ex = np.where(rng.random(1) < 0.3, 2, -1).astype(np.int32)
+            svc_engine.patch_rows(row, labels=lab, taints=t, free=f, excl=ex)
+            p.nodes.free[:, row] = f
+            p.nodes.taints[row] = t
+            p.nodes.excl[row] = ex
+        p.nodes.labels[:, row] = lab
+        got = svc_engine.place(p.job_class)
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+        if i % 4 == 3:  # a request without a patch keeps the registers
+            np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, O.place_c(p)[0])
+    got = svc_engine.place(p.job_class, want_tally=True)
+    a, cap, occ = O.place_c(p)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+    np.testing.assert_array_equal(got.occ, occ)
+
+
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_parked_service_survives_idle_gaps(svc_engine, cfg):
     """JSP_SERVICE_PARKED: no idle exit. Gaps of several idle limits, a
