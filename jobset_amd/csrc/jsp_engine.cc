@@ -1040,7 +1040,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     // request (patch_wait), so the launch need not wait for the engine's
     // streams.
     const size_t xbytes = ((size_t)4 * (nb + 1) + 127) & ~size_t(127);  // XCC vote words (co-located service)
-    const size_t mbytes = (size_t)4 * (2 + jsp::kMailboxPayload);       // the microbox (not zeroed: seq-tagged)
+    const size_t mbytes = (size_t)8 * (1 + jsp::kMailboxPayload);       // the microbox (not zeroed: seq-tagged)
     if (gpad + 128 + xbytes + mbytes > v.granules.bytes || !v.granules.p) v.zero_key = ~0ull;
     HIP_TRY(v.granules.reserve(gpad + 128 + xbytes + mbytes));
     const unsigned long long key = ((unsigned long long)nb << 8) | ((unsigned long long)n_tiles << 40) | (unsigned)shape;
@@ -1083,7 +1083,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     v.bitmap = shape == 2 && !e->hooks.svc_entries;
     a.bits = v.bitmap ? v.bits.as<unsigned long long>() : nullptr;
     // the microbox: a micro-patch's rows for the co-located resident tiles
-    a.mbox = shape == 2 ? reinterpret_cast<uint32_t*>(static_cast<char*>(v.granules.p) + gpad + 128 + xbytes) : nullptr;
+    a.mbox = shape == 2 ? reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128 + xbytes) : nullptr;
     a.done = w;
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;

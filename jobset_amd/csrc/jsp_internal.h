@@ -277,9 +277,10 @@ struct ServiceArgs {
     // per-job (seq << 32 | domain) entries in `assign` after a look-back.
     unsigned long long* bits;
     // the co-located resident compaction: the dispatcher's copy of a
-    // micro-patch for its tiles, device memory {request seq, m | flags << 16,
-    // m rows of micro_row_words} (kBellMicro), or null
-    uint32_t* mbox;
+    // micro-patch for its tiles (kBellMicro), device memory, each word tagged
+    // with the request's seq (seq << 32 | word): [0] m | flags << 16, then
+    // the m rows of micro_row_words; or null
+    unsigned long long* mbox;
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

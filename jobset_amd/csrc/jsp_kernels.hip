@@ -3164,22 +3164,18 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             // applied twice; each apply ends with a barrier and the completion word
             const bool fresh = pseq != s_p[7];
             // the resident co-located tiles take a micro-patch riding in a
-            // request with clean rows from the microbox (one L2 line) and
-            // patch their registers; the rows are written through after the bell
+            // request with clean rows from the microbox (seq-tagged words in
+            // this XCD's L2, stored beside the bell without waiting for them)
+            // and patch their registers; the rows are written through after the bell
             const bool mb = fresh && m > 0u && v.mbox != nullptr && v.resident != 0u && local &&
                             (jw & (kReqDirty | kReqPatchOnly)) == 0u;
             if (fresh) {
                 if (mb) {
-                    const uint32_t rw2 = m * rw;
-                    if (threadIdx.x < rw2)
-                        __hip_atomic_store(v.mbox + 2 + threadIdx.x, s_p[8 + threadIdx.x], __ATOMIC_RELAXED,
+                    if (threadIdx.x <= m * rw) {
+                        const uint32_t word = threadIdx.x == 0 ? m | (fl << 16) : s_p[7 + threadIdx.x];
+                        __hip_atomic_store(v.mbox + threadIdx.x, ((unsigned long long)q << 32) | word, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-                    if (threadIdx.x == 0) {
-                        __hip_atomic_store(v.mbox, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_store(v.mbox + 1, m | (fl << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    __syncthreads();
                 } else if (m > 0u) {
                     // a micro-patch on a co-located service: into this XCD's L2
                     // first (the tiles reload from there), written through for
@@ -3230,23 +3226,36 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
     }
 }
 
-// The micro-patch rows of this request from the microbox (ServiceArgs::mbox,
-// sc1 loads: L2 hits on the co-located service): thread t holds rows mine ..
-// mine + 3 in registers, and a patched row among them takes the columns the
-// patch carries (micro_row_words layout: row id, W label words as lo/hi
-// halves, taint, R free, excl).
+// One microbox word of request q (sc1 loads: L2 hits on the co-located
+// service). The dispatcher stores the words and rings the bell without
+// waiting between them, so a word may land after the bell: spin on its tag
+// (bounded; the stores were issued before the bell's).
+__device__ __forceinline__ uint32_t microbox_word(const unsigned long long* mb, uint32_t k, uint32_t q) {
+    unsigned long long x = __hip_atomic_load(mb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t s = 0; (uint32_t)(x >> 32) != q && s < (1u << 22); ++s) {
+        __builtin_amdgcn_s_sleep(1);
+        x = __hip_atomic_load(mb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return (uint32_t)x;
+}
+
+// The micro-patch rows of request q from the microbox (ServiceArgs::mbox):
+// thread t holds rows mine .. mine + 3 in registers, and a patched row among
+// them takes the columns the patch carries (micro_row_words layout: row id, W
+// label words as lo/hi halves, taint, R free, excl).
 template <int W, int R>
-__device__ __forceinline__ void apply_microbox(const uint32_t* mb, uint32_t mine, RowRegs<W, R>& x) {
-    const uint32_t mf = __hip_atomic_load(mb + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void apply_microbox(const unsigned long long* mb, uint32_t q, uint32_t mine,
+                                               RowRegs<W, R>& x) {
+    const uint32_t mf = microbox_word(mb, 0, q);
     const uint32_t m = mf & 0xFFFFu, fl = mf >> 16;
     constexpr uint32_t rw = 3u + 2u * W + R;
-    for (uint32_t r = 0; r < m && r * rw < kMailboxPayload; ++r) {
-        const uint32_t* p = mb + 2 + r * rw;
-        const uint32_t i = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - mine;
+    for (uint32_t r = 0; r < m && (r + 1) * rw <= kMailboxPayload; ++r) {
+        const uint32_t b = 1 + r * rw;
+        const uint32_t i = microbox_word(mb, b, q) - mine;
         if (i >= 4u) continue;
         uint32_t v[rw];
 #pragma unroll
-        for (uint32_t k = 1; k < rw; ++k) v[k] = __hip_atomic_load(p + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (uint32_t k = 1; k < rw; ++k) v[k] = microbox_word(mb, b + k, q);
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if ((uint32_t)s != i) continue;
@@ -3475,7 +3484,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             }
             // this request's micro-patch rows, from the microbox (their stores
             // to memory may land after this tile's loads)
-            if (Jw & kBellMicro) apply_microbox<W, R>(v.mbox, (bt.z & ~3u) + 4u * threadIdx.x, rows);
+            if (Jw & kBellMicro) apply_microbox<W, R>(v.mbox, next, (bt.z & ~3u) + 4u * threadIdx.x, rows);
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
                                                 lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
             svc_stamp(clk, 2);
