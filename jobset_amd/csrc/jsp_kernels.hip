@@ -3058,10 +3058,22 @@ __device__ void service_micro_stores(const TallyArgs& a, const uint32_t* s_w, ui
     __syncthreads();
 }
 
+// Whether request q's micro-patch goes to the resident tiles through the
+// microbox (their rows in registers, patched there, no reload): m rows, a
+// patch number this dispatcher has not applied (pseq != last), a co-located
+// resident service, and rows not marked patched otherwise (a dirty request
+// reloads them anyway; a patch-only request has no tiles to ring).
+__device__ __forceinline__ bool microbox_ring(const ServiceArgs& v, uint32_t m, uint32_t jw, uint32_t pseq,
+                                              uint32_t last, bool local) {
+    return m > 0u && pseq != last && v.mbox != nullptr && v.resident != 0u && local &&
+           (jw & (kReqDirty | kReqPatchOnly)) == 0u;
+}
+
 // The dispatcher's LDS words (s_p): [0] claimed request seq [1] J word [2]
 // stop [3] second request word [4] micro rows [5] patch number [6] column
 // flags [7] last applied patch number [8 .. 8 + kMailboxPayload) micro words
-// [8 + kMailboxPayload] the request's seen stamp (timing on).
+// [8 + kMailboxPayload] the request's seen stamp, [9 + kMailboxPayload] its
+// rung stamp when the claiming wave rang (timing on).
 __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const TallyArgs& a, uint32_t* s_p,
                                                  bool local = false) {
     const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -3117,6 +3129,31 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
                         if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
+                    if (microbox_ring(v, m, jw, (uint32_t)__builtin_amdgcn_readlane((int)x.z, 1), s_p[7], local)) {
+                        // a micro-patch for the resident tiles: its words into
+                        // the microbox and the bell rung from this wave, at
+                        // once (the barrier below waits for the other waves'
+                        // host polls in flight, up to a link round trip)
+                        const uint32_t mw = m * rw;
+                        const uint32_t b = 3u * (lane - 2u);
+                        const unsigned long long tq = (unsigned long long)q << 32;
+                        if (mine) {
+                            if (b < mw)
+                                __hip_atomic_store(v.mbox + 1 + b, tq | x.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (b + 1 < mw)
+                                __hip_atomic_store(v.mbox + 2 + b, tq | x.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if (b + 2 < mw)
+                                __hip_atomic_store(v.mbox + 3 + b, tq | x.w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                        if (lane == 0) {
+                            const uint32_t fl1 = (uint32_t)__builtin_amdgcn_readlane((int)x.w, 1);
+                            __hip_atomic_store(v.mbox, tq | m | (fl1 << 16), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            const uint32_t bj = (jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) | kBellMicro;
+                            __hip_atomic_store(v.bell, ((unsigned long long)bj << 32) | q, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP);
+                            s_p[9 + kMailboxPayload] = (uint32_t)wall_clock64();
+                        }
+                    }
                     if (v.clk && lane == 0) {  // timing on: the dispatcher's row after the tiles' (seen, rung)
                         if (patch) {
                             // written after the apply: a host store here would sit in
@@ -3163,20 +3200,12 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             // request posted before its completion word came back) is not
             // applied twice; each apply ends with a barrier and the completion word
             const bool fresh = pseq != s_p[7];
-            // the resident co-located tiles take a micro-patch riding in a
-            // request with clean rows from the microbox (seq-tagged words in
-            // this XCD's L2, stored beside the bell without waiting for them)
-            // and patch their registers; the rows are written through after the bell
-            const bool mb = fresh && m > 0u && v.mbox != nullptr && v.resident != 0u && local &&
-                            (jw & (kReqDirty | kReqPatchOnly)) == 0u;
-            if (fresh) {
-                if (mb) {
-                    if (threadIdx.x <= m * rw) {
-                        const uint32_t word = threadIdx.x == 0 ? m | (fl << 16) : s_p[7 + threadIdx.x];
-                        __hip_atomic_store(v.mbox + threadIdx.x, ((unsigned long long)q << 32) | word, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                } else if (m > 0u) {
+            // a micro-patch handed to the resident tiles in the microbox: the
+            // claiming wave has rung the bell already (the rows are written
+            // through below)
+            const bool mb = microbox_ring(v, m, jw, pseq, s_p[7], local);
+            if (fresh && !mb) {
+                if (m > 0u) {
                     // a micro-patch on a co-located service: into this XCD's L2
                     // first (the tiles reload from there), written through for
                     // every other reader after the bell
@@ -3189,13 +3218,15 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
             }
             if (threadIdx.x == 0 && (jw & kReqPatchOnly) == 0u) {  // the request behind the patch
                 // rows changed (and not handed over in the microbox): every tile reloads
-                const uint32_t bj = (jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) |
-                                    (mb ? kBellMicro : 0u) | (fresh && m > 0u && !mb ? kReqDirty : 0u);
-                const unsigned long long mm = ((unsigned long long)bj << 32) | q;
-                if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (!mb) {
+                    const uint32_t bj = (jw & ~(kReqPatch | kReqPatchOnly | kReqPatchInline)) |
+                                        (fresh && m > 0u ? kReqDirty : 0u);
+                    const unsigned long long mm = ((unsigned long long)bj << 32) | q;
+                    if (local) __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    else __hip_atomic_store(v.bell, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
                 if (v.clk) {
-                    const uint32_t t_rung = (uint32_t)wall_clock64();
+                    const uint32_t t_rung = mb ? s_p[9 + kMailboxPayload] : (uint32_t)wall_clock64();
                     __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles, s_p[8 + kMailboxPayload], __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_SYSTEM);
                     __hip_atomic_store(v.clk + kSvcClkSlots * v.n_tiles + 1, t_rung, __ATOMIC_RELAXED,
