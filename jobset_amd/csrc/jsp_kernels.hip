@@ -3257,36 +3257,38 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
     }
 }
 
-// One microbox word of request q (sc1 loads: L2 hits on the co-located
-// service). The dispatcher stores the words and rings the bell without
-// waiting between them, so a word may land after the bell: spin on its tag
-// (bounded; the stores were issued before the bell's).
-__device__ __forceinline__ uint32_t microbox_word(const unsigned long long* mb, uint32_t k, uint32_t q) {
-    unsigned long long x = __hip_atomic_load(mb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t s = 0; (uint32_t)(x >> 32) != q && s < (1u << 22); ++s) {
-        __builtin_amdgcn_s_sleep(1);
-        x = __hip_atomic_load(mb + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    return (uint32_t)x;
-}
-
 // The micro-patch rows of request q from the microbox (ServiceArgs::mbox):
-// thread t holds rows mine .. mine + 3 in registers, and a patched row among
-// them takes the columns the patch carries (micro_row_words layout: row id, W
+// every wave loads the whole box in one pass (lane k word k, sc1: L2 hits on
+// the co-located service) and takes the words by readlane. The dispatcher
+// stores the words and rings the bell without waiting between them, so a
+// word may land after the bell: the pass repeats until every word in use
+// carries q (bounded; the stores were issued before the bell's). Thread t
+// holds rows mine .. mine + 3 in registers, and a patched row among them
+// takes the columns the patch carries (micro_row_words layout: row id, W
 // label words as lo/hi halves, taint, R free, excl).
 template <int W, int R>
 __device__ __forceinline__ void apply_microbox(const unsigned long long* mb, uint32_t q, uint32_t mine,
                                                RowRegs<W, R>& x) {
-    const uint32_t mf = microbox_word(mb, 0, q);
-    const uint32_t m = mf & 0xFFFFu, fl = mf >> 16;
     constexpr uint32_t rw = 3u + 2u * W + R;
+    const uint32_t lane = threadIdx.x & 63u;
+    unsigned long long t = 0;
+    for (uint32_t s = 0; s < (1u << 22); ++s) {
+        if (lane <= kMailboxPayload) t = __hip_atomic_load(mb + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)t, 0) & 0xFFFFu;
+        const bool ok = lane > kMailboxPayload || lane > m0 * rw || (uint32_t)(t >> 32) == q;
+        if (__ballot(!ok) == 0ull) break;
+        __builtin_amdgcn_s_sleep(1);
+    }
+    const int word = (int)(uint32_t)t;
+    const uint32_t mf = (uint32_t)__builtin_amdgcn_readlane(word, 0);
+    const uint32_t m = mf & 0xFFFFu, fl = mf >> 16;
     for (uint32_t r = 0; r < m && (r + 1) * rw <= kMailboxPayload; ++r) {
         const uint32_t b = 1 + r * rw;
-        const uint32_t i = microbox_word(mb, b, q) - mine;
-        if (i >= 4u) continue;
+        const uint32_t i = (uint32_t)__builtin_amdgcn_readlane(word, b) - mine;
         uint32_t v[rw];
 #pragma unroll
-        for (uint32_t k = 1; k < rw; ++k) v[k] = microbox_word(mb, b + k, q);
+        for (uint32_t k = 1; k < rw; ++k) v[k] = (uint32_t)__builtin_amdgcn_readlane(word, b + k);
+        if (i >= 4u) continue;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             if ((uint32_t)s != i) continue;
