@@ -122,3 +122,6 @@ tools/bin/ab_inlinewake/libjsplace.so: jobset_amd/csrc/jsp_engine.cc build/jsp_k
 	@mkdir -p build/ab_iw tools/bin/ab_inlinewake
 	$(HIPCC) $(HIPFLAGS) -DJSP_AB_INLINE_WAKE -x hip -c -o build/ab_iw/e.o jobset_amd/csrc/jsp_engine.cc
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/jsp_kernels.o build/ab_iw/e.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+tools/bin/stop_anatomy: tools/stop_anatomy.hip
+	@mkdir -p tools/bin
+	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
