@@ -118,5 +118,47 @@ int main() {
                    grid, mb, med(seen), med(end), p90(end), med(tot), p90(tot), med(sync));
         }
     }
+    // how the host waits for the stopped kernel (grid 33, nothing dirtied):
+    // 0 poll hipStreamQuery, 1 hipStreamSynchronize, 2 hipDeviceSynchronize,
+    // 3 the leaving word then hipDeviceSynchronize, 4 hipEventSynchronize on
+    // an event recorded behind the kernel at launch
+    hipEvent_t ev;
+    hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+    const char* names[] = {"poll hipStreamQuery", "hipStreamSynchronize", "hipDeviceSynchronize",
+                           "leaving word + hipDeviceSynchronize", "hipEventSynchronize (event behind it)"};
+    for (int mode = 0; mode < 5; ++mode) {
+        std::vector<double> tot;
+        for (int i = 0; i < n + 5; ++i) {
+            ++gen;
+            hipLaunchKernelGGL(k_park, dim3(33), dim3(256), 0, s, host, bell, ready, gen, dirty, 0u);
+            if (mode == 4) hipEventRecord(ev, s);
+            for (unsigned b = 0; b < 33; ++b)
+                while (__atomic_load_n(ready + b, __ATOMIC_ACQUIRE) != gen) {
+                }
+            const double tw = now_us();
+            while (now_us() - tw < 200.0) {
+            }
+            const double t0 = now_us();
+            __atomic_store_n(host, gen, __ATOMIC_RELEASE);
+            if (mode == 0) {
+                while (hipStreamQuery(s) == hipErrorNotReady) {
+                }
+            } else if (mode == 1) {
+                hipStreamSynchronize(s);
+            } else if (mode == 2) {
+                hipDeviceSynchronize();
+            } else if (mode == 3) {
+                while (__atomic_load_n(host + 16, __ATOMIC_ACQUIRE) != gen) {
+                }
+                hipDeviceSynchronize();
+            } else {
+                hipEventSynchronize(ev);
+            }
+            const double t1 = now_us();
+            hipDeviceSynchronize();
+            if (i >= 5) tot.push_back(t1 - t0);
+        }
+        printf("stop word -> %-40s p50 %6.2f us p90 %6.2f\n", names[mode], med(tot), p90(tot));
+    }
     return 0;
 }
