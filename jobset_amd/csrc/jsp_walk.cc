@@ -12,6 +12,7 @@
 #include "jsp_walk.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace jsp {
@@ -87,7 +88,7 @@ void HostWalk::set_classes(const std::vector<DevClass>& cls) {
     }
     feas_.assign(woff_[C_] + 1, 0);
     sums_.assign(uoff_[C_] + 1, 0);
-    cursor_.assign(C_ + 1, 0);
+    cw_.assign(C_, ClassWalk{});
 }
 
 void HostWalk::set_tiles(const std::vector<uint32_t>& blk_l0, const std::vector<uint32_t>& blk_l1, uint32_t groups,
@@ -216,10 +217,11 @@ void HostWalk::build_feasibility(const uint64_t* slots) {
     }
 }
 
-void HostWalk::take(uint32_t d, uint32_t k) {
-    taken_[toff_[k] + (d >> 6)] |= 1ull << (d & 63);
-    if (K_ == 1) return;
-    if (fl_[k][d] == fl_[k][d + 1]) return;  // an empty domain intersects nothing (never feasible)
+// Taking domain d at level k (its own bit is set by the caller) takes its
+// ancestors and its descendants at every other level.
+void HostWalk::take_marks(uint32_t d, uint32_t k) {
+    const uint32_t* fl = fl_[k].data();
+    if (fl[d] == fl[d + 1]) return;  // an empty domain intersects nothing (never feasible)
     uint32_t dd = d;
     for (int kk = (int)k - 1; kk >= 0; --kk) {
         dd = (uint32_t)par_[kk + 1][dd];
@@ -237,37 +239,43 @@ uint32_t HostWalk::place(const uint64_t* slots, const uint32_t* run_class, const
                          int32_t* assign) {
     build_feasibility(slots);
     std::fill(taken_.begin(), taken_.end(), 0ull);
-    std::fill(cursor_.begin(), cursor_.end(), 0u);
+    // per class, everything a run needs in one record (cfg5: ~500 runs of one
+    // job each, so the per-run set-up is most of the walk)
+    cw_.resize(C_);
+    for (uint32_t c = 0; c < C_; ++c) {
+        const uint32_t k = level_[c];
+        cw_[c] = ClassWalk{feas_.data() + woff_[c], taken_.data() + toff_[k], D_[k], (D_[k] + 63) / 64, k, 0u};
+    }
     uint32_t placed = 0;
     size_t j = 0;
+    const bool marks = K_ > 1;
     for (uint32_t r = 0; r < n_runs; ++r) {
-        const uint32_t c = run_class[r], k = level_[c], D = D_[k], nw = (D + 63) / 64;
-        const uint64_t* F = feas_.data() + woff_[c];
-        uint64_t* T = taken_.data() + toff_[k];
+        ClassWalk& cw = cw_[run_class[r]];
         const uint32_t n = run_len[r];
-        uint32_t cur = cursor_[c], i = 0;
-        if (cur < D) {
+        uint32_t cur = cw.cursor, i = 0;
+        if (cur < cw.D) {
             // The run's jobs take the free feasible bits in order. Taking a
             // domain marks other levels only (ancestors above, descendants
             // below), so at this level the only bits that change are the ones
             // the run itself takes: the current word's free bits are kept
             // across jobs and re-read only when a new word starts.
+            const uint64_t* F = cw.F;
+            uint64_t* T = cw.T;
             uint32_t w = cur >> 6;
             uint64_t bits = F[w] & ~T[w] & (~0ull << (cur & 63));
-            const bool marks = K_ > 1;
             for (; i < n; ++i) {
-                while (bits == 0 && ++w < nw) bits = F[w] & ~T[w];
+                while (bits == 0 && ++w < cw.nw) bits = F[w] & ~T[w];
                 if (bits == 0) break;
                 const uint32_t b = (uint32_t)__builtin_ctzll(bits);
                 const uint32_t d = w * 64 + b;
                 bits &= bits - 1;
                 assign[j + i] = (int32_t)d;
                 T[w] |= 1ull << b;
-                if (marks) take(d, k);
+                if (marks) take_marks(d, cw.k);
                 cur = d + 1;
             }
             placed += i;
-            cursor_[c] = i < n ? D : cur;
+            cw.cursor = i < n ? cw.D : cur;
         }
         for (; i < n; ++i) assign[j + i] = -1;
         j += n;
@@ -277,16 +285,15 @@ uint32_t HostWalk::place(const uint64_t* slots, const uint32_t* run_class, const
 
 }  // namespace jsp
 
-// Internal entry for the CPU tests of the host walk (tests/test_host_walk.py):
-// not part of include/jsplace.h. The hierarchy tables are derived from
-// first_leaf as jsp_topology_upload derives them.
-extern "C" int jspi_walk_test(uint32_t K, const uint32_t* D, const uint32_t* const* first_leaf, uint32_t C,
-                              const uint32_t* cls_level, const uint32_t* cls_pods, uint32_t n_blocks,
-                              const uint32_t* blk_l0, const uint32_t* blk_l1, uint32_t groups, uint32_t cpg,
-                              const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len,
-                              uint32_t n_runs, int32_t* assign) {
+// Internal entries for the CPU tests of the host walk (tests/test_host_walk.py)
+// and its timing (tools/walk_bench.py): not part of include/jsplace.h. The
+// hierarchy tables are derived from first_leaf as jsp_topology_upload derives
+// them.
+static bool walk_setup(jsp::HostWalk& w, uint32_t K, const uint32_t* D, const uint32_t* const* first_leaf, uint32_t C,
+                       const uint32_t* cls_level, const uint32_t* cls_pods, uint32_t n_blocks, const uint32_t* blk_l0,
+                       const uint32_t* blk_l1, uint32_t groups, uint32_t cpg) {
     using jsp::kMaxLevels;
-    if (K < 1 || K > kMaxLevels) return -1;
+    if (K < 1 || K > kMaxLevels) return false;
     std::vector<uint32_t> fl[kMaxLevels], cs[kMaxLevels];
     std::vector<int32_t> par[kMaxLevels];
     for (uint32_t k = 0; k < K; ++k) fl[k].assign(first_leaf[k], first_leaf[k] + D[k] + 1);
@@ -308,10 +315,39 @@ extern "C" int jspi_walk_test(uint32_t K, const uint32_t* D, const uint32_t* con
         cls[c].level = cls_level[c];
         cls[c].pods = cls_pods[c];
     }
-    jsp::HostWalk w;
     w.set_topology(K, D, fl, cs, par);
     w.set_classes(cls);
     w.set_tiles(std::vector<uint32_t>(blk_l0, blk_l0 + n_blocks), std::vector<uint32_t>(blk_l1, blk_l1 + n_blocks),
                 groups, cpg);
+    return true;
+}
+
+extern "C" int jspi_walk_test(uint32_t K, const uint32_t* D, const uint32_t* const* first_leaf, uint32_t C,
+                              const uint32_t* cls_level, const uint32_t* cls_pods, uint32_t n_blocks,
+                              const uint32_t* blk_l0, const uint32_t* blk_l1, uint32_t groups, uint32_t cpg,
+                              const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len,
+                              uint32_t n_runs, int32_t* assign) {
+    jsp::HostWalk w;
+    if (!walk_setup(w, K, D, first_leaf, C, cls_level, cls_pods, n_blocks, blk_l0, blk_l1, groups, cpg)) return -1;
     return (int)w.place(slots, run_class, run_len, n_runs, assign);
+}
+
+// The same walk `iters` times on one set-up walker: mean ns per place() in
+// out_ns[0], and in out_ns[1] the feasibility build alone.
+extern "C" int jspi_walk_bench(uint32_t K, const uint32_t* D, const uint32_t* const* first_leaf, uint32_t C,
+                               const uint32_t* cls_level, const uint32_t* cls_pods, uint32_t n_blocks,
+                               const uint32_t* blk_l0, const uint32_t* blk_l1, uint32_t groups, uint32_t cpg,
+                               const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len,
+                               uint32_t n_runs, int32_t* assign, uint32_t iters, double* out_ns) {
+    jsp::HostWalk w;
+    if (!walk_setup(w, K, D, first_leaf, C, cls_level, cls_pods, n_blocks, blk_l0, blk_l1, groups, cpg)) return -1;
+    uint32_t placed = 0;
+    auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; i < iters; ++i) placed = w.place(slots, run_class, run_len, n_runs, assign);
+    auto t1 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; i < iters; ++i) w.feasibility_only(slots);
+    auto t2 = std::chrono::steady_clock::now();
+    out_ns[0] = std::chrono::duration<double, std::nano>(t1 - t0).count() / std::max<uint32_t>(iters, 1);
+    out_ns[1] = std::chrono::duration<double, std::nano>(t2 - t1).count() / std::max<uint32_t>(iters, 1);
+    return (int)placed;
 }

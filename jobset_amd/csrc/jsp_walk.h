@@ -51,10 +51,19 @@ public:
     // The feasibility bitmaps of the last request (tests / diagnostics):
     // words [woff[c], woff[c+1]) of class c.
     const std::vector<uint64_t>& feas() const { return feas_; }
+    // the feasibility build alone (timing: tools/walk_bench.py)
+    void feasibility_only(const uint64_t* slots) { build_feasibility(slots); }
 
 private:
     void build_feasibility(const uint64_t* slots);
-    void take(uint32_t d, uint32_t k);
+    void take_marks(uint32_t d, uint32_t k);
+
+    struct ClassWalk {
+        const uint64_t* F;  // feasibility words
+        uint64_t* T;        // taken words at the class's level
+        uint32_t D, nw, k;  // domains at that level, their words, the level
+        uint32_t cursor;    // first domain not yet passed
+    };
 
     uint32_t K_ = 0, L_ = 0, C_ = 0, groups_ = 1, cpg_ = 1, nw_ = 1;
     uint32_t D_[kMaxLevels] = {0, 0, 0, 0};
@@ -67,7 +76,7 @@ private:
     std::vector<uint64_t> feas_;             // feasibility words of every class (woff_ layout)
     std::vector<uint64_t> sums_;             // clamped capacity sums of every upper class's domains (uoff_ layout)
     std::vector<uint64_t> taken_;            // taken domains per level (toff_ layout)
-    std::vector<uint32_t> cursor_;           // per class: first domain not yet passed
+    std::vector<ClassWalk> cw_;              // per class, set up per request
     bool any_upper_ = false;
 };
 
