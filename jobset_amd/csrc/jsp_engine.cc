@@ -156,6 +156,7 @@ struct TestHooks {
                                     //   after a look-back instead of tile bitmaps (A/B)
     uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
+    bool warm = true;               // warm=0: no prefetch of the engine's lines at call entry (A/B)
 };
 
 TestHooks read_hooks() {
@@ -185,6 +186,7 @@ TestHooks read_hooks() {
         else if (k == "svc_entries") h.svc_entries = v != 0;
         else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
+        else if (k == "warm") h.warm = v != 0;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -2253,10 +2255,37 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
                                  const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner,
                                  std::chrono::steady_clock::time_point t0);
 
+// The first calls of a recovery run on a host core that slept for hours (or
+// for the bench's 60 ms): its caches are gone, and every line a call touches
+// would miss in turn -- the engine's fields, the request and answer lines in
+// pinned memory, the tables the answer is expanded with. Touched up front by
+// independent prefetches their misses overlap instead. (On a warm core: ~100
+// prefetches of lines already cached.)
+static inline void warm_lines(const void* p, size_t bytes) {
+    const char* c = static_cast<const char*>(p);
+    if (!c) return;
+    for (size_t i = 0; i < bytes; i += 64) __builtin_prefetch(c + i, 0, 3);
+}
+
+static void warm_engine(const jsp_engine* e, bool place) {
+    if (!e->hooks.warm) return;
+    warm_lines(e, std::min<size_t>(sizeof(jsp_engine), 16384));
+    warm_lines(e->svc.box.p, 128);
+    warm_lines(e->h_patch_done.p, 128);
+    if (place) {
+        warm_lines(e->svc.words.p, std::min<size_t>(e->svc.words.bytes, 4096));
+        warm_lines(e->svc.bits.p, std::min<size_t>(e->svc.bits.bytes, 8192));
+        warm_lines(e->blk_l0.data(), 4 * e->blk_l0.size());
+    } else {
+        warm_lines(e->h_patch.p, std::min<size_t>(e->h_patch.bytes, 1024));
+    }
+}
+
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
                        const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner); }
+    warm_engine(e, false);
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     {
@@ -2638,6 +2667,7 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::place(e->multi, run_class, run_len, n_runs, assign_out, tally_out, occ_out, stats); }
+    warm_engine(e, true);
     auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
     if (int rc = ready(e, true)) return rc;
