@@ -156,7 +156,8 @@ struct TestHooks {
                                     //   after a look-back instead of tile bitmaps (A/B)
     uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
-    bool warm = true;               // warm=0: no prefetch of the engine's lines at call entry (A/B)
+    uint32_t warm = 2;              // warm=N: call-entry prefetch, 0 none, 1 the engine's data lines,
+                                    //   2 also the hot code (A/B)
 };
 
 TestHooks read_hooks() {
@@ -186,7 +187,7 @@ TestHooks read_hooks() {
         else if (k == "svc_entries") h.svc_entries = v != 0;
         else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
-        else if (k == "warm") h.warm = v != 0;
+        else if (k == "warm") h.warm = (uint32_t)v;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -2267,6 +2268,19 @@ static inline void warm_lines(const void* p, size_t bytes) {
     for (size_t i = 0; i < bytes; i += 64) __builtin_prefetch(c + i, 0, 3);
 }
 
+// The code of the call's hot path into the core's (unified) L2 as well: a
+// slept core fetches it from memory otherwise, one miss after another. The
+// functions' entry addresses, 2 KB on from each (their bodies are of that
+// order; a prefetch past a function's end fetches a neighbour's code, which
+// costs nothing).
+static void warm_code(bool place) {
+    const void* fp[] = {reinterpret_cast<const void*>(&jsp_place), reinterpret_cast<const void*>(&svc_place),
+                        reinterpret_cast<const void*>(&svc_wait_bits), reinterpret_cast<const void*>(&jsp_snapshot_patch),
+                        reinterpret_cast<const void*>(&snapshot_patch_locked), reinterpret_cast<const void*>(&patch_wait)};
+    const int n = sizeof fp / sizeof fp[0];
+    for (int i = place ? 0 : 3; i < (place ? 3 : n); ++i) warm_lines(fp[i], 2048);
+}
+
 static void warm_engine(const jsp_engine* e, bool place) {
     if (!e->hooks.warm) return;
     warm_lines(e, std::min<size_t>(sizeof(jsp_engine), 16384));
@@ -2278,7 +2292,9 @@ static void warm_engine(const jsp_engine* e, bool place) {
         warm_lines(e->blk_l0.data(), 4 * e->blk_l0.size());
     } else {
         warm_lines(e->h_patch.p, std::min<size_t>(e->h_patch.bytes, 1024));
+        warm_lines(e->svc.pstage.p, 256);
     }
+    if (e->hooks.warm >= 2) warm_code(place);
 }
 
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
@@ -2678,6 +2694,9 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (int rc = check_runs(e, run_class, run_len, n_runs, &J64)) return rc;
     const uint32_t J = (uint32_t)J64;
     if (J > 0 && !assign_out) return set_err(JSP_EINVAL, "assign_out is NULL");
+    if (e->hooks.warm)  // the caller's assign[], written by the answer's expansion: for write, ahead of the wait
+        for (size_t i = 0; i < std::min<size_t>((size_t)J * 4, 16384); i += 64)
+            __builtin_prefetch(reinterpret_cast<char*>(assign_out) + i, 1, 3);
     const bool want_tally = (tally_out && e->C > 0) || occ_out;
     if (!want_tally && J < jsp::kReqPatchInline && svc_ok(e)) {  // J and the request bits share a word
         const auto t1 = std::chrono::steady_clock::now();
