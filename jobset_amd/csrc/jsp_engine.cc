@@ -156,8 +156,7 @@ struct TestHooks {
                                     //   after a look-back instead of tile bitmaps (A/B)
     uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
-    uint32_t warm = 2;              // warm=N: call-entry prefetch, 0 none, 1 the engine's data lines,
-                                    //   2 also the hot code (A/B)
+    bool warm = true;               // warm=0: no call-entry prefetch of the engine's lines (A/B)
 };
 
 TestHooks read_hooks() {
@@ -187,7 +186,7 @@ TestHooks read_hooks() {
         else if (k == "svc_entries") h.svc_entries = v != 0;
         else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
-        else if (k == "warm") h.warm = (uint32_t)v;
+        else if (k == "warm") h.warm = v != 0;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -2261,24 +2260,15 @@ static int snapshot_patch_locked(jsp_engine* e, const uint32_t* rows, uint32_t n
 // would miss in turn -- the engine's fields, the request and answer lines in
 // pinned memory, the tables the answer is expanded with. Touched up front by
 // independent prefetches their misses overlap instead. (On a warm core: ~100
-// prefetches of lines already cached.)
+// prefetches of lines already cached.) Measured on the cold recovery, data
+// lines only (tools/warm_ab.py, profiles/r05/probes/warm_ab.txt): cfg2 p50
+// 11.0 -> 9.4 us at a 10 ms gap on one box, 16.7 -> 11.8 us at 1 ms on a
+// slower-waking one; prefetching the hot code into L2 as well showed no
+// consistent gain and is not done.
 static inline void warm_lines(const void* p, size_t bytes) {
     const char* c = static_cast<const char*>(p);
     if (!c) return;
     for (size_t i = 0; i < bytes; i += 64) __builtin_prefetch(c + i, 0, 3);
-}
-
-// The code of the call's hot path into the core's (unified) L2 as well: a
-// slept core fetches it from memory otherwise, one miss after another. The
-// functions' entry addresses, 2 KB on from each (their bodies are of that
-// order; a prefetch past a function's end fetches a neighbour's code, which
-// costs nothing).
-static void warm_code(bool place) {
-    const void* fp[] = {reinterpret_cast<const void*>(&jsp_place), reinterpret_cast<const void*>(&svc_place),
-                        reinterpret_cast<const void*>(&svc_wait_bits), reinterpret_cast<const void*>(&jsp_snapshot_patch),
-                        reinterpret_cast<const void*>(&snapshot_patch_locked), reinterpret_cast<const void*>(&patch_wait)};
-    const int n = sizeof fp / sizeof fp[0];
-    for (int i = place ? 0 : 3; i < (place ? 3 : n); ++i) warm_lines(fp[i], 2048);
 }
 
 static void warm_engine(const jsp_engine* e, bool place) {
@@ -2294,7 +2284,6 @@ static void warm_engine(const jsp_engine* e, bool place) {
         warm_lines(e->h_patch.p, std::min<size_t>(e->h_patch.bytes, 1024));
         warm_lines(e->svc.pstage.p, 256);
     }
-    if (e->hooks.warm >= 2) warm_code(place);
 }
 
 int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the call-entry prefetch of the engine's lines (jsp_engine.cc
-warm_engine; test hook warm=0 turns it off, warm=1 keeps the data lines only) on the realistic cold recovery
+warm_engine; test hook warm=0 turns it off) on the realistic cold recovery
 of cfg2: sleep 60 ms, one-row patch, gap, jsp_place, timed in C
 (jsp_recovery_loop), default and parked service. Alternating blocks per
 variant; p50 / p95 / p99 of patch + place, and the patch and place p50.
@@ -23,7 +23,7 @@ def main():
     p = synth.config2()
     res = {}
     for rep in range(reps):
-        for hooks in ("", "warm=1", "warm=0"):
+        for hooks in ("", "warm=0"):
             os.environ["JSP_TEST_HOOKS"] = hooks
             eng = Engine(0)
             eng.load(p)
@@ -34,7 +34,7 @@ def main():
                 for gap in (1.0, 10.0):
                     rows = np.array([(t * 7919 + rep) % p.nodes.n_nodes for t in range(trials)], dtype=np.uint32)
                     out = call.recovery(trials, 60_000.0, gap * 1e3, rows, p.nodes.taints[rows])
-                    res.setdefault((hooks or "warm=2", parked, gap), []).append(out)
+                    res.setdefault((hooks or "warm=1", parked, gap), []).append(out)
                 eng.service_stop()
             eng.set_service(True)
             eng.close()
