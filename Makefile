@@ -125,3 +125,8 @@ tools/bin/ab_inlinewake/libjsplace.so: jobset_amd/csrc/jsp_engine.cc build/jsp_k
 tools/bin/stop_anatomy: tools/stop_anatomy.hip
 	@mkdir -p tools/bin
 	$(HIPCC) --offload-arch=gfx950 -O3 -std=c++17 -o $@ $<
+# A/B build: real-time stamps inside the resident evaluation (slots 3, 4, 6, 7)
+tools/bin/ab_eval/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_eval tools/bin/ab_eval
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_EVALSTAMP -c -o build/ab_eval/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_eval/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl

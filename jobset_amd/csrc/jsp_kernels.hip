@@ -3342,10 +3342,25 @@ __device__ __forceinline__ uint32_t wave_off(uint4 ws, uint32_t w) {
     return w == 0 ? 0u : w == 1 ? e1 : w == 2 ? e2 : e3;
 }
 
+// A/B build (tools/bin/ab_eval, -DJSP_AB_EVALSTAMP): real-time stamps inside
+// the resident evaluation, in the service's stamp slots the bitmap path leaves
+// free (3 after the row predicates, 4 after the scans' LDS stores, 6 after the
+// barrier, 7 at the end). Diagnostic only.
+#ifdef JSP_AB_EVALSTAMP
+#define JSP_EVAL_STAMP(clk, s) \
+    do {                       \
+        if ((clk) && threadIdx.x == 0) (clk)[s] = (uint32_t)wall_clock64(); \
+    } while (0)
+#else
+#define JSP_EVAL_STAMP(clk, s) \
+    do {                       \
+    } while (0)
+#endif
+
 template <int W, int R>
 __device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const RowRegs<W, R>& x, const bool (&valid)[4],
                                               const ResidentLeaf& lf, JSP_LDS uint32_t* s_pre,
-                                              JSP_LDS uint32_t* s_wsum) {
+                                              JSP_LDS uint32_t* s_wsum, JSP_LDS uint32_t* clk = nullptr) {
     const int tid = threadIdx.x, lane = tid & 63;
     const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
     uint32_t cap[4];
@@ -3361,6 +3376,7 @@ __device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const Ro
     }
     const uint32_t a0 = v0[0], a1 = a0 + v0[1], a2 = a1 + v0[2], a3 = a2 + v0[3];
     const uint32_t b0 = v1[0], b1 = b0 + v1[1], b2 = b1 + v1[2], b3 = b2 + v1[3];
+    JSP_EVAL_STAMP(clk, 3);
     const uint32_t ia = wave_incl_scan(a3, lane), ib = wave_incl_scan(b3, lane);
     const uint32_t wa = ia - a3, wb = ib - b3;
     reinterpret_cast<JSP_LDS u32x4*>(s_pre)[tid] = u32x4{wa + a0, wa + a1, wa + a2, ia};
@@ -3369,7 +3385,9 @@ __device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const Ro
         s_wsum[wid] = ia;
         s_wsum[kTallyWaves + wid] = ib;
     }
+    JSP_EVAL_STAMP(clk, 4);
     __syncthreads();
+    JSP_EVAL_STAMP(clk, 6);
     if (!lf.live) return false;
     const u32x4 va = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum);
     const u32x4 vb = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum + kTallyWaves);
@@ -3378,6 +3396,7 @@ __device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const Ro
     const uint32_t la = lf.has_lo ? s_pre[lf.xb] : 0u, lb = lf.has_lo ? s_pre[kChunkRows + lf.xb] : 0u;
     const uint32_t capsum = (ha + wave_off(wsa, lf.wh)) - (lf.has_lo ? la + wave_off(wsa, lf.wb) : 0u);
     const uint32_t occsum = (hb + wave_off(wsb, lf.wh)) - (lf.has_lo ? lb + wave_off(wsb, lf.wb) : 0u);
+    JSP_EVAL_STAMP(clk, 7);
     return capsum >= k.pods && occsum == 0u;
 }
 
@@ -3519,7 +3538,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             // to memory may land after this tile's loads)
             if (Jw & kBellMicro) apply_microbox<W, R>(v.mbox, next, (bt.z & ~3u) + 4u * threadIdx.x, rows);
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
-                                                lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)));
+                                                lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)), clk);
             svc_stamp(clk, 2);
             if (v.bits) bitmap_finish(tile, ok, next, v.bits, s_x + 4);
             else compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
