@@ -3337,9 +3337,10 @@ __device__ __forceinline__ ResidentLeaf resident_leaf(const TallyArgs& a, uint4 
     return f;
 }
 
+// Sum of the wave totals before wave w (0..3), branch-free: three selects and
+// an add (a nested conditional compiled to divergent branches here).
 __device__ __forceinline__ uint32_t wave_off(uint4 ws, uint32_t w) {
-    const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
-    return w == 0 ? 0u : w == 1 ? e1 : w == 2 ? e2 : e3;
+    return (w > 0u ? ws.x : 0u) + (w > 1u ? ws.y : 0u) + (w > 2u ? ws.z : 0u);
 }
 
 // A/B build (tools/bin/ab_eval, -DJSP_AB_EVALSTAMP): real-time stamps inside
@@ -3392,8 +3393,11 @@ __device__ __forceinline__ bool resident_eval(const ClassRegs<W, R>& k, const Ro
     const u32x4 va = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum);
     const u32x4 vb = *reinterpret_cast<const JSP_LDS u32x4*>(s_wsum + kTallyWaves);
     const uint4 wsa = make_uint4(va[0], va[1], va[2], va[3]), wsb = make_uint4(vb[0], vb[1], vb[2], vb[3]);
+    // all four prefix reads unconditional (xb = 0 when the leaf starts the
+    // chunk: a valid address whose value is dropped), then selects -- no
+    // divergent branches around the LDS reads
     const uint32_t ha = s_pre[lf.xh], hb = s_pre[kChunkRows + lf.xh];
-    const uint32_t la = lf.has_lo ? s_pre[lf.xb] : 0u, lb = lf.has_lo ? s_pre[kChunkRows + lf.xb] : 0u;
+    const uint32_t la = s_pre[lf.xb], lb = s_pre[kChunkRows + lf.xb];
     const uint32_t capsum = (ha + wave_off(wsa, lf.wh)) - (lf.has_lo ? la + wave_off(wsa, lf.wb) : 0u);
     const uint32_t occsum = (hb + wave_off(wsb, lf.wh)) - (lf.has_lo ? lb + wave_off(wsb, lf.wb) : 0u);
     JSP_EVAL_STAMP(clk, 7);
