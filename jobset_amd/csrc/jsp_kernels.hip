@@ -90,6 +90,11 @@ __device__ __forceinline__ JSP_LDS T* lds_ptr(T* p) {
 // Inclusive wave64 prefix sum on the VALU with DPP (no LDS traffic):
 // row_shr 1/2/4/8 scan each 16-lane row, row_bcast15 / row_bcast31 carry the
 // row totals across rows (GFX9/CDNA DPP controls).
+// s_waitcnt vmcnt(0) with the other counters unconstrained (gfx9 encoding:
+// vmcnt bits 3:0 and 15:14, expcnt 6:4, lgkmcnt 11:8), as the builtin's
+// immediate: the compiler's wait insertion sees it, unlike inline asm.
+constexpr int kWaitVmcnt0 = 0x0F70;
+
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x, int /*lane*/) {
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
@@ -2870,13 +2875,16 @@ __device__ __forceinline__ void compact_finish(const TallyArgs& a, uint32_t tile
 // line with one store instruction: one whole-line write to host memory
 // instead of four partial ones (each a read-modify-write there, and a
 // snoop of the host's polling copy).
+// The line goes out from the last wave, not wave 0: a host store retires
+// only after a link round trip, and wave 0's thread 0 polls the bell for the
+// next request -- its first poll would wait (vmcnt) for these stores.
 __device__ __forceinline__ void bitmap_finish(uint32_t tile, bool ok, uint32_t tag, unsigned long long* bits,
                                               uint32_t* s_w) {
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const uint64_t word = __ballot(ok);
     if (lane < 2) s_w[2 * wid + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
     __syncthreads();
-    if (wid == 0 && lane < 8)
+    if (wid == kTallyWaves - 1 && lane < 8)
         __hip_atomic_store(bits + 8u * tile + (uint32_t)lane, ((unsigned long long)tag << 32) | s_w[lane],
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -3537,6 +3545,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             if (!use_cache) {  // first request, or rows patched since the last one: from memory (sc1, no stale L1)
                 const uint32_t row = (bt.z & ~3u) + 4u * threadIdx.x;
                 load_rows<W, R, true>(a, row, row < bt.w && row + 3 >= bt.z, rows);
+                // waited for here, on this path only: otherwise the waits the
+                // compiler places at the rows' first use, in code both paths
+                // share, would make the cached path wait for the previous
+                // request's host stores too (vmcnt counts them)
+                __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
             }
             // this request's micro-patch rows, from the microbox (their stores
             // to memory may land after this tile's loads)
@@ -3559,8 +3572,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             // row reads (svc_settle), so it follows the line without waiting
             // for the line's host write to complete -- a write to host memory
             // takes a link round trip to retire, and the tile polls the bell
-            // for the next request right away instead
-            if (threadIdx.x == 0) __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // for the next request right away instead. From the last wave,
+            // after its line stores (bitmap_finish): wave 0 polls the bell,
+            // and its first poll would wait for its own host stores (vmcnt)
+            if (threadIdx.x == kTallyThreads - 64)
+                __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
             signal_host_clk(v.done + tile, next, clk, clk_out);
         }
