@@ -3696,7 +3696,11 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     JSP_LDS uint32_t* clk = v.clk ? lds_ptr(s_clk + 1) : nullptr;
     uint32_t* clk_out = v.clk ? v.clk + kSvcClkSlots * tile : nullptr;
     while (true) {
-        if (threadIdx.x == 0) {
+        // the bell is polled from the last wave: wave 0 issues the tile's
+        // host stores (its lines, the done word; the last wave holds leaves
+        // only in tiles of more than 192), and a poll from it would first
+        // wait for them to retire, a link round trip (vmcnt counts stores)
+        if (threadIdx.x == kTallyThreads - 64) {
             uint32_t next = 0, dirty = 0;  // next 0: leave
             const uint64_t t0 = wall_clock64();
             while (true) {
@@ -3713,7 +3717,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
                 __builtin_amdgcn_s_sleep(1);
             }
-            if (next != 0) svc_stamp(clk, 0);
+            if (next != 0 && clk) clk[0] = (uint32_t)wall_clock64();  // svc_stamp's slot 0, from this thread
             s_x[0] = next;
             s_x[1] = dirty;
         }
