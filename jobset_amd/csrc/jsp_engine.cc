@@ -1301,6 +1301,8 @@ int svc_wait_entries(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint
 // holds no state of this request that a patch or the next request could
 // disturb, so neither waits for the tiles' done words (svc_settle); after an
 // answer complete before its last tiles, they do.
+constexpr uint32_t kPrefetchAhead = 8;  // answer lines in flight ahead of the one expanded
+
 int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_t* placed, bool* all) {
     auto& v = e->svc;
     const unsigned long long* b = v.bits.as<unsigned long long>();
@@ -1323,6 +1325,14 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
             }
             if (bad) break;
             if (t == 0) v.first_seen = std::chrono::steady_clock::now();
+            // the tiles answer within ~0.1 us of each other: once a line is in,
+            // the next ones have landed too (and the copies the spin's
+            // prefetches brought in before they landed are gone). Keep the
+            // lines kPrefetchAhead ahead in flight while this one is expanded.
+            if (t == 0)
+                for (uint32_t u = 1; u < n && u <= kPrefetchAhead; ++u) __builtin_prefetch(b + 8u * u, 0, 3);
+            else if (t + kPrefetchAhead < n)
+                __builtin_prefetch(b + 8u * (t + kPrefetchAhead), 0, 3);
             const uint32_t d0 = base + l0[t];
             for (uint32_t w = 0; w < 4 && j < J; ++w) {
                 // run by run: feasible leaves come in long runs (a word of 64
