@@ -1186,11 +1186,22 @@ int svc_wait_ready(jsp_engine* e) {
     return JSP_OK;
 }
 
-// Waits for every tile's done word == seq. kSvcGone: the service left before
-// answering (its stream finished).
+// Tile t's bitmap answer line to request seq has arrived whole (its 8
+// halves carry seq): the tile is past its row reads -- the bitmap answer's
+// done signal (timing off: the tiles write no done word then).
+static inline bool bits_line_done(const unsigned long long* b, uint32_t t, uint32_t seq) {
+    uint32_t bad = 0;
+    for (int k = 0; k < 8; ++k) bad |= (uint32_t)(__atomic_load_n(b + 8u * t + k, __ATOMIC_ACQUIRE) >> 32) ^ seq;
+    return bad == 0;
+}
+
+// Waits for every tile's done word == seq (the bitmap answer, timing off:
+// every tile's line). kSvcGone: the service left before answering (its stream
+// finished).
 int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     auto& v = e->svc;
     const uint32_t* words = v.words.as<uint32_t>();
+    const unsigned long long* lines = v.bitmap && !v.clk ? v.bits.as<unsigned long long>() : nullptr;
     const uint32_t n = v.nb;
     const bool split = v.shape == 3;
     // compaction: tiles 0..i-1 have answered, so assign[] up to about i/n of
@@ -1201,7 +1212,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     uint32_t i = 0;
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
-        while (i < n && __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq) {
+        while (i < n && (lines ? bits_line_done(lines, i, seq) : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq)) {
             if (split) e->walk.prefetch_tile(v.split.as<uint64_t>(), i);  // its slots are final: start their misses
             ++i;
             if (as) {
@@ -1214,7 +1225,8 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {
                 for (; i < n; ++i)
-                    if (__atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq) return kSvcGone;
+                    if (lines ? !bits_line_done(lines, i, seq) : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq)
+                        return kSvcGone;
                 return JSP_OK;
             }
             if (q != hipErrorNotReady) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));

@@ -3568,15 +3568,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             cached = row_cache != nullptr;
         }
         if (v.bits && !clk_out) {
-            // bitmap answer: the done word only says this tile is past its
-            // row reads (svc_settle), so it follows the line without waiting
-            // for the line's host write to complete -- a write to host memory
-            // takes a link round trip to retire, and the tile polls the bell
-            // for the next request right away instead. From the last wave,
-            // after its line stores (bitmap_finish): wave 0 polls the bell,
-            // and its first poll would wait for its own host stores (vmcnt)
-            if (threadIdx.x == kTallyThreads - 64)
-                __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // bitmap answer: no done word. It would only say that this tile is
+            // past its row reads, and the tile's answer line (every half
+            // tagged with the request) says as much: the host's settle reads
+            // the lines (svc_wait) -- one host write per tile and request, not two
         } else {
             signal_host_clk(v.done + tile, next, clk, clk_out);
         }
