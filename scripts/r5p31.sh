@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest tests/test_service_gpu.py tests/test_engin
 tail -2 $out/pytest.log
 node=$(cat /sys/bus/pci/devices/$(python -c "import ctypes;h=ctypes.CDLL('libamdhip64.so');b=ctypes.create_string_buffer(64);h.hipDeviceGetPCIBusId(b,64,0);print(b.value.decode().lower())")/numa_node)
 cpus=$(cat /sys/devices/system/node/node$node/cpulist)
-JSP_LIB_PATH=tools/bin/ab_eval/libjsplace.so timeout -k 10 200 taskset -c $cpus python tools/svc_probe.py 1000 2 > $out/svc_eval.txt 2>&1 || { cat $out/svc_eval.txt; exit 3; }
+timeout -k 10 200 taskset -c $cpus python tools/svc_probe.py 1000 2 > $out/svc_eval.txt 2>&1 || { cat $out/svc_eval.txt; exit 3; }
 grep -v amdgpu $out/svc_eval.txt
 timeout -k 10 200 taskset -c $cpus python tools/split_probe.py > $out/split.txt 2>&1 || { cat $out/split.txt; exit 5; }
 grep -v amdgpu $out/split.txt
