@@ -3731,10 +3731,9 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     svc_stamp(clk, 4);
 #endif
         if (!clk_out) {
-            // the tagged lines are the answer; the done word only says this
-            // tile is past its row reads, so it follows without waiting for
-            // the lines' host writes to retire
-            if (threadIdx.x == 0) __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the tagged lines are the answer, and they also say that this
+            // tile is past its row reads: no done word (the host's settle
+            // reads the lines, svc_wait) -- fewer host writes per request
         } else {
             signal_host_clk(v.done + tile, next, clk, clk_out);
         }
