@@ -1205,6 +1205,13 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     const uint32_t n = v.nb;
     const bool split = v.shape == 3;
     const bool split_lines = split && !v.clk;  // the split service's tagged lines and records (no done words)
+    // every tile's line(s) at once: read one after another they would miss
+    // one after another (a settle usually comes after the host slept or
+    // worked, with none of them cached)
+    if (lines)
+        for (uint32_t t = 0; t < n; ++t) __builtin_prefetch(lines + 8u * t, 0, 3);
+    if (split_lines)
+        for (uint32_t t = 0; t < n; ++t) e->walk.prefetch_tile(v.split.as<uint64_t>(), t);
     // compaction: tiles 0..i-1 have answered, so assign[] up to about i/n of
     // J is final (tiles own consecutive ranges of roughly equal size): start
     // those lines' misses before the copy-out (cfg2 copy-out 0.55 us cold)
