@@ -1195,8 +1195,8 @@ static inline bool bits_line_done(const unsigned long long* b, uint32_t t, uint3
     return bad == 0;
 }
 
-// Waits for every tile's done word == seq (timing off, the bitmap answer and
-// the split service: every tile's tagged line(s) instead). kSvcGone: the service left before answering (its stream
+// Waits for every tile's done word == seq (timing off, the bitmap answer:
+// every tile's tagged line instead). kSvcGone: the service left before answering (its stream
 // finished).
 int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     auto& v = e->svc;
@@ -1204,14 +1204,15 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     const unsigned long long* lines = v.bitmap && !v.clk ? v.bits.as<unsigned long long>() : nullptr;
     const uint32_t n = v.nb;
     const bool split = v.shape == 3;
-    const bool split_lines = split && !v.clk;  // the split service's tagged lines and records (no done words)
+    // (the split service writes done words for requests without jobs, the
+    // only ones this waits for; with jobs the host reads its lines,
+    // svc_wait_split)
     // every tile's line(s) at once: read one after another they would miss
     // one after another (a settle usually comes after the host slept or
     // worked, with none of them cached)
     if (lines)
         for (uint32_t t = 0; t < n; ++t) __builtin_prefetch(lines + 8u * t, 0, 3);
-    if (split_lines)
-        for (uint32_t t = 0; t < n; ++t) e->walk.prefetch_tile(v.split.as<uint64_t>(), t);
+
     // compaction: tiles 0..i-1 have answered, so assign[] up to about i/n of
     // J is final (tiles own consecutive ranges of roughly equal size): start
     // those lines' misses before the copy-out (cfg2 copy-out 0.55 us cold)
@@ -1220,9 +1221,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
     uint32_t i = 0;
     QueryPacer qp;
     for (uint64_t spins = 1;; ++spins) {
-        while (i < n && (lines         ? bits_line_done(lines, i, seq)
-                         : split_lines ? e->walk.tile_ready(v.split.as<uint64_t>(), i, seq)
-                                       : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq)) {
+        while (i < n && (lines ? bits_line_done(lines, i, seq) : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) == seq)) {
             if (split) e->walk.prefetch_tile(v.split.as<uint64_t>(), i);  // its slots are final: start their misses
             ++i;
             if (as) {
@@ -1235,9 +1234,7 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {
                 for (; i < n; ++i)
-                    if (lines         ? !bits_line_done(lines, i, seq)
-                        : split_lines ? !e->walk.tile_ready(v.split.as<uint64_t>(), i, seq)
-                                      : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq)
+                    if (lines ? !bits_line_done(lines, i, seq) : __atomic_load_n(words + i, __ATOMIC_ACQUIRE) != seq)
                         return kSvcGone;
                 return JSP_OK;
             }

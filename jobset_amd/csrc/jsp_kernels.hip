@@ -3696,7 +3696,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         // only in tiles of more than 192), and a poll from it would first
         // wait for them to retire, a link round trip (vmcnt counts stores)
         if (threadIdx.x == kTallyThreads - 64) {
-            uint32_t next = 0, dirty = 0;  // next 0: leave
+            uint32_t next = 0, dirty = 0, jobs = 0;  // next 0: leave
             const uint64_t t0 = wall_clock64();
             while (true) {
                 const unsigned long long m = __hip_atomic_load(v.bell, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -3707,6 +3707,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
                 if (q != seq && q != 0 && q != kSvcStop) {
                     next = q;
                     dirty = (uint32_t)(m >> 63);
+                    jobs = (uint32_t)(m >> 32) & ~(kReqDirty | kBellMicro);
                     break;
                 }
                 if (wall_clock64() - t0 > 2 * v.idle_ticks) break;
@@ -3715,11 +3716,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
             if (next != 0 && clk) clk[0] = (uint32_t)wall_clock64();  // svc_stamp's slot 0, from this thread
             s_x[0] = next;
             s_x[1] = dirty;
+            s_x[2] = jobs;
         }
         __syncthreads();
         const uint32_t next = s_x[0];
         if (next == 0) return;
         const bool use_cache = cached && s_x[1] == 0u;
+        const bool job_less = s_x[2] == 0u;  // a request without jobs: this tile writes its done word
         svc_stamp(clk, 1);
         tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), clk, row_cache, use_cache);
         cached = row_cache != nullptr;
@@ -3731,9 +3734,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     svc_stamp(clk, 4);
 #endif
         if (!clk_out) {
-            // the tagged lines are the answer, and they also say that this
-            // tile is past its row reads: no done word (the host's settle
-            // reads the lines, svc_wait) -- fewer host writes per request
+            // the tagged lines are the answer, and the host waits for them
+            // (svc_wait_split); a done word -- this tile is past its row reads
+            // -- only for a request without jobs (the warm-up after a wake),
+            // which the host settles later from the done words, contiguous
+            // where the lines are not: one host write per tile and request
+            if (job_less && threadIdx.x == 0)
+                __hip_atomic_store(v.done + tile, next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
             signal_host_clk(v.done + tile, next, clk, clk_out);
         }

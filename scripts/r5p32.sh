@@ -2,7 +2,7 @@
 # the settle's reading of the tiles' lines, prefetched: service GPU tests, then the bench's cold legs
 out=gpurun_out/r5/${1:-p32}
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest tests/test_service_gpu.py -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { tail -60 $out/pytest.log; exit 2; }
+timeout -k 10 600 python -u -m pytest tests/test_service_gpu.py tests/test_engine_gpu.py -x -q --timeout 120 --timeout-method thread > $out/pytest.log 2>&1 || { tail -60 $out/pytest.log; exit 2; }
 tail -1 $out/pytest.log
 timeout -k 10 500 python bench.py --gpus 1 --steps 20 --warmup 5 > $out/bench.json 2> $out/bench.err || { tail -30 $out/bench.err; exit 4; }
 python - <<PY
