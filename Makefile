@@ -4,7 +4,7 @@ ARCH ?= gfx950
 HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 CXX ?= g++
 CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
-HDR = include/jsplace.h include/jsk_host.h jobset_amd/csrc/jsp_internal.h jobset_amd/csrc/jsp_walk.h jobset_amd/csrc/jsp_multi.h
+HDR = include/jsplace.h include/jsplace_bench.h include/jsk_host.h jobset_amd/csrc/jsp_internal.h jobset_amd/csrc/jsp_walk.h jobset_amd/csrc/jsp_multi.h
 HOST_SRC = $(wildcard jobset_amd/csrc/host/*.cc)
 HOST_HDR = $(wildcard jobset_amd/csrc/host/*.h)
 HOST_OBJ = $(patsubst jobset_amd/csrc/host/%.cc,build/host_%.o,$(HOST_SRC))
@@ -71,11 +71,23 @@ build/asan/host_%.o: jobset_amd/csrc/host/%.cc $(HOST_HDR) $(HDR)
 build/asan/libjsplace.so: build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(ASAN_OBJ)
 	$(CXX) -shared -fsanitize=address,undefined -o $@ $^ -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64
 
+# ThreadSanitizer build of the host mirror (the engine objects as built):
+# tests/test_concurrency.py runs its concurrent host-mirror callers against it
+# with libtsan preloaded. Host code only.
+TSANFLAGS = -O1 -g -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter -fsanitize=thread -fno-omit-frame-pointer
+TSAN_OBJ = $(patsubst jobset_amd/csrc/host/%.cc,build/tsan/host_%.o,$(HOST_SRC))
+tsan: build/tsan/libjsplace.so
+build/tsan/host_%.o: jobset_amd/csrc/host/%.cc $(HOST_HDR) $(HDR)
+	@mkdir -p build/tsan
+	$(CXX) $(TSANFLAGS) -c -o $@ $<
+build/tsan/libjsplace.so: build/jsp_kernels.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(TSAN_OBJ)
+	$(CXX) -shared -fsanitize=thread -o $@ $^ -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lamdhip64 -ldl
+
 clean:
 	rm -rf build $(LIB)
 	$(MAKE) -s -C oracle clean
 
-.PHONY: all oracle clean diag sanitize
+.PHONY: all oracle clean diag sanitize tsan
 
 # achievable streaming ceiling (read-only and copy, cold and warm) at the placement kernels' byte counts
 tools/bin/stream_ceiling: tools/stream_ceiling.hip

@@ -10,28 +10,42 @@ tallies, decides feasibility and assigns all 990 jobs, and assign[] comes
 back to the caller's host buffer (placements/sec = J_placed /
 wall time of jsp_place including H2D and D2H). The snapshot is resident (its
 upload is the "post-delete snapshot ready" point and is not timed).
-`kernel_only_*` is the same placement from device-resident runs to a
+`kernel_only` is the same placement from device-resident runs to a
 device-resident assign[] (no host round trip).
+
+p99 recovery latency (`p99_recovery_us`): the realistic, cold recovery
+(failures are hours apart): the caller's thread sleeps past the resident
+service's idle exit, a watch event patches one row, and after the
+reconciler's round trip (1 ms) the recreate calls jsp_place; timed = the
+patch call + the place call, >= 1000 trials issued and timed in C
+(jspb_recovery_loop). Gaps 0 and 10 ms and the parked service are reported
+beside it, each next to the CPU evaluator's same recovery at equal sample
+size. The bench sets JSP_SERVICE_IDLE_MS=30 (unless given) so that a trial
+sleeps only 35 ms and 1000 trials fit the run; a 10 ms gap stays inside the
+idle limit's half, so the service stays up across it as with the default 50.
 
 `--gpus N` (torchrun, one rank per GPU): config 2 has ~0.4 MB of rows and does
 not shard usefully, so ranks run independent replicas (weak scaling, no
 data-path collective, SURVEY.md §8e "replicas only"); value = all ranks'
 placements / max-over-ranks time. The sharded path of config 4 (1M nodes,
 node dimension split over the ranks, per-leaf tallies SUM-all-reduced by RCCL)
-is reported beside it under "cfg4_1M".
+is reported beside it under "cfg4".
 
-Roofline: the dominant kernel's average duration comes from two HIP events
-recorded on the launch stream around K back-to-back launches; its algorithmic
-bytes are DESIGN.md §4's. `traffic` is the PMC-measured HBM bytes per launch
-of the same kernel from the committed rocprofv3 passes under profiles/
-(FETCH_SIZE x 2 for gfx950's wide-load halving + WRITE_SIZE, per
+Roofline: the dominant kernel's average duration comes from events on the
+dispatch packets of K back-to-back launches on the launch stream; its
+algorithmic bytes are DESIGN.md §4's. `traffic` is the PMC-measured HBM bytes
+per launch of the same kernel from the committed rocprofv3 passes under
+profiles/ (FETCH_SIZE x 2 for gfx950's wide-load halving + WRITE_SIZE, per
 MI355X_MICROARCH.md "HBM"), or null when no pass for it is committed.
 
 CPU baseline: oracle/cpu_fast.c, an optimized threaded evaluator of the same
 rules (bit-exact with the oracle), timed on this host at 1 thread, 2 threads
 (the reference manager's 2-CPU limit) and every core of the box's share.
 
-Prints ONE JSON line on rank 0.
+Prints ONE compact JSON line on rank 0 (build_line; tests/test_bench_line.py
+keeps it under the driver's 8 KB tail). Every measured figure, with its
+context, goes to the detail file (--detail-out, default
+gpurun_out/bench_detail.json); DESIGN.md §8 defines each field.
 """
 from __future__ import annotations
 
@@ -49,15 +63,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level parameters")
-SHAPES = {0: "three launches (tally -> feas -> assign + expand)", 1: "fused single launch",
-          2: "single-class compaction, one launch",
-          3: "single-class compaction answered by the resident service (no launch per placement)",
-          4: "fused shape answered by the resident service (no launch per placement)",
-          5: "split service: resident tiles tally and hand back per-domain feasibility, the host walks"}
+METRIC = "exclusive-topology placements/sec at 15k nodes; p99 recovery placement latency"
+LINE_MAX_BYTES = 6144  # the driver keeps the last 8 KB of stdout+stderr; leave room for stderr
+SHAPES = {0: "three launches", 1: "fused single launch", 2: "one-class compaction, one launch",
+          3: "compaction service (resident)", 5: "split service (resident tiles, host walk)"}
 # the launch shape the device path (jsp_place_device) takes for a host-API shape
 DEVICE_SHAPE = {3: 2, 4: 1, 5: 1}
 KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel",
           4: "place_fused_kernel", 5: "place_fused_kernel"}
+# cold recovery: the gap between the patch and the place (ms) -> share of --cold-trials
+COLD_GAPS = {1.0: 1.0, 0.0: 0.1, 10.0: 0.1}
+COLD_SLEEP_EXTRA_MS = 5.0  # a trial sleeps the idle limit plus this (the service has left)
 
 
 def tally_bytes(p) -> int:
@@ -145,8 +161,7 @@ def trace_avg_us(kernel: str):
     """Median duration (µs) of `kernel` in the newest committed rocprofv3
     kernel-trace summary under profiles/ (this bench run under the profiler),
     taken at the grid size with the most dispatches (the timed cfg2 loop):
-    the cross-check of the event-timed average, which also counts the gap
-    between back-to-back launches."""
+    the cross-check of the event-timed average."""
     for d in evidence_dirs():
         f = os.path.join(d, "summary.txt")
         if not os.path.exists(f):
@@ -181,11 +196,9 @@ def event_loop_us(fn, k: int, stream) -> float:
 
 def cold_us(fn, k: int, stream, scrub, dirty: bool = False) -> float:
     """Median µs of one call of `fn` with cold caches: before each call a
-    512 MiB buffer is read on the same stream (a sum: no lines dirtied, as the
-    read-only scrub of tools/stream_ceiling.hip), which evicts the 256 MiB
-    Infinity Cache and every XCD's L2; HIP events bracket the call. dirty=True
-    reads and writes it instead (add_): the call's misses then also pay the
-    write-back of the scrub's dirty lines."""
+    512 MiB buffer is read on the same stream (a sum: no lines dirtied), which
+    evicts the 256 MiB Infinity Cache and every XCD's L2; HIP events bracket
+    the call. dirty=True reads and writes it instead (add_)."""
     import torch
     s = torch.cuda.ExternalStream(stream) if stream else torch.cuda.default_stream()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -216,13 +229,23 @@ def cpu_threads() -> int:
 def time_cpu(fc, seconds: float):
     """µs per placement of the prepared FastCPU over a bounded sample, the
     placements timed in C (jspf_run_loop, batches of 64) like the GPU's
-    host-API loop (jsp_place_loop): no interpreter between the calls."""
+    host-API loop (jspb_place_loop): no interpreter between the calls."""
     fc.run()
     n, tot = 0, 0.0
     while tot < seconds * 1e6:
         tot += fc.run_loop(64)
         n += 64
     return tot / n, n, tot * 1e-6
+
+
+def _pct(lat, q):
+    return round(lat[min(len(lat) - 1, int(q * len(lat)))], 2)
+
+
+def pcts(lat):
+    lat = sorted(lat)
+    return {"p50_us": _pct(lat, 0.50), "p95_us": _pct(lat, 0.95), "p99_us": _pct(lat, 0.99),
+            "max_us": round(lat[-1], 2), "n": len(lat)}
 
 
 def host_api_latency(eng, p, trials: int, trial_fn=None):
@@ -248,9 +271,7 @@ def host_api_latency(eng, p, trials: int, trial_fn=None):
             t0 = time.perf_counter()
             call()
             lat.append((time.perf_counter() - t0) * 1e6)
-    lat.sort()
-    pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 1)  # noqa: E731
-    return {"p50_us": pct(0.50), "p99_us": pct(0.99), "n": len(lat)}
+    return pcts(lat)
 
 
 def settled_place(eng, job_class):
@@ -264,13 +285,11 @@ def settled_place(eng, job_class):
     return r
 
 
-def _pcts(lat):
-    lat = sorted(lat)
-    pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))], 1)  # noqa: E731
-    return {"p50_us": pct(0.50), "p95_us": pct(0.95), "p99_us": pct(0.99), "max_us": round(lat[-1], 1), "n": len(lat)}
-
-
-COLD_GAPS_MS = (0.0, 1.0, 10.0)
+def cold_plan(trials: int, gaps=COLD_GAPS):
+    """Trials per gap: the 1 ms gap (the headline's) gets all of `trials`,
+    the others a tenth (at least 20)."""
+    return {g: max(20, int(round(trials * share))) if share < 1.0 else trials for g, share in gaps.items()} \
+        if trials > 0 else {}
 
 
 def _recovery_rows(p, trials: int, gap: float):
@@ -280,14 +299,15 @@ def _recovery_rows(p, trials: int, gap: float):
 
 def _recovery_line(out):
     tot = out[:, 0] + out[:, 1]
-    line = _pcts(tot.tolist())
-    line.update({"patch_p50_us": _pcts(out[:, 0].tolist())["p50_us"], "patch_p99_us": _pcts(out[:, 0].tolist())["p99_us"],
-                 "place_p50_us": _pcts(out[:, 1].tolist())["p50_us"], "place_p99_us": _pcts(out[:, 1].tolist())["p99_us"],
+    line = pcts(tot.tolist())
+    pa, pl = pcts(out[:, 0].tolist()), pcts(out[:, 1].tolist())
+    line.update({"patch_p50_us": pa["p50_us"], "patch_p99_us": pa["p99_us"],
+                 "place_p50_us": pl["p50_us"], "place_p99_us": pl["p99_us"],
                  "gap_ms_p50": round(float(np.median(out[:, 2])) * 1e-3, 3)})
     return line
 
 
-def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
+def cold_recovery_latency(eng, p, plan, idle_ms: float):
     """The realistic recovery (failures are hours apart,
     keps/262-ConfigurableFailurePolicy/README.md:232-234): the resident
     service has idle-exited (the caller sleeps past JSP_SERVICE_IDLE_MS), a
@@ -298,76 +318,63 @@ def cold_recovery_latency(eng, p, trials: int, gaps_ms=COLD_GAPS_MS):
     patches are foreground deletes whose completion triggers the recreate
     (pkg/controllers/jobset_controller.go:553-576, 698-709), at least one
     API-server round trip (1 and 10 ms here); the gap itself is not counted.
-    The patch wakes the service (jsp_snapshot_patch, ABI v5). The trials run
-    in C (jsp_recovery_loop: sleep, patch, gap, place, each call timed by the
-    library's clock), as a cgo caller would make the calls -- no interpreter
-    waking up between them."""
+    The trials run in C (jspb_recovery_loop: sleep, patch, gap, place, each
+    call timed by the library's clock), as a cgo caller would make them."""
     from jobset_amd.snapshot import job_runs
-    if trials <= 0:
+    if not plan:
         return None
-    idle_ms = float(os.environ.get("JSP_SERVICE_IDLE_MS", "50"))
     call = eng.host_placer(*job_runs(p.job_class))
     call()
     out = {}
-    for gap in gaps_ms:
+    for gap, trials in plan.items():
         rows, vals = _recovery_rows(p, trials, gap)
         eng.timing(reset=True)
-        res = call.recovery(trials, (idle_ms + 10.0) * 1e3, gap * 1e3, rows, vals)
+        res = call.recovery(trials, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows, vals)
         t = eng.timing(reset=True)
         line = _recovery_line(res)
-        line["answered_by_service"] = f"{int(t.svc_calls)}/{trials}"
+        line["answered_by_service"] = int(t.svc_calls)
         out[f"gap_{gap:g}ms"] = line
-    out["note"] = (f"service idle-exited (sleep {idle_ms + 10:.0f} ms), then a one-row patch (jsp_snapshot_patch) and, "
-                   "after the stated gap, jsp_place; timed = patch call + place call, the gap excluded; trials issued "
-                   "and timed in C (jsp_recovery_loop)")
     return out
 
 
-def cpu_cold_recovery(p, trials: int, threads, idle_ms: float, gaps_ms=COLD_GAPS_MS):
+def cpu_cold_recovery(p, plan, threads, idle_ms: float):
     """The same recovery on the CPU evaluator, like for like with the GPU legs
     and, like them, timed in C (jspf_recovery_loop): after the same idle
     sleep, the same one-row patch (written into the evaluator's columns), the
     same gap (slept), then one placement; timed = patch + placement, the gap
-    excluded. Per gap, per thread count. (The evaluator's pool threads spin
-    between placements -- cpu_fast.c worker -- so its multi-thread legs start
-    with hot workers: a CPU-favouring baseline.) The widest leg (the CPU's
-    best median) runs the GPU leg's number of trials, so the two p99s are
-    order statistics of equal samples; the narrower legs run half as many
-    (context)."""
+    excluded. The widest leg (the box's share: the CPU's best median) runs the
+    GPU leg's number of trials, so the two p99s are order statistics of equal
+    samples; narrower legs run a fifth as many (context). (The evaluator's
+    pool threads spin between placements -- cpu_fast.c worker -- so its
+    multi-thread legs start with hot workers: a CPU-favouring baseline.)"""
     from oracle import oracle as O
     out = {}
-    for gap in gaps_ms:
+    for gap, trials in plan.items():
         legs = {}
         for th in threads:
             fc = O.FastCPU(th)
             fc.prepare(p)
             fc.run()
-            n = trials if th == max(threads) else max(10, trials // 2)
+            n = trials if th == max(threads) else max(20, trials // 5)
             rows, vals = _recovery_rows(p, n, gap)
-            res = fc.recovery_loop(n, (idle_ms + 10.0) * 1e3, gap * 1e3, rows, vals)
+            res = fc.recovery_loop(n, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows, vals)
             fc.close()
-            legs[f"{th}t"] = _pcts((res[:, 0] + res[:, 1]).tolist())
+            legs[f"{th}t"] = pcts((res[:, 0] + res[:, 1]).tolist())
         out[f"gap_{gap:g}ms"] = legs
     return out
 
 
 def cold_vs_cpu(cold, cpu):
     """Per gap: the GPU cold p50/p95/p99 beside the best like-for-like CPU
-    leg's -- the leg with the best median (the CPU configuration one would
-    deploy), at the GPU leg's sample size. The smallest p99 of any CPU leg is
-    kept beside it: a minimum over legs of a p99 that is a sample's maximum
-    picks the luckiest sample, so it is context, not the comparison."""
+    leg's (the leg with the best median, at the GPU leg's sample size)."""
     out = {}
     for g, legs in cpu.items():
         if g not in cold:
             continue
         name, best = min(legs.items(), key=lambda kv: kv[1]["p50_us"])
-        out[g] = {"gpu_p50_us": cold[g]["p50_us"], "gpu_p95_us": cold[g].get("p95_us"), "gpu_p99_us": cold[g]["p99_us"],
-                  "gpu_n": cold[g]["n"], "best_cpu_leg": name, "best_cpu_p50_us": best["p50_us"],
-                  "best_cpu_p95_us": best.get("p95_us"), "best_cpu_p99_us": best["p99_us"], "best_cpu_n": best["n"],
-                  "min_cpu_p99_any_leg_us": min(v["p99_us"] for v in legs.values()),
-                  "p50_gpu_over_cpu_speedup": round(best["p50_us"] / cold[g]["p50_us"], 3),
-                  "p99_gpu_over_cpu_speedup": round(best["p99_us"] / cold[g]["p99_us"], 3)}
+        out[g] = {"gpu_p50_us": cold[g]["p50_us"], "gpu_p95_us": cold[g]["p95_us"], "gpu_p99_us": cold[g]["p99_us"],
+                  "gpu_n": cold[g]["n"], "best_cpu_leg": name, "cpu_p50_us": best["p50_us"],
+                  "cpu_p95_us": best["p95_us"], "cpu_p99_us": best["p99_us"], "cpu_n": best["n"]}
     return out
 
 
@@ -394,22 +401,31 @@ def patched_step_us(eng, p, steps: int):
     """Host-API steps with one row patched before each placement (a watch
     event between recoveries): the patch rides in the next request
     (micro-patch) and the resident tiles apply it before they answer. µs per
-    (patch + place), timed in C (jsp_place_loop with patch rows), and the
-    same steps from a Python loop (two ctypes calls each) beside it."""
+    (patch + place), timed in C (jspb_place_loop with patch rows)."""
     from jobset_amd.snapshot import job_runs
     call = eng.host_placer(*job_runs(p.job_class))
     rows = np.array([(i * 7919) % p.nodes.n_nodes for i in range(16)], dtype=np.uint32)
     taints = np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)
     call.loop(20, rows, taints)
     tot, med, p99 = call.loop(steps, rows, taints)
-    patches = [eng.host_patcher(rows[i:i + 1], taints=taints[i:i + 1]) for i in range(16)]
-    t0 = time.perf_counter()
-    for i in range(steps):
-        patches[i % 16]()
-        call()
-    py = (time.perf_counter() - t0) * 1e6 / steps
-    return {"mean_us": round(tot / steps, 3), "p50_us": round(med, 2), "p99_us": round(p99, 2),
-            "python_loop_us": round(py, 3)}
+    return {"mean_us": round(tot / steps, 3), "p50_us": round(med, 2), "p99_us": round(p99, 2)}
+
+
+def cpu_legs(p, ref_assign, threads, seconds_total: float, placed: int):
+    """cpu_fast.c placing `p` at each thread count (bit-exact with the
+    engine's answer), each leg timed in C over a bounded sample."""
+    from oracle import oracle as O
+    legs = []
+    for th in threads:
+        fc = O.FastCPU(th)
+        fc.prepare(p)
+        a = fc.run()[0]
+        assert np.array_equal(a, ref_assign), "CPU evaluator differs from the engine"
+        us, n, dt = time_cpu(fc, seconds_total / len(threads))
+        fc.close()
+        legs.append({"threads": th, "us_per_placement": round(us, 2),
+                     "placements_per_s": round(placed / (us * 1e-6), 1), "runs": n, "seconds": round(dt, 2)})
+    return legs
 
 
 def device_set_leg(p4, ref_assign, steps: int):
@@ -428,18 +444,15 @@ def device_set_leg(p4, ref_assign, steps: int):
             call = ds.host_placer(*job_runs(p4.job_class))
             for _ in range(3):
                 call()
-            us = call.loop(steps)[0] / steps  # timed in C (jsp_place_loop), like the single-device leg
+            us = call.loop(steps)[0] / steps  # timed in C (jspb_place_loop), like the single-device leg
             sh, nd = ds.shards()
             exact = bool(np.array_equal(call.assign, ref_assign))
-            return {"device_ids": ids, "shards": sh, "devices": nd,
-                    "combine": "RCCL all-reduce, out of place (ncclCommInitAll in this process)" if nd > 1
-                    else "one device buffer, each shard writes its own leaf columns and feasibility bits (no add)",
-                    "us_per_step": round(us, 1), "placed": int((call.assign >= 0).sum()),
+            return {"device_ids": ids, "shards": sh, "devices": nd, "us_per_step": round(us, 1),
+                    "placed": int((call.assign >= 0).sum()),
                     "placements_per_s": round(int((call.assign >= 0).sum()) / (us * 1e-6), 1),
-                    "bit_exact_vs_single_device": exact, "steps": steps,
-                    "note": "host API (jsp_place): run list in, assign[] back in host memory; timed in C"}
+                    "bit_exact_vs_single_device": exact, "steps": steps}
     except Exception as ex:  # noqa: BLE001 -- reported in the line, never hidden
-        return {"device_ids": ids, "error": str(ex)}
+        return {"device_ids": ids, "error": str(ex)[:200]}
 
 
 def relaunch_with_torchrun(n: int) -> int:
@@ -471,10 +484,8 @@ def bind_to_gpu_node(device: int):
     manager gives a GPU pod the same with its single-numa-node policy): every
     host-API call polls pinned host memory the GPU writes, and a thread on the
     other socket pays the cross-socket coherence on each line. The CPU
-    baseline legs run under the same binding. Returns what was done (or why
-    not) for the bench line."""
+    baseline legs run under the same binding."""
     import ctypes
-    import glob
     try:
         hip = ctypes.CDLL("libamdhip64.so")
         buf = ctypes.create_string_buffer(64)
@@ -498,18 +509,138 @@ def bind_to_gpu_node(device: int):
     return {"bound": True, "gpu": bdf, "gpu_numa_node": node, "cpus": len(local), "of_allowed": len(allowed)}
 
 
+# ----------------------------------------------------------------------------- the printed line
+
+def _r(x, nd=2):
+    return None if x is None else round(float(x), nd)
+
+
+def _cold_row(v):
+    """[gpu p50, p95, p99, n, cpu p50, p95, p99, n] (µs) of one gap."""
+    return [v["gpu_p50_us"], v["gpu_p95_us"], v["gpu_p99_us"], v["gpu_n"],
+            v["cpu_p50_us"], v["cpu_p95_us"], v["cpu_p99_us"], v["cpu_n"]]
+
+
+def _cold_rows(vs):
+    return {g.replace("gap_", ""): _cold_row(v) for g, v in (vs or {}).items()} or None
+
+
+def build_line(d: dict) -> dict:
+    """The one JSON line the driver parses, from the bench's detail dict:
+    numbers only (DESIGN.md §8 defines every field), so that it stays under
+    LINE_MAX_BYTES whatever the measured values."""
+    c2 = d["cfg2"]
+    line = {
+        "metric": METRIC, "value": c2["value"], "unit": "placements/s", "n_gpus": d["world"],
+        "steps": d["steps"], "warmup": d["warmup"], "ms_per_step": c2["ms_per_step"],
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": "synthetic",
+        "config": {"workload": "cfg2: 15k-node/1k-rack post-delete snapshot, full-JobSet recovery; one step = "
+                               "one host-API jsp_place (run list in, assign[] back in host memory)",
+                   "nodes": c2["nodes"], "domains": c2["domains"], "jobs": c2["jobs"],
+                   "pods_per_job": c2["pods_per_job"], "classes": c2["classes"],
+                   "shape": c2["shape"], "parallelism": f"replicas{d['world']}"},
+        "host_api_us": {"p50": c2.get("loop_p50_us"), "p99": c2.get("loop_p99_us")},
+        "kernel_only": {"placements_per_s": c2.get("kernel_only_placements_per_s"),
+                        "us_per_step": c2.get("kernel_only_us_per_step")},
+    }
+    rf = c2.get("roofline")
+    if rf:
+        line["roofline"] = {"bound": "hbm", "achieved": rf["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": rf["frac"], "traffic": rf.get("traffic"), "kernel": rf["kernel"],
+                            "bytes": rf["bytes"], "avg_us": rf["avg_us"], "trace_median_us": rf.get("trace_median_us")}
+    cpu = c2.get("cpu")
+    if cpu:
+        line["cpu_baseline"] = {"value": cpu["value"], "unit": "placements/s", "cores": cpu["cores"], "kind": "port",
+                                "sample": cpu["sample"],
+                                "legs_us": {str(x["threads"]): x["us_per_placement"] for x in cpu["legs"]}}
+        line["gpu_over_best_cpu"] = cpu.get("gpu_over_best_cpu")
+    cold = d.get("cold2") or {}
+    vs = cold.get("vs_cpu")
+    head = (vs or {}).get("gap_1ms") or {}
+    g1 = (cold.get("gpu") or {}).get("gap_1ms")
+    if g1:
+        line["p50_recovery_us"] = g1["p50_us"]
+        line["p99_recovery_us"] = g1["p99_us"]
+        line["recovery_trials"] = g1["n"]
+        line["recovery_leg"] = "cold: idle-exited service, 1-row patch, 1 ms gap, jsp_place; patch+place, timed in C"
+        if head:
+            line["p99_recovery_cpu_us"] = head["cpu_p99_us"]
+            line["p50_recovery_cpu_us"] = head["cpu_p50_us"]
+    warm = c2.get("warm_trials")
+    if warm:
+        line["p99_recovery_warm_us"] = warm["p99_us"]
+    if vs:
+        line["cold_cols"] = "gpu p50,p95,p99,n | best cpu p50,p95,p99,n (us)"
+        line["cold_recovery"] = _cold_rows(vs)
+    parked = d.get("cold2_parked")
+    if parked:
+        line["cold_recovery_parked"] = _cold_rows(parked.get("vs_cpu"))
+    ps = c2.get("patched")
+    if ps:
+        line["patched_step_us"] = {"gpu": ps["mean_us"], "gpu_p99": ps["p99_us"], "cpu_best": c2.get("cpu_patched_best_us")}
+    line["link_floor_us"] = c2.get("link_floor_p50_us")
+    line["service_request_us_device"] = c2.get("service_request_us_device")
+    for name in ("cfg1", "cfg3", "cfg5"):
+        c = (d.get("configs") or {}).get(name)
+        if not c:
+            continue
+        e = {"host_p50_us": c["host_api_resident"]["p50_us"], "host_p99_us": c["host_api_resident"]["p99_us"],
+             "kernel_only_us": c["kernel_us"], "kernel_frac": c["kernel_frac"], "placed": c["placed"],
+             "jobs": c["jobs"]}
+        if "cpu_us" in c:
+            e["cpu_us"] = c["cpu_us"]
+        if c.get("cold_vs_cpu"):
+            e["cold"] = _cold_rows(c["cold_vs_cpu"])
+        if c.get("service_frac") is not None:
+            e["service_frac"] = c["service_frac"]
+        line[name] = e
+    c4 = d.get("cfg4")
+    if c4:
+        e = {k: c4.get(k) for k in ("placements_per_s", "host_api_us", "kernel_only_us", "kernel_only_placements_per_s",
+                                    "tally_us", "tally_frac", "tally_cold_us", "tally_cold_frac", "copy_cold_us",
+                                    "tally_traffic", "allreduce_us", "shards", "placed")}
+        cpu4 = c4.get("cpu_baseline")
+        if cpu4:
+            e["cpu_best_us"] = cpu4["best_us"]
+            e["cpu_cores"] = cpu4["cores"]
+            e["gpu_over_best_cpu"] = cpu4["gpu_over_best_cpu"]
+        ds = c4.get("device_set")
+        if ds:
+            e["device_set"] = {"us": ds.get("us_per_step"), "shards": ds.get("shards"), "devices": ds.get("devices"),
+                               "exact": ds.get("bit_exact_vs_single_device"), "error": ds.get("error")}
+        line["cfg4"] = e
+    line["host_binding"] = {k: d.get("binding", {}).get(k) for k in ("bound", "gpu_numa_node", "cpus")}
+    line["detail"] = d.get("detail_path")
+    return line
+
+
+def emit(line: dict) -> str:
+    s = json.dumps(line, separators=(",", ":"))
+    if len(s) > LINE_MAX_BYTES:  # never print a line the driver cannot parse: drop the per-config blocks first
+        for k in ("cfg1", "cfg5", "cfg3", "cold_recovery_parked", "cfg4"):
+            line.pop(k, None)
+            s = json.dumps(line, separators=(",", ":"))
+            if len(s) <= LINE_MAX_BYTES:
+                break
+    return s
+
+
+# ----------------------------------------------------------------------------- measurement
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--trials", type=int, default=1000, help="recovery-latency trials (p99) on config 2")
+    ap.add_argument("--trials", type=int, default=200, help="warm recovery trials (trial snapshots, upload untimed)")
     ap.add_argument("--cpu-seconds", type=float, default=9.0, help="bounded CPU-baseline sample (all legs)")
-    ap.add_argument("--cold-trials", type=int, default=100,
-                    help="realistic recovery trials on config 2 (half on 3 and 5): the resident service has "
-                         "idle-exited, a row patch arrives, then jsp_place")
+    ap.add_argument("--cold-trials", type=int, default=1000,
+                    help="cold recovery trials on config 2 at the 1 ms gap (a tenth at 0 and 10 ms, and on 3 and 5)")
     ap.add_argument("--no-cfg4", action="store_true", help="skip the 1M-node sharded leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the per-config (1, 3, 5) lines")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="where the full measurement record goes ('' = nowhere)")
     args = ap.parse_args()
 
     # --gpus N is the job's rank count. Without a launcher (no WORLD_SIZE) and
@@ -523,6 +654,10 @@ def main() -> None:
         sys.exit(relaunch_with_torchrun(args.gpus))
     if env_world is not None and int(env_world) != args.gpus:
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+    # the resident service's idle exit: short enough that a cold trial (sleep
+    # past it) costs 35 ms, long enough that a 10 ms gap stays within its half
+    os.environ.setdefault("JSP_SERVICE_IDLE_MS", "30")
+    idle_ms = float(os.environ["JSP_SERVICE_IDLE_MS"])
 
     import torch
     import torch.distributed as dist
@@ -544,9 +679,12 @@ def main() -> None:
     from jobset_amd.engine import Engine
     from jobset_amd.snapshot import job_runs
 
-    binding = bind_to_gpu_node(local)  # before the engine allocates its pinned buffers and threads
+    d = {"world": world, "steps": args.steps, "warmup": args.warmup, "idle_ms": idle_ms}
+    d["binding"] = bind_to_gpu_node(local)  # before the engine allocates its pinned buffers and threads
     stream = torch.cuda.current_stream().cuda_stream
     eng = Engine(local)
+    T = cpu_threads()
+    do_cpu = rank == 0 and world == 1 and args.cpu_seconds > 0
 
     def device_step(p):
         rc_np, rl_np = job_runs(p.job_class)
@@ -556,6 +694,8 @@ def main() -> None:
 
         def step():
             eng.place_device(rc.data_ptr(), rl.data_ptr(), rc_np.shape[0], p.n_jobs, out.data_ptr(), stream)
+        step.keep = (rc, rl)
+        step.rc, step.rl, step.n_runs = rc, rl, rc_np.shape[0]
         return step, out
 
     # ------------------------------------------------ config 2: host-API placements/s (value)
@@ -566,20 +706,20 @@ def main() -> None:
     call = eng.host_placer(*job_runs(p.job_class))
     for _ in range(args.warmup):
         call()
-    # The resident service (shapes 3-5) stays on the GPU between calls, and a
-    # device-wide synchronize waits for it to leave: it is stopped right
-    # before each synchronize. One untimed call after the opening synchronize
-    # restarts it (the steady state of back-to-back placements; its cold start
-    # is measured apart, "cold_recovery"); its stop after the last timed call
-    # is inside the timed region.
+    # The resident service stays on the GPU between calls, and a device-wide
+    # synchronize waits for it to leave: it is stopped right before each
+    # synchronize. One untimed call after the opening synchronize restarts it
+    # (the steady state of back-to-back placements; its cold start is measured
+    # apart, "cold_recovery"); its stop after the last timed call is inside
+    # the timed region.
     eng.service_stop()
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
     call()
-    eng.timing(reset=True)  # the library's own phase clocks of the timed calls (host side, always on)
+    eng.timing(reset=True)
     t0 = time.perf_counter()
-    # the K timed jsp_place calls, issued from C (jsp_place_loop) as a cgo
+    # the K timed jsp_place calls, issued from C (jspb_place_loop) as a cgo
     # caller's loop would: no interpreter between them
     _, loop_p50, loop_p99 = call.loop(args.steps)
     eng.service_stop()
@@ -590,58 +730,35 @@ def main() -> None:
     tphase = eng.timing(reset=True)
     placed = int((call.assign >= 0).sum())
     value = placed * args.steps * world / elapsed
+    c2 = {"value": round(value, 1), "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
+          "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J, "placed": placed,
+          "pods_per_job": p.classes[0].pods, "classes": len(p.classes), "shape": SHAPES.get(shape, str(shape)),
+          "loop_p50_us": round(loop_p50, 3), "loop_p99_us": round(loop_p99, 3),
+          "library_us_per_call": round((tphase.host_prep_us + tphase.host_wait_us) / max(int(tphase.host_calls), 1), 3),
+          "svc_calls": int(tphase.svc_calls)}
+    d["cfg2"] = c2
 
     # the service's own clock: per request, first tile saw it -> last tile's
-    # assign[] drained (100 MHz device stamps, timing on; not the timed loop)
-    svc = None
+    # answer drained (100 MHz device stamps, timing on; not the timed loop)
     if shape == 3:
         eng.set_timing(True)
         for _ in range(args.warmup):
             call()
         eng.timing(reset=True)
-        for _ in range(args.steps):
+        for _ in range(max(args.steps, 200)):
             call()
         ts = eng.timing(reset=True)
         eng.set_timing(False)
         eng.service_stop()
         req_us = ts.svc_us / max(ts.svc_calls, 1)
-        svc = {"request_us_device": round(req_us, 3),
-               "achieved_gbs": round(compact_bytes(p) / (req_us * 1e-6) / 1e9, 2),
-               "calls": int(ts.svc_calls),
-               "note": "device time of one request inside the resident kernel (stamps on, which add "
-                       "~0.5-1 us); the host-API wall adds the host-link hand-offs"}
-
-    # one row patched before each call (the resident tiles reload their rows
-    # from memory instead of their LDS copies); not the timed loop
-    patched = patched_step_us(eng, p, max(200, args.steps * 5)) if shape == 3 else None
-    # the same K steps from a Python loop (one ctypes call each), beside the C-timed value
-    t0p = time.perf_counter()
-    for _ in range(args.steps):
-        call()
-    py_step_us = (time.perf_counter() - t0p) * 1e6 / args.steps
+        c2["service_request_us_device"] = round(req_us, 3)
+        c2["service_achieved_gbs"] = round(compact_bytes(p) / (req_us * 1e-6) / 1e9, 2)
+        # one row patched before each call: the patch rides in the request
+        c2["patched"] = patched_step_us(eng, p, max(200, args.steps * 5))
     eng.service_stop()
-    # the host-link floor: host -> device -> host through pinned memory with
-    # the service's polling, and where the timed host-API step's time went
-    floor = eng.link_floor(2000) if rank == 0 else None
-    step_us = elapsed * 1e6 / args.steps
-    n_calls = max(int(tphase.host_calls), 1)
-    breakdown = None
-    if floor is not None and shape == 3:
-        pre = tphase.svc_pre_us / n_calls
-        ans = tphase.svc_answer_us / n_calls
-        first = tphase.svc_first_us / n_calls
-        lib_us = (tphase.host_prep_us + tphase.host_wait_us) / n_calls
-        dev = svc["request_us_device"] if svc else None
-        breakdown = {"host_api_step_us": round(step_us, 2), "library_us": round(lib_us, 2),
-                     "outside_library_us": round(step_us - lib_us, 2),
-                     "svc_pre_us": round(pre, 2), "svc_answer_us": round(ans, 2),
-                     "svc_first_entry_us": round(first, 2), "first_to_last_entry_us": round(ans - first, 2),
-                     "link_floor_p50_us": round(floor[0], 2), "device_request_us": dev,
-                     "answer_beyond_floor_and_device_us": round(ans - floor[0] - dev, 2) if dev else None,
-                     "note": "means over the timed calls (jsp_timing, host clock): svc_pre = library entry of the "
-                             "service path to the request post, svc_answer = post to the answer's last entry (svc_first_entry: to its first); the "
-                             "floor is jsp_engine_link_floor's median round trip; device_request = the service's "
-                             "in-kernel request time (stamps on, a separate leg)"}
+    if rank == 0:
+        floor = eng.link_floor(2000)
+        c2["link_floor_p50_us"], c2["link_floor_p99_us"] = round(floor[0], 2), round(floor[1], 2)
 
     # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
     step, out = device_step(p)
@@ -656,96 +773,72 @@ def main() -> None:
     barrier(world)
     el_dev = max_over_ranks(time.perf_counter() - t0, world)
     assert int((out[:J].cpu().numpy() >= 0).sum()) == placed
+    c2["kernel_only_placements_per_s"] = round(placed * args.steps * world / el_dev, 1)
+    c2["kernel_only_us_per_step"] = round(el_dev * 1e6 / args.steps, 3)
 
     # dominant kernel: the step's single launch (compaction / fused), else the
-    # tally. With the resident service (shape 3) the same tile code runs inside
-    # the persistent kernel, which HIP events cannot bracket per request: the
-    # roofline is the launch-path compaction kernel's, the service's own
-    # per-request device time is under "service".
-    # The launch's own duration: events on its dispatch packets
-    # (jsp_place_device_timed, the engine stream), back to back, none of the
-    # host's submit time between them -- what a kernel trace reports; the
-    # event loop around ctypes-issued launches is kept beside it.
+    # tally. The resident service runs the same tile code inside the
+    # persistent kernel, which HIP events cannot bracket per request: the
+    # roofline is the launch-path compaction kernel's, timed by events on the
+    # dispatch packets of back-to-back launches (jspb_place_device_timed).
     n_dev_iters = max(200, args.steps)
     if shape in (1, 2, 3, 4):
-        rc_np, rl_np = job_runs(p.job_class)
-        rct = torch.from_numpy(rc_np.astype(np.int32)).cuda()
-        rlt = torch.from_numpy(rl_np.astype(np.int32)).cuda()
-        dom_med, dom_us = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc_np.shape[0], J, out.data_ptr(),
-                                                 n_dev_iters)
-        loop_us = event_loop_us(step, args.steps, stream)
+        dom_med, dom_us = eng.place_device_timed(step.rc.data_ptr(), step.rl.data_ptr(), step.n_runs, J,
+                                                 out.data_ptr(), n_dev_iters)
         tb = compact_bytes(p) if shape in (2, 3) else tally_bytes(p) + placement_tail_bytes(p)
     else:
         cap = torch.empty((len(p.classes) + 1, p.topology.n_leaves), dtype=torch.int32, device="cuda")
         dom_med, dom_us = eng.tally_device_timed(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves, n_dev_iters)
-        loop_us = event_loop_us(lambda: eng.tally_device(cap.data_ptr(), cap[-1].data_ptr(), p.topology.n_leaves,
-                                                         stream), args.steps, stream)
         tb = tally_bytes(p)
     eng.check()
     achieved = tb / (dom_us * 1e-6) / 1e9
-    # the same kernel's dispatch-only duration from the committed rocprofv3 trace of this bench (cfg2 grid)
     tr_us, tr_src = trace_avg_us(KERNEL[shape])
     traffic = pmc_traffic(KERNEL[shape], 2)
+    c2["roofline"] = {"kernel": KERNEL[shape], "bytes": tb, "avg_us": round(dom_us, 3), "median_us": round(dom_med, 3),
+                      "achieved": round(achieved, 2), "frac": round(achieved / HBM_PEAK_GBS, 5),
+                      "traffic": traffic["bytes"] if traffic else None,
+                      "traffic_source": traffic["source"] if traffic else None,
+                      "trace_median_us": tr_us, "trace_source": tr_src}
 
-    # ------------------------------------------------ p50/p99 recovery latency (host API, trial snapshots)
-    lat2 = host_api_latency(eng, p, args.trials, synth.config2) if rank == 0 and args.trials > 0 else None
-    cold2 = cold_recovery_latency(eng, p, args.cold_trials) if rank == 0 and args.cold_trials > 0 else None
-    eng.service_stop()
-    idle_ms = float(os.environ.get("JSP_SERVICE_IDLE_MS", "50"))
-    if cold2 is not None and world == 1 and args.cpu_seconds > 0:
-        cold2["cpu"] = cpu_cold_recovery(p, args.cold_trials, sorted({1, 2, cpu_threads()}), idle_ms)
-        cold2["cpu_note"] = ("oracle/cpu_fast.c like for like: the same idle sleep, the same one-row patch written into "
-                             "its columns, the same slept gap, then one placement; timed = patch + placement, the gap "
-                             "excluded; timed in C (jspf_recovery_loop)")
-        cold2["vs_cpu"] = cold_vs_cpu(cold2, cold2["cpu"])
-    # the same recovery with the service parked (JSP_SERVICE_PARKED: no idle
-    # exit, a dedicated GPU -- the GPU side of the CPU pool's spinning threads)
-    cold2p = None
-    if rank == 0 and args.cold_trials > 0:
+    # ------------------------------------------------ recovery latency (rank 0)
+    if rank == 0 and args.trials > 0:
+        c2["warm_trials"] = host_api_latency(eng, p, args.trials, synth.config2)
+    plan2 = cold_plan(args.cold_trials) if rank == 0 else {}
+    if plan2:
+        cold = {"gpu": cold_recovery_latency(eng, p, plan2, idle_ms)}
+        eng.service_stop()
+        if do_cpu:
+            cold["cpu"] = cpu_cold_recovery(p, plan2, sorted({2, T}), idle_ms)
+            cold["vs_cpu"] = cold_vs_cpu(cold["gpu"], cold["cpu"])
+        d["cold2"] = cold
+        # the same recovery with the service parked (JSP_SERVICE_PARKED: no
+        # idle exit, a dedicated GPU -- the GPU side of the CPU pool's
+        # spinning threads), at the short gaps' sample size
+        plan_p = {g: n for g, n in cold_plan(max(20, args.cold_trials // 10), {1.0: 1.0, 0.0: 1.0}).items()}
         eng.set_service(True, parked=True)
         settled_place(eng, p.job_class)
-        cold2p = cold_recovery_latency(eng, p, args.cold_trials)
+        gp = cold_recovery_latency(eng, p, plan_p, idle_ms)
         eng.service_stop()
         eng.set_service(True)
-        cold2p["note"] = ("JSP_SERVICE_PARKED (the service never idles out): the same 60 ms sleep, one-row patch, gap "
-                          "and jsp_place; the patch rides in the request")
-        if cold2 is not None and "cpu" in cold2:
-            cold2p["vs_cpu"] = cold_vs_cpu(cold2p, cold2["cpu"])
+        parked = {"gpu": gp}
+        if "cpu" in cold:
+            parked["vs_cpu"] = cold_vs_cpu(gp, {g: v for g, v in cold["cpu"].items() if g in gp})
+        d["cold2_parked"] = parked
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
-    cpu = None
-    T = cpu_threads()
-    cpu_patched = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0 and patched is not None:
-        legs_p = cpu_patched_step(p, sorted({1, 2, T}), min(2.0, args.cpu_seconds / 6))
-        best_p = min(legs_p.values())
-        cpu_patched = {"legs_us": legs_p, "best_us": best_p, "gpu_patched_step_us": patched["mean_us"],
-                       "gpu_over_best_cpu": round(best_p / patched["mean_us"], 3),
-                       "note": "oracle/cpu_fast.c: the same one-row write into its columns, then one placement, "
-                               "back to back, timed in C (jspf_run_loop; the CPU side of patched_step_us)"}
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        from oracle import oracle as O
-        legs = []
-        for th in sorted({1, 2, T}):
-            fc = O.FastCPU(th)
-            fc.prepare(p)
-            a, _, _, pl = fc.run()
-            assert np.array_equal(a, call.assign), "CPU evaluator differs from the engine"
-            us, n, dt = time_cpu(fc, args.cpu_seconds / 3)
-            fc.close()
-            legs.append({"threads": th, "us_per_placement": round(us, 2),
-                         "placements_per_s": round(pl / (us * 1e-6), 1), "runs": n, "seconds": round(dt, 2)})
+    if do_cpu:
+        legs = cpu_legs(p, call.assign, sorted({1, 2, T}), args.cpu_seconds, placed)
         best = max(legs, key=lambda x: x["placements_per_s"])  # the fastest leg is the baseline
-        cpu = {"value": best["placements_per_s"], "unit": "placements/s", "cores": best["threads"], "kind": "port",
-               "nproc": os.cpu_count(), "threads_share": T,
-               "sample": f"config 2 placed {best['runs']} times in {best['seconds']} s by oracle/cpu_fast.c "
-                         f"({best['threads']} threads -- the fastest of the legs at 1/2/{T} threads, all below; "
-                         f"-O3 AVX2, same snapshot and rules, bit-exact with the engine)",
-               "gpu_over_best_cpu": round(value / best["placements_per_s"], 3),
-               "legs": legs}
+        c2["cpu"] = {"value": best["placements_per_s"], "cores": best["threads"], "legs": legs,
+                     "sample": f"cfg2 placed {best['runs']}x in {best['seconds']} s by oracle/cpu_fast.c "
+                               f"({best['threads']} threads, fastest of 1/2/{T}; bit-exact with the engine)",
+                     "gpu_over_best_cpu": round(value / best["placements_per_s"], 3)}
+        if "patched" in c2:
+            legs_p = cpu_patched_step(p, sorted({2, T}), min(2.0, args.cpu_seconds / 6))
+            c2["cpu_patched_legs_us"] = legs_p
+            c2["cpu_patched_best_us"] = min(legs_p.values())
 
     # ------------------------------------------------ configs 1, 3, 5 (one GPU)
-    configs = None
     if rank == 0 and not args.no_configs:
         configs = {}
         for cfg in (1, 3, 5):
@@ -761,21 +854,11 @@ def main() -> None:
             kb = compact_bytes(pc) if dev_shape == 2 else (tally_bytes(pc) + placement_tail_bytes(pc) if dev_shape == 1
                                                            else tally_bytes(pc))
             line = {"nodes": pc.nodes.n_nodes, "jobs": pc.n_jobs, "classes": len(pc.classes),
-                    "levels": pc.topology.n_levels, "placed": r.placed, "shape": SHAPES[r.fused],
-                    "kernel_us_per_placement": round(us, 2),
-                    "kernel_placements_per_s": round(r.placed / (us * 1e-6), 1),
-                    "roofline": {"bound": "hbm", "kernel": KERNEL[dev_shape], "bytes_per_launch": kb,
-                                 "avg_us": round(us, 3),
-                                 "achieved": round(kb / (us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                 "frac": round(kb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
-                                 "note": "device path (launch, device-resident runs and assign[]), HIP events "
-                                         "around 200 back-to-back placements"},
+                    "levels": pc.topology.n_levels, "placed": r.placed, "shape": SHAPES.get(r.fused, str(r.fused)),
+                    "kernel_us": round(us, 2), "kernel_kernel": KERNEL[dev_shape], "kernel_bytes": kb,
+                    "kernel_frac": round(kb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
                     "host_api_resident": host_api_latency(eng, pc, 200)}
             if r.fused in (3, 5):
-                # the shipped shape's device time: the resident service's own
-                # per-request stamps (first tile saw the request -> last tile
-                # drained), its algorithmic bytes (the rows evaluated, the
-                # leaf offsets, what it hands back)
                 eng.set_timing(True)
                 cl = eng.host_placer(*job_runs(pc.job_class))
                 for _ in range(20):
@@ -787,33 +870,31 @@ def main() -> None:
                 eng.set_timing(False)
                 dev_us = tsv.svc_us / max(tsv.svc_calls, 1)
                 sb = compact_bytes(pc) if r.fused == 3 else tally_bytes(pc)
-                line["service_roofline"] = {
-                    "bound": "hbm", "shape": SHAPES[r.fused], "request_us_device": round(dev_us, 3),
-                    "bytes_per_request": sb, "achieved": round(sb / (dev_us * 1e-6) / 1e9, 2), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(sb / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5), "requests": int(tsv.svc_calls),
-                    "note": "the host API's shape: in-kernel stamps per request (timing on), rows held on chip between "
-                            "requests; algorithmic bytes = the rows evaluated + leaf offsets + the outputs"}
+                line["service_request_us_device"] = round(dev_us, 3)
+                line["service_bytes"] = sb
+                line["service_frac"] = round(sb / (dev_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5)
             if cfg in (3, 5):
-                line["host_api_recovery_trials"] = host_api_latency(eng, pc, 200, synth.CONFIGS[cfg])
-                line["host_api_cold_recovery"] = cold_recovery_latency(eng, pc, args.cold_trials // 2)
-                if line["host_api_cold_recovery"] is not None and world == 1 and args.cpu_seconds > 0:
-                    cc = line["host_api_cold_recovery"]
-                    cc["cpu"] = cpu_cold_recovery(pc, max(10, args.cold_trials // 2), sorted({1, 2, T}), idle_ms)
-                    cc["vs_cpu"] = cold_vs_cpu(cc, cc["cpu"])
+                line["host_api_recovery_trials"] = host_api_latency(eng, pc, 100, synth.CONFIGS[cfg])
+                plan = cold_plan(max(20, args.cold_trials // 10), {1.0: 1.0, 10.0: 1.0, 0.0: 0.5})
+                line["cold"] = cold_recovery_latency(eng, pc, plan, idle_ms)
+                if line["cold"] is not None and do_cpu:
+                    line["cold_cpu"] = cpu_cold_recovery(pc, plan, [T], idle_ms)
+                    line["cold_vs_cpu"] = cold_vs_cpu(line["cold"], line["cold_cpu"])
             eng.service_stop()
-            if world == 1 and args.cpu_seconds > 0:
+            if do_cpu:
                 from oracle import oracle as O
                 for th in sorted({1, T}):
                     fc = O.FastCPU(th)
                     fc.prepare(pc)
                     us_c, _, _ = time_cpu(fc, min(0.5, args.cpu_seconds / 10))
                     fc.close()
-                    line[f"cpu_fast_{th}t_us_per_placement"] = round(us_c, 1)
+                    line[f"cpu_{th}t_us"] = round(us_c, 2)
+                line["cpu_us"] = {"1t": line["cpu_1t_us"], f"{T}t": line[f"cpu_{T}t_us"]}
             configs[f"cfg{cfg}"] = line
+        d["configs"] = configs
         eng.load(p)
 
     # ------------------------------------------------ config 4: 1M nodes, sharded over the ranks
-    cfg4 = None
     if not args.no_cfg4:
         p4 = synth.config4()
         sp = ShardedPlacement(Engine(local) if world > 1 else eng, p4, rank, world, stream)
@@ -822,7 +903,6 @@ def main() -> None:
         torch.cuda.synchronize()
         barrier(world)
         steps4 = max(50, args.steps // 4)
-        tally_loop = 200  # back-to-back tally launches for the warm average: fixed, not tied to --steps
         t0 = time.perf_counter()
         for _ in range(steps4):
             sp.step()
@@ -830,204 +910,85 @@ def main() -> None:
         barrier(world)
         el4 = max_over_ranks(time.perf_counter() - t0, world)
         placed4 = sp.placed()
-        sp.engine.set_timing(True)
-        for _ in range(steps4):
-            sp.step()
-        torch.cuda.synchronize()
-        t4 = sp.engine.timing(reset=True)
-        sp.engine.set_timing(False)
-        n4 = max(t4.calls - t4.fused_calls, 1)
-        # tally alone, back to back, events around the loop
+        a4 = sp.assign()
         C4, L4 = len(p4.classes), p4.topology.n_leaves
         cap4 = torch.zeros((C4 + 1, L4), dtype=torch.int32, device="cuda")
         tally_fn = lambda: sp.engine.tally_device(cap4.data_ptr(), cap4[-1].data_ptr(), L4, stream)  # noqa: E731
         for _ in range(10):  # untimed: the first launches into a new output buffer pay its first touch
             tally_fn()
         # the kernel's own time: events on the dispatch packets of back-to-back
-        # launches on the engine stream (jsp_tally_device_timed) -- what the
-        # kernel trace reports; the event loop around 200 ctypes-issued
-        # launches (host submit in the gaps) is kept beside it
-        tally_med, tally_mean = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, tally_loop)
-        tally_loop_us = event_loop_us(tally_fn, tally_loop, stream)
-        tally_us = tally_mean
-        # a third, tracer-free measure: the kernel's own span (first wave start
-        # -> last wave end, device clock stamps per wave; jsp_tally_device_spans)
+        # launches on the engine stream (jspb_tally_device_timed)
+        tally_med, tally_us = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, 200)
         try:
             span_med, span_mean, empty_us, period_us = sp.engine.tally_device_spans(cap4.data_ptr(), cap4[-1].data_ptr(),
-                                                                                    L4, tally_loop)
+                                                                                    L4, 200)
         except Exception:  # noqa: BLE001 -- another tally shape (sharded ranks): no span
             span_med = span_mean = empty_us = period_us = None
         tb4 = tally_bytes(p4) if world == 1 else sp.shard_tally_bytes()
         scrub = torch.zeros(128 << 20, dtype=torch.int32, device="cuda")  # 512 MiB
-        # cold: the library's read-only sweep of the 512 MiB buffer before each launch, dispatch events
-        tally_cold, tally_cold_mean = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, 20,
-                                                                   scrub.data_ptr(), scrub.numel() * 4)
-        tally_cold_dirty = cold_us(tally_fn, 20, stream, scrub, dirty=True)
-        step_dev = None
-        if world == 1:  # the whole single-GPU step on the device (first dispatch -> last), warm and cold
-            rc4, rl4 = job_runs(p4.job_class)
-            rc4t = torch.from_numpy(rc4.astype(np.int32)).cuda()
-            rl4t = torch.from_numpy(rl4.astype(np.int32)).cuda()
-            a4t = torch.empty(p4.n_jobs, dtype=torch.int32, device="cuda")
-            sw = eng.place_device_timed(rc4t.data_ptr(), rl4t.data_ptr(), rc4.shape[0], p4.n_jobs, a4t.data_ptr(), 100)
-            sc = eng.place_device_timed(rc4t.data_ptr(), rl4t.data_ptr(), rc4.shape[0], p4.n_jobs, a4t.data_ptr(), 20,
+        tally_cold, _ = sp.engine.tally_device_timed(cap4.data_ptr(), cap4[-1].data_ptr(), L4, 20,
+                                                     scrub.data_ptr(), scrub.numel() * 4)
+        c4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4", "placed": placed4,
+              "shards": world, "kernel_only_us": round(el4 * 1e6 / steps4, 2),
+              "kernel_only_placements_per_s": round(placed4 * steps4 / el4, 1),
+              "tally_us": round(tally_us, 2), "tally_median_us": round(tally_med, 2),
+              "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+              "tally_span_us": _r(span_mean), "tally_period_us": _r(period_us), "tally_empty_launch_us": _r(empty_us),
+              "tally_cold_us": round(tally_cold, 2),
+              "tally_cold_frac": round(tb4 / (tally_cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+              "tally_bytes": tb4, "allreduce_us": sp.allreduce_us()}
+        if world == 1:
+            # the whole single-GPU step on the device (first dispatch -> last), warm and cold
+            sw = eng.place_device_timed(sp.rc.data_ptr(), sp.rl.data_ptr(), sp.n_runs, p4.n_jobs, sp.out.data_ptr(), 100)
+            sc = eng.place_device_timed(sp.rc.data_ptr(), sp.rl.data_ptr(), sp.n_runs, p4.n_jobs, sp.out.data_ptr(), 20,
                                         scrub.data_ptr(), scrub.numel() * 4)
-            step_dev = {"warm_median_us": round(sw[0], 2), "warm_mean_us": round(sw[1], 2),
-                        "cold_median_us": round(sc[0], 2),
-                        "note": "device span of one three-launch step (first dispatch start -> last dispatch end, "
-                                "dispatch-packet events, engine stream)"}
-            del rc4t, rl4t, a4t
-        host_step = None
-        if world == 1:  # the same step through the host API (jsp_place: run list in, assign[] back in host memory)
+            c4["step_device_us"] = round(sw[0], 2)
+            c4["step_device_cold_us"] = round(sc[0], 2)
+            # placements/s through the host API (run list in, assign[] back in host memory)
             call4 = eng.host_placer(*job_runs(p4.job_class))
             for _ in range(5):
                 call4()
-            host_step = round(call4.loop(steps4)[0] / steps4, 2)  # timed in C (jsp_place_loop)
-            assert np.array_equal(call4.assign, sp.assign()), "host API differs from the device path on cfg4"
-        copy_ceiling = None
-        if world == 1:  # achievable streaming rate: a cold copy of the same byte count
+            tot4, med4, _ = call4.loop(steps4)  # timed in C (jspb_place_loop)
+            host4 = tot4 / steps4
+            assert np.array_equal(call4.assign, a4), "host API differs from the device path on cfg4"
+            c4["host_api_us"] = round(host4, 2)
+            c4["host_api_p50_us"] = round(med4, 2)
+            c4["placements_per_s"] = round(placed4 / (host4 * 1e-6), 1)
             src = torch.empty(tb4 // 2 // 16 * 4, dtype=torch.int32, device="cuda").fill_(1)
             dst = torch.empty_like(src)
-            cu = cold_us(lambda: dst.copy_(src), 20, stream, scrub)
-            cud = cold_us(lambda: dst.copy_(src), 20, stream, scrub, dirty=True)
-            copy_ceiling = {"bytes": 2 * src.numel() * 4, "cold_us": round(cu, 2),
-                            "cold_gbs": round(2 * src.numel() * 4 / (cu * 1e-6) / 1e9, 1),
-                            "cold_dirty_us": round(cud, 2)}
+            c4["copy_cold_us"] = round(cold_us(lambda: dst.copy_(src), 20, stream, scrub), 2)
             del src, dst
+            c4["tally_traffic"] = (pmc_traffic(("tally_wave",), 4) or {}).get("bytes")
+        else:  # the sharded step through torch.distributed (device-resident runs and assign[])
+            c4["placements_per_s"] = c4["kernel_only_placements_per_s"]
         del scrub
         sp.engine.check()
-        cpu4 = None
-        if rank == 0 and world == 1 and args.cpu_seconds > 0:  # the CPU evaluator beside it
-            from oracle import oracle as O
-            legs4 = []
-            for th in sorted({1, 2, cpu_threads()}):
-                fc = O.FastCPU(th)
-                fc.prepare(p4)
-                a4c = fc.run()[0]
-                assert np.array_equal(a4c, sp.assign()), "CPU evaluator differs from the engine on cfg4"
-                us_c, n_c, dt_c = time_cpu(fc, max(0.5, args.cpu_seconds / 6))
-                fc.close()
-                legs4.append({"threads": th, "us_per_placement": round(us_c, 1),
-                              "placements_per_s": round(placed4 / (us_c * 1e-6), 1), "runs": n_c,
-                              "seconds": round(dt_c, 2)})
+        if do_cpu:
+            legs4 = cpu_legs(p4, a4, sorted({1, 2, T}), max(1.5, args.cpu_seconds / 2), placed4)
             best4 = max(legs4, key=lambda x: x["placements_per_s"])
-            cpu4 = {"value": best4["placements_per_s"], "unit": "placements/s", "cores": best4["threads"],
-                    "kind": "port", "gpu_over_best_cpu": round(placed4 * steps4 / el4 / best4["placements_per_s"], 2),
-                    "sample": "cfg4 placed by oracle/cpu_fast.c at 1/2/box-share threads (fastest leg = value), "
-                              "bit-exact with the engine", "legs": legs4}
-        cfg4 = {"workload": "cfg4: 1,048,576 nodes / 50,000 racks, 40,000 jobs x 16 pods, C=4",
-                "placements_per_s": round(placed4 * steps4 / el4, 1), "ms_per_step": round(el4 * 1e3 / steps4, 4),
-                "placed": placed4, "tally_us": round(tally_us, 2), "tally_median_us": round(tally_med, 2),
-                "tally_event_loop_us": round(tally_loop_us, 2),
-                "tally_span_us": round(span_mean, 2) if span_mean else None,
-                "tally_span_median_us": round(span_med, 2) if span_med else None,
-                "tally_span_vs_events": round(span_mean / tally_mean, 3) if span_mean else None,
-                "tally_empty_launch_event_us": round(empty_us, 2) if empty_us else None,
-                "tally_period_us": round(period_us, 2) if period_us else None,
-                "tally_period_vs_events": round(period_us / tally_mean, 3) if period_us else None,
-                "tally_measure": "tally_us (events on the dispatch packets) is the figure used; tally_period_us is the "
-                                 "same back-to-back launches' period by the kernels' own clock (first wave to first "
-                                 "wave, per-wave stamps, no tracer): the cross-check; tally_span_us is the execution "
-                                 "part of it (first wave start -> last wave end), the rest the gap dispatch leaves "
-                                 "between launches; tally_empty_launch_event_us = an empty one-workgroup launch's events",
-                "tally_note": "tally_us = mean, tally_median_us = median of 200 back-to-back launches timed by events "
-                              "on their dispatch packets (jsp_tally_device_timed); tally_event_loop_us = HIP events "
-                              "around 200 ctypes-issued launches (includes host submit gaps)",
-                "tally_gbs": round(tb4 / (tally_us * 1e-6) / 1e9, 1),
-                "tally_frac": round(tb4 / (tally_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "tally_cold_us": round(tally_cold, 2),
-                "tally_cold_gbs": round(tb4 / (tally_cold * 1e-6) / 1e9, 1),
-                "tally_cold_frac": round(tb4 / (tally_cold * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                "tally_cold_dirty_us": round(tally_cold_dirty, 2),
-                "cold_note": "cold: the library's read-only sweep of a 512 MiB buffer before each of 20 launches, "
-                             "median of the dispatch-packet events; cold_dirty: torch writes the buffer before each "
-                             "launch (events around it), so the launch's misses pay its write-backs",
-                "step_device": step_dev,
-                "host_api_step_us": host_step,
-                "host_api_note": "jsp_place calls back to back, timed in C (jsp_place_loop)",
-                "copy_ceiling_same_bytes": copy_ceiling,
-                "tally_traffic": pmc_traffic(("tally_wave",), 4) if world == 1 else None,
-                "feas_us": round(t4.feas_ms * 1e3 / n4, 2),
-                "assign_expand_us": round(t4.assign_ms * 1e3 / n4, 2),
-                "allreduce_us": sp.allreduce_us(), "shards": world, "cpu_baseline": cpu4}
+            c4["cpu_baseline"] = {"value": best4["placements_per_s"], "cores": best4["threads"],
+                                  "best_us": best4["us_per_placement"], "legs": legs4,
+                                  "gpu_over_best_cpu": round(c4["placements_per_s"] / best4["placements_per_s"], 2)}
         # the device-set engine inside the C ABI (what the Go manager's one
         # process would drive, main.go:161-190): rank 0 opens every visible GPU
-        # (ids {0, 0} on a one-GPU box: two shards, on-device add), the others
-        # wait at a barrier
+        # (ids {0, 0} on a one-GPU box: two shards, on-device add)
         barrier(world)
         if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
-            cfg4["device_set"] = device_set_leg(p4, sp.assign(), max(20, args.steps))
-            if host_step and "us_per_step" in cfg4["device_set"]:
-                cfg4["device_set"]["over_single_device_host_api"] = round(cfg4["device_set"]["us_per_step"] / host_step, 3)
+            c4["device_set"] = device_set_leg(p4, a4, max(20, args.steps))
             torch.cuda.set_device(local)  # the rank's own device for the barrier (the library restores it too)
         barrier(world)
+        d["cfg4"] = c4
 
     if rank == 0:
-        line = {
-            "metric": "exclusive-topology placements/sec at 15k nodes; p99 recovery placement latency",
-            "value": round(value, 1),
-            "unit": "placements/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 5),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic",
-            "config": {"workload": "cfg2: 15k-node / 1k-rack post-delete snapshot, full-JobSet recovery; one step "
-                                   "= one host-API jsp_place (run list in, assign[] back in the caller's host buffer)",
-                       "nodes": p.nodes.n_nodes, "domains": p.topology.n_leaves, "jobs": J,
-                       "pods_per_job": p.classes[0].pods, "classes": len(p.classes),
-                       "shape": SHAPES[shape], "parallelism": f"replicas{world}"},
-            "kernel_only_placements_per_s": round(placed * args.steps * world / el_dev, 1),
-            "kernel_only_us_per_step": round(el_dev * 1e6 / args.steps, 3),
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5),
-                         "traffic": traffic["bytes"] if traffic else None,
-                         "traffic_source": traffic["source"] if traffic else None,
-                         "traffic_is_latest": traffic["latest"] if traffic else None,
-                         "kernel": KERNEL[shape], "bytes_per_launch": tb, "avg_us": round(dom_us, 3),
-                         "median_us": round(dom_med, 3), "event_loop_us": round(loop_us, 3),
-                         "trace_median_us": tr_us, "trace_source": tr_src,
-                         "note": "avg_us / median_us: events on the dispatch packets of back-to-back launches "
-                                 "(jsp_place_device_timed, the engine stream); event_loop_us: HIP events around "
-                                 "ctypes-issued launches. Latency-bound: one launch moving 0.43 MB; DESIGN.md §8"},
-            "host_binding": binding,
-            "timed_loop": "the K timed steps are jsp_place calls issued and timed from C (jsp_place_loop), as a cgo "
-                          "caller's loop would issue them; the same K steps from a Python loop (one ctypes call "
-                          "each) are python_loop_us_per_step",
-            "python_loop_us_per_step": round(py_step_us, 3),
-            "host_api_step_p50_us": round(loop_p50, 3),
-            "host_api_step_p99_us": round(loop_p99, 3),
-            "service": svc,
-            "rows_note": "the timed loop places the same snapshot repeatedly: the resident tiles keep their rows in "
-                         "LDS between requests (no row traffic); patched_step_us times one row patched before "
-                         "each call (rows reloaded from memory)",
-            "patched_step_us": patched,
-            "cpu_patched_step": cpu_patched,
-            "host_link_floor_us": {"p50": round(floor[0], 2), "p99": round(floor[1], 2), "mean": round(floor[2], 2)}
-            if floor else None,
-            "host_api_breakdown": breakdown,
-            "p50_recovery_us": lat2["p50_us"] if lat2 else None,
-            "p99_recovery_us": lat2["p99_us"] if lat2 else None,
-            "p99_recovery_leg": "warm: 1000 seeded trial snapshots, each uploaded untimed (the upload restarts the "
-                                "service and returns once it polls), then jsp_place on host wall; the realistic "
-                                "cold recovery is cold_recovery",
-            "p99_cold_recovery_us": {g: v["p99_us"] for g, v in cold2.items() if g.startswith("gap_")} if cold2 else None,
-            "p99_cold_recovery_best_cpu_us": {g: v["best_cpu_p99_us"] for g, v in cold2.get("vs_cpu", {}).items()}
-            if cold2 else None,
-            "p99_cold_recovery_parked_us": {g: v["p99_us"] for g, v in cold2p.items() if g.startswith("gap_")}
-            if cold2p else None,
-            "cold_recovery_parked": cold2p,
-            "recovery_trials": lat2["n"] if lat2 else 0,
-            "cold_recovery": cold2,
-            "cpu_baseline": cpu,
-            "configs": configs,
-            "cfg4_1M": cfg4,
-        }
-        print(json.dumps(line), flush=True)
+        if args.detail_out:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(args.detail_out)), exist_ok=True)
+                with open(args.detail_out, "w") as f:
+                    json.dump(d, f, indent=1)
+                d["detail_path"] = args.detail_out
+            except OSError:
+                d["detail_path"] = None
+        print(emit(build_line(d)), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

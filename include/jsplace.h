@@ -60,6 +60,12 @@
  * Environment: JSP_SERVICE=0 (no resident service) / =parked, JSP_SERVICE_IDLE_MS
  * (its idle exit, default 50), JSP_RCCL_LIB (device sets) are the operational
  * switches; JSP_TEST_HOOKS is for tests only (jsp_engine.cc TestHooks).
+ *
+ * This header is the product boundary: every entry point in it is one the Go
+ * binding calls (tests/test_abi.py checks the two agree).
+ * The bench's and probes' entry points -- C-timed loops, dispatch-timed
+ * kernels, the host-link floor, phase clocks, shape selection -- are a
+ * separate symbol set, jspb_*, declared in jsplace_bench.h (ABI v7).
  */
 #ifndef JSPLACE_H
 #define JSPLACE_H
@@ -71,7 +77,7 @@
 extern "C" {
 #endif
 
-#define JSP_ABI_VERSION 6
+#define JSP_ABI_VERSION 7
 
 #define JSP_MAX_LEVELS 4      /* topology levels, 0 = coarsest (zone) .. K-1 = finest (rack) */
 #define JSP_MAX_LABEL_WORDS 4 /* 256 interned (key,value) label bits */
@@ -136,43 +142,42 @@ typedef struct jsp_stats {
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 
-typedef struct jsp_timing {
-    uint64_t calls;            /* timed placements (or tallies) since last reset */
-    double tally_ms;           /* summed HIP-event time of the tally kernel */
-    double feas_ms;            /* summed HIP-event time of the feasibility-bitmap kernel */
-    double assign_ms;          /* summed HIP-event time of the assignment kernel */
-    double fused_ms;           /* summed HIP-event time of single-launch placements (fused / compaction) */
-    uint64_t fused_calls;      /* placements that ran as a single launch */
-    /* host-API placements (jsp_place), host wall clock, always accumulated */
-    uint64_t host_calls;
-    double host_prep_us;       /* entry to launch: checks, run list into the pinned staging buffer */
-    double host_launch_us;     /* the kernel launch call(s) */
-    double host_wait_us;       /* launch return to completion seen (completion words or stream sync) */
-    double host_post_us;       /* assign[] (and tallies) out, stats; the split service: its host walk (inside wait) */
-    /* resident service (jsp_engine_set_service) */
-    uint64_t svc_calls;        /* jsp_place calls it answered */
-    uint64_t svc_starts;       /* service launches (first use, after uploads, idle exits, restarts) */
-    double svc_us;             /* summed in-kernel request time (first tile saw the request -> last tile
-                                  done, 100 MHz device clock); accumulated while timing is on */
-    uint64_t svc_fallbacks;    /* jsp_place calls the service could not answer (its grid does not fit the
-                                  CUs, it left twice, or a request failed on the device): answered by the
-                                  launch path instead. When its grid cannot be co-resident the service stays
-                                  off until the next upload; otherwise the next call starts it again */
-    double svc_ready_us;       /* host time spent waiting for a (re)started service's dispatcher to poll */
-    double svc_pre_us;         /* service-answered jsp_place: entry of the service path to the request post
-                                  (a queued wake, settling the previous request, patch bookkeeping) (ABI v6) */
-    double svc_answer_us;      /* ... the request post to the answer's last entry seen (ABI v6) */
-    double svc_first_us;       /* ... the request post to its first answer entry seen (compaction service) */
-    /* jsp_snapshot_patch (ABI v5), host wall clock, always accumulated */
-    uint64_t patches;          /* patch calls with at least one row */
-    double patch_us;           /* their host time (a waker-thread restart is not in it) */
-    double wake_us;            /* host time (re)starting the service for a coming recovery, wherever it ran */
-} jsp_timing;
+/* Engine metrics (ABI v7; SURVEY.md §5 "engine histograms"): what a
+ * Prometheus exporter in the Go manager publishes beside the reference's
+ * jobset_failed_total / jobset_completed_total counters
+ * (pkg/metrics/metrics.go:24-38). Always on, per engine, cheap (a few adds
+ * per call under a lock of their own).
+ *
+ * A log2 histogram: bucket 0 counts values below lo, bucket i (1..30) values
+ * in [lo * 2^(i-1), lo * 2^i), bucket 31 the rest. Counts are per bucket (not
+ * cumulative: an exporter sums them up for its `le` boundaries lo * 2^i). */
+#define JSP_HIST_BUCKETS 32
+typedef struct jsp_hist {
+    uint64_t count;
+    double sum;
+    double max;
+    uint64_t bucket[JSP_HIST_BUCKETS];
+} jsp_hist;
 
-/* jsp_engine_set_fused modes */
-#define JSP_FUSED_OFF 0       /* always tally -> feas -> assign (three launches) */
-#define JSP_FUSED_AUTO 1      /* one launch when possible (default): the single-class compaction
-                                 for one leaf-level class, the fused tail for small snapshots */
+#define JSP_HIST_LO_US 0.5     /* lo of the latency histograms (us): bucket 30 ends at ~537 s */
+#define JSP_HIST_LO_JOBS 1.0   /* lo of the batch-size histogram */
+
+typedef struct jsp_metrics {
+    jsp_hist place_us;         /* jsp_place / jsp_place_jobs: host wall per call, us (failed calls too) */
+    jsp_hist patch_us;         /* jsp_snapshot_patch: host wall per call, us */
+    jsp_hist batch_jobs;       /* jobs per successful jsp_place call */
+    jsp_hist device_us;        /* device time per placement, us: the resident service's in-kernel request
+                                  time, or a single-launch placement's kernel events. Recorded only while
+                                  device timing is on (jsplace_bench.h jspb_set_timing): the stamps and
+                                  events cost ~1 us per call */
+    uint64_t placed;           /* jobs given a domain */
+    uint64_t unplaceable;      /* jobs answered -1 */
+    uint64_t place_errors;     /* jsp_place calls that returned an error */
+    uint64_t patch_errors;     /* jsp_snapshot_patch calls that returned an error */
+    uint64_t svc_calls;        /* placements the resident service answered (stats.fused 3 or 5) */
+    uint64_t svc_starts;       /* resident service launches (first use, after uploads, idle exits, wakes) */
+    uint64_t svc_fallbacks;    /* placements the service could not answer (answered on the launch path) */
+} jsp_metrics;
 
 /* jsp_engine_set_service modes. With AUTO, a host-API jsp_place of the
  * one-class compaction shape or of a multi-class / multi-level shape whose
@@ -263,25 +268,6 @@ int jsp_classes_upload(jsp_engine* e, const jsp_job_class* classes, uint32_t n_c
  * occ_out (nullable) [n_leaves_total]: rows covered by other exclusive jobs. */
 int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
               int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);
-/* `iters` jsp_place calls back to back, timed in C (ABI v6): what a cgo
- * caller's loop sees, with no interpreter between the calls (the bench's
- * host-API steps). With n_patch > 0, each call is preceded by a one-row
- * jsp_snapshot_patch of the taint column (row patch_rows[i % n_patch] set to
- * patch_taints[i % n_patch]: a watch event between recoveries). out_us[0]
- * total wall, [1] median and [2] p99 per step, microseconds; assign_out holds
- * the last call's answer. */
-int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
-                   int32_t* assign_out, uint32_t iters, const uint32_t* patch_rows, const uint32_t* patch_taints,
-                   uint32_t n_patch, double* out_us);
-/* The realistic recovery timed in C (ABI v6), `trials` times: the idle period
- * (idle_us, slept -- or spun when spin != 0), a one-row taint patch
- * (patch_rows[t % n_patch] := patch_taints[t % n_patch]; the failed job's
- * node back to schedulable), the gap (gap_us: the reconciler's round trips
- * between the deletions and the recreate), then jsp_place. out_us[3t] = the
- * patch call, [3t+1] = the place call, [3t+2] = the gap as it passed (us). */
-int jsp_recovery_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
-                      int32_t* assign_out, uint32_t trials, double idle_us, double gap_us, int spin,
-                      const uint32_t* patch_rows, const uint32_t* patch_taints, uint32_t n_patch, double* out_us);
 /* Same with one class id per job (run-length encoded on the host). */
 int jsp_place_jobs(jsp_engine* e, const uint32_t* job_class, uint32_t n_jobs,
                    int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats);
@@ -316,56 +302,17 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
                          const uint32_t* follower_off, const int32_t* follower_domains,
                          uint32_t n_jobs, uint32_t* bad_out);
 
-/* ---- instrumentation / tuning ---- */
-int jsp_engine_set_fused(jsp_engine* e, int mode);
+/* ---- resident service, metrics, synchronisation ---- */
 int jsp_engine_set_service(jsp_engine* e, int mode);
-/* Stops the resident service (if running) and waits for its workgroups to leave. */
+/* Stops the resident service (if running) and waits (bounded: 2 s, then
+ * JSP_EHIP and the service stays off until the next upload) for its
+ * workgroups to leave. */
 int jsp_engine_service_stop(jsp_engine* e);
-/* With timing on: the last service request's 100 MHz device-clock stamps, 8
- * per tile (0 request seen, 1 after the acquire, 2 tallied, 3 feasible count
- * scanned, 4 look-back done, 5 assign[] drained; 6-7 unused). Copies up to
- * cap/8 tiles; *n_tiles = how many (0 when no timed request is held). When
- * cap leaves room for one more row after all the tiles, it receives the
- * dispatcher's {0 request seen in the mailbox, 1 bell rung} (ABI v6). */
-int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles);
-/* Device time of `iters` back-to-back steps on the engine stream (the bench's
- * kernel-time legs): each step carries a start event on its first dispatch and
- * a stop event on its last (hipExtLaunchKernel: the dispatch packets' own
- * timestamps, as a kernel trace reports them, with no host submit time between
- * them). d_scrub (nullable): a device buffer larger than the caches, read
- * (never written) before every step, so each step starts cold.
- * out_us[0] = median, out_us[1] = mean per step, in microseconds.
- * jsp_tally_device_timed: the tally of jsp_tally_device.
- * jsp_place_device_timed: the whole placement of jsp_place_device. */
-int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
-                           const void* d_scrub, size_t scrub_bytes, double* out_us);
-int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
-                           uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub,
-                           size_t scrub_bytes, double* out_us);
-/* The host-link floor (ABI v6): `iters` host -> device -> host round trips
- * through pinned memory with the resident service's polling (four device
- * waves a quarter of a round trip apart poll a request word; the first to
- * see request i writes an ack the host spins on). out_us[0] median, [1]
- * p99, [2] mean, microseconds. Every host-API request pays this at least
- * once; the bench reports it beside the host-API latency. */
-int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us);
-/* The tally's in-kernel span (ABI v6): `iters` back-to-back launches of the
- * one-tile wave tally with per-wave stamps of the device's 100 MHz clock
- * (every wave's start, and its end once its stores drained); per launch the
- * span from the first wave's start to the last wave's end -- a third measure
- * beside the dispatch-packet events and a kernel trace, with no tracer and no
- * dispatch overhead in it. out_us[0] median, [1] mean; out_us[2] the median
- * dispatch-event time of an empty one-workgroup launch (the fixed cost events
- * on the dispatch packets add to a kernel's own span); out_us[3] the launches'
- * period by the same clock (first wave of the first launch to first wave of
- * the last, per launch: execution plus the gap dispatch leaves between
- * back-to-back launches). JSP_ESTATE when the snapshot's tally runs another
- * shape. */
-int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
-                           double* out_us);
-int jsp_engine_set_timing(jsp_engine* e, int enable);
-int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset);
+/* The engine's metrics since creation or the last reset (jsp_metrics). */
+int jsp_engine_get_metrics(jsp_engine* e, jsp_metrics* out, int reset);
+/* The engine's own stream (a caller may pass it to the *_device calls). */
 void* jsp_engine_stream(jsp_engine* e);
+/* Waits for every patch and launch the engine has issued. */
 int jsp_engine_sync(jsp_engine* e);
 /* Waits for every launch the engine has enqueued (on any stream) and returns
  * JSP_EHIP if one of them failed on the device (see "Kernel-side failures"). */

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -17,7 +18,7 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/jsplace.h"
+#include "../../include/jsplace_bench.h"
 #include "jsp_internal.h"
 #include "jsp_multi.h"
 #include "jsp_walk.h"
@@ -34,6 +35,21 @@ int set_err(int code, const char* fmt, ...) {
     va_end(ap);
     g_err = buf;
     return code;
+}
+
+// One value into a log2 histogram (jsplace.h jsp_hist): bucket 0 below lo,
+// bucket i in [lo 2^(i-1), lo 2^i), the last one the rest.
+void hist_add(jsp_hist& h, double v, double lo) {
+    h.count += 1;
+    h.sum += v;
+    if (v > h.max) h.max = v;
+    int i = 0;
+    if (v >= lo) {
+        int ex = 0;
+        (void)std::frexp(v / lo, &ex);
+        i = std::min(ex, JSP_HIST_BUCKETS - 1);
+    }
+    h.bucket[i] += 1;
 }
 
 #define HIP_TRY(expr)                                                                        \
@@ -154,9 +170,10 @@ struct TestHooks {
     bool have_seq0 = false;
     bool svc_entries = false;       // svc_entries=1: the compaction service answers with per-job entries
                                     //   after a look-back instead of tile bitmaps (A/B)
-    uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jsp_place_loop spins N ns between calls (diagnostic)
+    uint32_t loop_gap_ns = 0;       // loop_gap_ns=N: jspb_place_loop spins N ns between calls (diagnostic)
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
     bool warm = true;               // warm=0: no call-entry prefetch of the engine's lines (A/B)
+    uint32_t micro_spins = 1u << 22;  // micro_spins=N: a resident tile's passes over the microbox (kErrMicro)
 };
 
 TestHooks read_hooks() {
@@ -187,6 +204,7 @@ TestHooks read_hooks() {
         else if (k == "loop_gap_ns") h.loop_gap_ns = (uint32_t)v;
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
         else if (k == "warm") h.warm = v != 0;
+        else if (k == "micro_spins") h.micro_spins = (uint32_t)v;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -355,6 +373,11 @@ struct jsp_engine {
     } svc;
     int svc_mode = JSP_SERVICE_AUTO;
     Grave grave;  // buffers replaced while the service ran: freed when it stops
+
+    // metrics (jsp_engine_get_metrics): their own lock, so that reading them
+    // never waits for a placement; taken after mu where both are held
+    std::mutex met_mu;
+    jsp_metrics met{};
 
     // timing
     bool timing = false;
@@ -534,7 +557,11 @@ int resolve_timing(jsp_engine* e) {
         if (e->ev[i].tag == 0) e->acc.tally_ms += ms;
         else if (e->ev[i].tag == 1) e->acc.feas_ms += ms;
         else if (e->ev[i].tag == 2) e->acc.assign_ms += ms;
-        else e->acc.fused_ms += ms;
+        else {
+            e->acc.fused_ms += ms;
+            std::lock_guard<std::mutex> l(e->met_mu);
+            hist_add(e->met.device_us, ms * 1e3, JSP_HIST_LO_US);
+        }
     }
     e->ev_used = 0;
     return JSP_OK;
@@ -843,6 +870,10 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
 // service is seen by a stream query and the request re-posted once).
 constexpr uint32_t kSvcMaxBlocks = 255;  // one tile per workgroup + the dispatcher, all co-resident (<= one per CU)
 constexpr int kSvcGone = 1;
+constexpr int kSvcFailed = 3;  // a tile reported a failed wait through the service's error word
+// svc_stop's bound on the kernel's exit after the stop word (it leaves within
+// ~2 us; the runtime reports it ~8 us later)
+constexpr std::chrono::milliseconds kStopLimit{2000};
 
 double svc_idle_ms() {
     static const double ms = [] {
@@ -956,7 +987,24 @@ int svc_stop(jsp_engine* e) {
     if (!v.ev_exit) HIP_TRY(hipEventCreateWithFlags(&v.ev_exit, hipEventDisableTiming));
     const hipError_t rec = hipEventRecord(v.ev_exit, v.stream);
     svc_post_stop(e);
-    const hipError_t q = rec == hipSuccess ? hipEventSynchronize(v.ev_exit) : hipStreamSynchronize(v.stream);
+    // Bounded: a kernel that never reads the stop word -- a wedged
+    // dispatcher -- would hold a blocking synchronize forever. The event is
+    // polled instead, up to kStopLimit; past it the service is marked broken
+    // (the launch path answers until the next upload) and the call fails.
+    hipError_t q = hipSuccess;
+    if (rec == hipSuccess) {
+        const auto t0 = std::chrono::steady_clock::now();
+        while ((q = hipEventQuery(v.ev_exit)) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > kStopLimit) {
+                v.broken = true;
+                return set_err(JSP_EHIP, "placement service did not leave within %lld ms of its stop word",
+                               (long long)std::chrono::duration_cast<std::chrono::milliseconds>(kStopLimit).count());
+            }
+            _mm_pause();
+        }
+    } else {
+        q = hipStreamSynchronize(v.stream);
+    }
     if (q != hipSuccess) return set_err(JSP_EHIP, "placement service failed: %s", hipGetErrorString(q));
     e->grave.flush();  // nothing resident any more: a free no longer waits
     return JSP_OK;
@@ -1086,6 +1134,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     a.bits = v.bitmap ? v.bits.as<unsigned long long>() : nullptr;
     // the microbox: a micro-patch's rows for the co-located resident tiles
     a.mbox = shape == 2 ? reinterpret_cast<unsigned long long*>(static_cast<char*>(v.granules.p) + gpad + 128 + xbytes) : nullptr;
+    a.micro_spins = e->hooks.micro_spins;
     a.done = w;
     a.stats = w + n_tiles;
     a.err = w + n_tiles + 2;
@@ -1153,6 +1202,10 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     v.t_launch = std::chrono::steady_clock::now();
     v.last = v.t_launch;
     e->acc.svc_starts += 1;
+    {
+        std::lock_guard<std::mutex> l(e->met_mu);
+        e->met.svc_starts += 1;
+    }
     return wait_ready ? svc_wait_ready(e) : JSP_OK;
 }
 
@@ -1230,6 +1283,9 @@ int svc_wait(jsp_engine* e, uint32_t seq, uint32_t J) {
             }
         }
         if (i == n) return JSP_OK;
+        // a tile whose microbox wait gave up writes no line, but the error word
+        if ((spins & 255) == 0 && lines && __atomic_load_n(words + n + 2, __ATOMIC_ACQUIRE) != v.err_ack)
+            return kSvcFailed;
         if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {
@@ -1258,6 +1314,14 @@ int svc_settle(jsp_engine* e) {
         v.running = false;
         return JSP_OK;
     }
+    if (rc == kSvcFailed) {
+        // a tile past the early answer's last job gave up its microbox wait
+        // (the answer itself was complete: that tile's line was not needed).
+        // Its registers may be stale: the service is stopped, and the next
+        // request starts it afresh from the rows in memory.
+        v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
+        return svc_stop(e);
+    }
     // The early answer had all J entries, so a tile past them that timed out
     // in its look-back (it scattered nothing) did not touch it: acknowledge
     // its error word here rather than blame the next request for it.
@@ -1266,7 +1330,6 @@ int svc_settle(jsp_engine* e) {
     return rc;
 }
 
-constexpr int kSvcFailed = 3;  // svc_wait_entries: a tile reported a look-back time-out (err word)
 
 // The compaction service's answer read from the entries themselves: entry j
 // is (seq << 32 | domain) in one 8-byte store, so the host copies each out as
@@ -1380,6 +1443,9 @@ int svc_wait_bits(jsp_engine* e, uint32_t seq, uint32_t J, int32_t* out, uint32_
             for (uint32_t i = j; i < J; ++i) out[i] = -1;
             return JSP_OK;
         }
+        // a tile whose microbox wait gave up writes no line, but the error word
+        if ((spins & 255) == 0 && __atomic_load_n(e->svc.words.as<uint32_t>() + n + 2, __ATOMIC_ACQUIRE) != v.err_ack)
+            return kSvcFailed;
         if ((spins & 255) == 0 && qp.due()) {
             const hipError_t q = hipStreamQuery(v.stream);
             if (q == hipSuccess) {  // it left: only a line already complete counts
@@ -1680,6 +1746,13 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
     if (!restart) {
         if (int rc = svc_wait_ready(e)) return rc;
         if (int rc = svc_settle(e)) return rc;
+        if (!v.running) {  // the settle stopped it (kSvcFailed): a fresh start, the patch applied first
+            restart = true;
+            if (carry) {
+                carry = false;
+                if (int rc = patch_wait(e)) return rc;
+            }
+        }
     }
     if (carry) {  // held back, or posted and its completion word not back yet
         // (a posted patch the dispatcher has taken is applied before it takes
@@ -1728,10 +1801,13 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
                        : v.bitmap ? svc_wait_bits(e, seq, J, assign_out, &n_early, &all_tiles)
                                   : svc_wait_entries(e, seq, J, assign_out, &n_early);
         if (rc == kSvcFailed) {
-            v.err_ack = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
+            const uint32_t ew = __atomic_load_n(v.words.as<uint32_t>() + v.nb + 2, __ATOMIC_ACQUIRE);
+            v.err_ack = ew;
             (void)svc_stop(e);
-            return set_err(JSP_EHIP, "placement service request %u failed: the compaction look-back timed out; "
-                                     "its assign[] is invalid", seq);
+            return set_err(JSP_EHIP, "placement service request %u failed: %s; its assign[] is invalid", seq,
+                           (ew & jsp::kErrKindMask) == jsp::kErrMicro
+                               ? "a resident tile's wait for the request's micro-patch rows gave up"
+                               : "the compaction look-back timed out");
         }
         if (rc == kSvcGone && attempt == 0) {
             v.running = false;
@@ -1758,6 +1834,8 @@ int svc_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             hi = std::max(hi, (int32_t)(clk[jsp::kSvcClkSlots * t + 5] - ref));
         }
         e->acc.svc_us += (double)(hi - lo) / 100.0;
+        std::lock_guard<std::mutex> l(e->met_mu);
+        hist_add(e->met.device_us, (double)(hi - lo) / 100.0, JSP_HIST_LO_US);
     }
     if (v.shape == 3) {  // the tiles answered: the walk, into the caller's buffer
         const auto tw = std::chrono::steady_clock::now();
@@ -2317,18 +2395,29 @@ static void warm_engine(const jsp_engine* e, bool place) {
     }
 }
 
-int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
-                       const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
-    if (int rc = check_engine(e)) return rc;
+static int snapshot_patch_call(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
+                               const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
     if (e->multi) { DeviceGuard dg; return jspm::snapshot_patch(e->multi, rows, n, labels, taints, free_res, excl_owner); }
-    warm_engine(e, false);
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     {
         std::lock_guard<std::mutex> g(e->mu);
+        warm_engine(e, false);  // under the lock: the waker may be replacing the buffers it touches
         rc = snapshot_patch_locked(e, rows, n, labels, taints, free_res, excl_owner, t0);
     }
     notify_waker(e);
+    return rc;
+}
+
+int jsp_snapshot_patch(jsp_engine* e, const uint32_t* rows, uint32_t n, const uint64_t* labels,
+                       const uint32_t* taints, const uint32_t* free_res, const int32_t* excl_owner) {
+    if (int rc = check_engine(e)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = snapshot_patch_call(e, rows, n, labels, taints, free_res, excl_owner);
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> l(e->met_mu);
+    hist_add(e->met.patch_us, us, JSP_HIST_LO_US);
+    if (rc != JSP_OK) e->met.patch_errors += 1;
     return rc;
 }
 
@@ -2591,7 +2680,7 @@ int jsp_place_device(jsp_engine* e, const uint32_t* d_run_class, const uint32_t*
 }
 
 
-int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+int jspb_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
                            const void* d_scrub, size_t scrub_bytes, double* out_us) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) return set_err(JSP_ESTATE, "device-set engine: time its shard engines");
@@ -2603,7 +2692,7 @@ int jsp_tally_device_timed(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
                       [&](hipStream_t s) { return tally_impl(e, d_cap, d_occ, ld, s); });
 }
 
-int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
+int jspb_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint32_t ld, uint32_t iters,
                            double* out_us) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) return set_err(JSP_ESTATE, "device-set engine: time its shard engines");
@@ -2683,7 +2772,7 @@ int jsp_tally_device_spans(jsp_engine* e, uint32_t* d_cap, uint32_t* d_occ, uint
     return check_launch_error(e);
 }
 
-int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
+int jspb_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs,
                            uint32_t n_jobs, int32_t* d_assign, uint32_t iters, const void* d_scrub, size_t scrub_bytes,
                            double* out_us) {
     if (int rc = check_engine(e)) return rc;
@@ -2699,13 +2788,12 @@ int jsp_place_device_timed(jsp_engine* e, const uint32_t* d_run_class, const uin
     });
 }
 
-int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
-              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
-    if (int rc = check_engine(e)) return rc;
+static int place_call(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                      int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
     if (e->multi) { DeviceGuard dg; return jspm::place(e->multi, run_class, run_len, n_runs, assign_out, tally_out, occ_out, stats); }
-    warm_engine(e, true);
     auto t0 = std::chrono::steady_clock::now();
     std::lock_guard<std::mutex> g(e->mu);
+    warm_engine(e, true);  // under the lock: the waker may be replacing the buffers it touches
     if (int rc = ready(e, true)) return rc;
     if (e->leaf_begin != 0 || e->n_leaves != e->L_total)
         return set_err(JSP_ESTATE, "sharded engine: use jsp_tally_device + all-reduce + jsp_assign_device");
@@ -2732,6 +2820,10 @@ int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len,
             if (src == JSP_ERANGE || e->svc.start_failed) e->svc.broken = true;
             e->svc.start_failed = false;
             e->acc.svc_fallbacks += 1;
+            {
+                std::lock_guard<std::mutex> l(e->met_mu);
+                e->met.svc_fallbacks += 1;
+            }
             g_err.clear();  // answered: the call succeeds (jsp_timing.svc_fallbacks counts it)
             goto launch_path;
         }
@@ -2810,9 +2902,40 @@ launch_path:
     return JSP_OK;
 }
 
-int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+int jsp_place(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+              int32_t* assign_out, uint32_t* tally_out, uint32_t* occ_out, jsp_stats* stats) {
+    if (int rc = check_engine(e)) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
+    jsp_stats local{};
+    jsp_stats* st = stats ? stats : &local;
+    const int rc = place_call(e, run_class, run_len, n_runs, assign_out, tally_out, occ_out, st);
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> l(e->met_mu);
+    hist_add(e->met.place_us, us, JSP_HIST_LO_US);
+    if (rc != JSP_OK) {
+        e->met.place_errors += 1;
+        return rc;
+    }
+    hist_add(e->met.batch_jobs, (double)st->jobs, JSP_HIST_LO_JOBS);
+    e->met.placed += st->placed;
+    e->met.unplaceable += st->jobs - st->placed;
+    if (st->fused == 3 || st->fused == 5) e->met.svc_calls += 1;
+    return rc;
+}
+
+int jsp_engine_get_metrics(jsp_engine* e, jsp_metrics* out, int reset) {
+    if (!e) return set_err(JSP_EINVAL, "engine is NULL");
+    if (!out && !reset) return set_err(JSP_EINVAL, "out is NULL");
+    std::lock_guard<std::mutex> l(e->met_mu);
+    if (out) *out = e->met;
+    if (reset) e->met = jsp_metrics{};
+    return JSP_OK;
+}
+
+int jspb_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                    int32_t* assign_out, uint32_t iters, const uint32_t* patch_rows, const uint32_t* patch_taints,
                    uint32_t n_patch, double* out_us) {
+    if (int rc = check_engine(e)) return rc;
     if (iters == 0 || iters > 1000000) return set_err(JSP_EINVAL, "iters %u out of range [1,1000000]", iters);
     if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
     if (n_patch > 0 && (!patch_rows || !patch_taints)) return set_err(JSP_EINVAL, "patch rows / taints are NULL");
@@ -2842,7 +2965,7 @@ int jsp_place_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run
     return JSP_OK;
 }
 
-// The idle period or gap of jsp_recovery_loop: slept, or spun (a busy caller).
+// The idle period or gap of jspb_recovery_loop: slept, or spun (a busy caller).
 static void recovery_wait(double us, bool spin) {
     if (us <= 0.0) return;
     const auto end = std::chrono::steady_clock::now() + std::chrono::duration<double, std::micro>(us);
@@ -2853,9 +2976,10 @@ static void recovery_wait(double us, bool spin) {
     while (std::chrono::steady_clock::now() < end) __builtin_ia32_pause();
 }
 
-int jsp_recovery_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+int jspb_recovery_loop(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                       int32_t* assign_out, uint32_t trials, double idle_us, double gap_us, int spin,
                       const uint32_t* patch_rows, const uint32_t* patch_taints, uint32_t n_patch, double* out_us) {
+    if (int rc = check_engine(e)) return rc;
     if (trials == 0 || trials > 100000) return set_err(JSP_EINVAL, "trials %u out of range [1,100000]", trials);
     if (!out_us) return set_err(JSP_EINVAL, "out_us is NULL");
     if (!(idle_us >= 0.0 && idle_us <= 1e7 && gap_us >= 0.0 && gap_us <= 1e7))
@@ -2956,7 +3080,7 @@ int jsp_audit_placements(jsp_engine* e, const int32_t* leader_rows, const uint32
     return JSP_OK;
 }
 
-int jsp_engine_set_fused(jsp_engine* e, int mode) {
+int jspb_set_fused(jsp_engine* e, int mode) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 0, mode); }
     std::lock_guard<std::mutex> g(e->mu);
@@ -2985,7 +3109,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
     return JSP_OK;
 }
 
-int jsp_engine_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles) {
+int jspb_service_clock(jsp_engine* e, uint32_t* out, uint32_t cap, uint32_t* n_tiles) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { if (n_tiles) *n_tiles = 0; return JSP_OK; }
     std::lock_guard<std::mutex> g(e->mu);
@@ -3058,7 +3182,7 @@ int jspi_check(jsp_engine* e) {
 
 extern "C" {
 
-int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us) {
+int jspb_link_floor(jsp_engine* e, uint32_t iters, double* out_us) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) return set_err(JSP_ESTATE, "device-set engine: probe a shard engine");
     std::lock_guard<std::mutex> g(e->mu);
@@ -3105,7 +3229,7 @@ int jsp_engine_link_floor(jsp_engine* e, uint32_t iters, double* out_us) {
     return JSP_OK;
 }
 
-int jsp_engine_set_timing(jsp_engine* e, int enable) {
+int jspb_set_timing(jsp_engine* e, int enable) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::forward(e->multi, 2, enable); }
     std::lock_guard<std::mutex> g(e->mu);
@@ -3113,7 +3237,7 @@ int jsp_engine_set_timing(jsp_engine* e, int enable) {
     return JSP_OK;
 }
 
-int jsp_engine_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
+int jspb_get_timing(jsp_engine* e, jsp_timing* out, int reset) {
     if (int rc = check_engine(e)) return rc;
     if (e->multi) { DeviceGuard dg; return jspm::get_timing(e->multi, out, reset); }
     std::lock_guard<std::mutex> g(e->mu);

@@ -78,7 +78,7 @@ struct TallyArgs {
     // range, then an OR of its bits), so no feasibility launch follows. Null: off.
     uint64_t* feas_fold;
     uint32_t fold_nw;
-    // In-kernel span of the one-tile wave tally (jsp_tally_device_spans):
+    // In-kernel span of the one-tile wave tally (jspb_tally_device_spans):
     // lane 0 of every wave stores {its start, its end after its stores
     // drained} (100 MHz clock) at [2 t, 2 t + 1] for wave tile t. Null: off.
     unsigned long long* wstamps;
@@ -97,7 +97,10 @@ constexpr uint32_t kSpareBlocks = 64;
 // host reports as JSP_EHIP (jsp_engine.cc check_launch_error) -- never a stale
 // assign[] with success. The tag's top two bits say which wait (kErr*); the
 // compaction's look-back writes its launch number (kind 0).
-constexpr uint32_t kErrLookback = 0u, kErrExpand = 1u << 30, kErrPipe = 2u << 30, kErrKindMask = 3u << 30;
+// kErrMicro: a resident compaction tile whose microbox wait gave up (its
+// registers may lack the request's patched rows; it writes no answer line)
+constexpr uint32_t kErrLookback = 0u, kErrExpand = 1u << 30, kErrPipe = 2u << 30, kErrMicro = 3u << 30,
+                   kErrKindMask = 3u << 30;
 struct WaitErr {
     uint32_t* err;         // host-mapped error word (null: no report)
     uint32_t tag;          // written there by a wait that gave up
@@ -281,6 +284,7 @@ struct ServiceArgs {
     // with the request's seq (seq << 32 | word): [0] m | flags << 16, then
     // the m rows of micro_row_words; or null
     unsigned long long* mbox;
+    uint32_t micro_spins;               // passes over the microbox before a tile gives up (kErrMicro)
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay

@@ -3274,19 +3274,27 @@ __device__ __forceinline__ void service_dispatch(const ServiceArgs& v, const Tal
 // holds rows mine .. mine + 3 in registers, and a patched row among them
 // takes the columns the patch carries (micro_row_words layout: row id, W
 // label words as lo/hi halves, taint, R free, excl).
+// Returns false (wave-uniform) when the words still lack q after `spins`
+// passes: the registers are then left as they were, and the tile reports the
+// failure instead of answering (place_service_kernel: kErrMicro).
 template <int W, int R>
-__device__ __forceinline__ void apply_microbox(const unsigned long long* mb, uint32_t q, uint32_t mine,
-                                               RowRegs<W, R>& x) {
+__device__ __forceinline__ bool apply_microbox(const unsigned long long* mb, uint32_t q, uint32_t mine,
+                                               RowRegs<W, R>& x, uint32_t spins) {
     constexpr uint32_t rw = 3u + 2u * W + R;
     const uint32_t lane = threadIdx.x & 63u;
     unsigned long long t = 0;
-    for (uint32_t s = 0; s < (1u << 22); ++s) {
+    bool got = false;
+    for (uint32_t s = 0; s < spins; ++s) {
         if (lane <= kMailboxPayload) t = __hip_atomic_load(mb + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)t, 0) & 0xFFFFu;
         const bool ok = lane > kMailboxPayload || lane > m0 * rw || (uint32_t)(t >> 32) == q;
-        if (__ballot(!ok) == 0ull) break;
+        if (__ballot(!ok) == 0ull) {
+            got = true;
+            break;
+        }
         __builtin_amdgcn_s_sleep(1);
     }
+    if (!got) return false;
     const int word = (int)(uint32_t)t;
     const uint32_t mf = (uint32_t)__builtin_amdgcn_readlane(word, 0);
     const uint32_t m = mf & 0xFFFFu, fl = mf >> 16;
@@ -3312,6 +3320,7 @@ __device__ __forceinline__ void apply_microbox(const unsigned long long* mb, uin
             if (fl & kPatchExcl) x.ex[s] = (int32_t)v[2 + 2 * W + R];
         }
     }
+    return true;
 }
 
 // ---- resident compaction tile (ServiceArgs::resident): every tile is one
@@ -3533,6 +3542,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             if (next != 0) svc_stamp(clk, 0);
             s_x[16] = next;
             s_x[17] = J;
+            s_x[19] = 0u;  // a wave whose microbox wait gave up sets it
         }
         __syncthreads();
         const uint32_t next = s_x[16], Jw = s_x[17];
@@ -3553,14 +3563,34 @@ __global__ __launch_bounds__(kTallyThreads) void place_service_kernel(TallyArgs 
             }
             // this request's micro-patch rows, from the microbox (their stores
             // to memory may land after this tile's loads)
-            if (Jw & kBellMicro) apply_microbox<W, R>(v.mbox, next, (bt.z & ~3u) + 4u * threadIdx.x, rows);
+            if (Jw & kBellMicro)
+                if (!apply_microbox<W, R>(v.mbox, next, (bt.z & ~3u) + 4u * threadIdx.x, rows, v.micro_spins) &&
+                    (threadIdx.x & 63u) == 0u)
+                    s_x[19] = 1u;
             const bool ok = resident_eval<W, R>(kreg, rows, valid, lf, lds_ptr(lds + tally_pre_off(1, 2, (int)a.la)),
                                                 lds_ptr(lds + tally_wsum_off(1, 2, (int)a.la)), clk);
             svc_stamp(clk, 2);
-            if (v.bits) bitmap_finish(tile, ok, next, v.bits, s_x + 4);
-            else compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
-                                v.stats, v.err, true, s_x, clk, next, local);
-            cached = true;
+            // (resident_eval's barrier orders the flag's LDS stores before this read)
+            const bool mb_fail = s_x[19] != 0u;
+            if (mb_fail) {
+                // a microbox wait gave up: this tile's registers may lack the
+                // request's patched rows. No answer line (the host never takes
+                // the request as answered) and the error word instead, which
+                // the host's waits poll; the rows come from memory next time
+                // (the dispatcher wrote them through before its completion word)
+                if (threadIdx.x == 0)
+                    __hip_atomic_store(v.err, kErrMicro | (next & ~kErrKindMask), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_SYSTEM);
+                if (!v.bits)
+                    compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit,
+                                   v.assign, v.stats, v.err, true, s_x, clk, next, local);
+            } else if (v.bits) {
+                bitmap_finish(tile, ok, next, v.bits, s_x + 4);
+            } else {
+                compact_finish(a, tile, bt.x, ok, epoch == 0 ? 1u : epoch, J, 1u, v.granules, v.spin_limit, v.assign,
+                               v.stats, v.err, true, s_x, clk, next, local);
+            }
+            cached = !mb_fail;
         } else {
             compact_tile<W, R, true>(a, tile, bt, epoch == 0 ? 1u : epoch, v.pods, J, 1u, v.granules, v.spin_limit,
                                      v.assign, v.stats, v.err, true, lds, s_x, clk, row_cache, use_cache, next, local,
@@ -3851,7 +3881,7 @@ __global__ __launch_bounds__(256) void add_u32_kernel(uint32_t* __restrict__ dst
 }
 
 // ----------------------------------------------------------------- host-link floor (instrumentation)
-// jsp_engine_link_floor: the dispatcher's polling alone -- lane 0 of four
+// jspb_link_floor: the dispatcher's polling alone -- lane 0 of four
 // waves a quarter of a round trip apart, system-scope loads of one request
 // word in pinned host memory -- answering request number i with an ack word
 // of its own in pinned memory, which the host spins on: the host -> device ->
@@ -3903,7 +3933,7 @@ __global__ __launch_bounds__(256) void scrub_kernel(const uint4* __restrict__ p,
 // after each call cost 2-3 us of GPU time per call, profiles/r03).
 // set_launch_start names a start event the NEXT launch carries (then
 // cleared): with a stop event it brackets the dispatches themselves, as a
-// kernel trace does (jsp_tally_device_timed).
+// kernel trace does (jspb_tally_device_timed).
 namespace {
 thread_local hipEvent_t t_stop = nullptr;
 thread_local hipEvent_t t_start = nullptr;

@@ -578,9 +578,9 @@ int audit(Multi* m, const int32_t* leader_rows, const uint32_t* levels, const ui
 int forward(Multi* m, int what, int value) {
     std::lock_guard<std::mutex> g(m->mu);
     for (jsp_engine* e : m->sh) {
-        if (what == 0) MTRY(jsp_engine_set_fused(e, value));
+        if (what == 0) MTRY(jspb_set_fused(e, value));
         else if (what == 1) MTRY(jsp_engine_set_service(e, JSP_SERVICE_OFF));  // shards stay on the device path
-        else MTRY(jsp_engine_set_timing(e, value));
+        else MTRY(jspb_set_timing(e, value));
     }
     return JSP_OK;
 }
@@ -602,7 +602,7 @@ int get_timing(Multi* m, jsp_timing* out, int reset) {
     jsp_timing sum{};
     for (jsp_engine* e : m->sh) {
         jsp_timing t{};
-        MTRY(jsp_engine_get_timing(e, &t, reset));
+        MTRY(jspb_get_timing(e, &t, reset));
         sum.calls += t.calls;
         sum.tally_ms += t.tally_ms;
         sum.feas_ms += t.feas_ms;

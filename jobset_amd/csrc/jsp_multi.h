@@ -13,7 +13,7 @@
 #pragma once
 #include <stdint.h>
 
-#include "../../include/jsplace.h"
+#include "../../include/jsplace_bench.h"
 
 namespace jspm {
 

@@ -193,25 +193,25 @@ class Engine:
 
         def recovery(trials: int, idle_us: float, gap_us: float, patch_rows: np.ndarray, patch_taints: np.ndarray,
                      spin: bool = False) -> np.ndarray:
-            """The cold recovery timed in C (jsp_recovery_loop): per trial the
+            """The cold recovery timed in C (jspb_recovery_loop): per trial the
             idle wait, a one-row patch, the gap, jsp_place. [trials, 3] µs:
             patch call, place call, gap."""
             pr = np.ascontiguousarray(patch_rows, dtype=np.uint32)
             pt = np.ascontiguousarray(patch_taints, dtype=np.uint32)
             out = np.zeros((int(trials), 3), dtype=np.float64)
-            check(self._lib.jsp_recovery_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
+            check(self._lib.jspb_recovery_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
                                               int(trials), float(idle_us), float(gap_us), 1 if spin else 0, _p(pr),
                                               _p(pt), int(pr.shape[0]), out.ctypes.data))
             return out
 
         def loop(iters: int, patch_rows: Optional[np.ndarray] = None,
                  patch_taints: Optional[np.ndarray] = None) -> Tuple[float, float, float]:
-            """`iters` calls back to back timed in C (jsp_place_loop), each
+            """`iters` calls back to back timed in C (jspb_place_loop), each
             after a one-row taint patch when rows are given: total, median and
             p99 per step, microseconds."""
             pr = None if patch_rows is None else np.ascontiguousarray(patch_rows, dtype=np.uint32)
             pt = None if patch_taints is None else np.ascontiguousarray(patch_taints, dtype=np.uint32)
-            check(self._lib.jsp_place_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
+            check(self._lib.jspb_place_loop(self._h, rc.ctypes.data, rl.ctypes.data, rc.shape[0], assign.ctypes.data,
                                            int(iters), _p(pr), _p(pt), 0 if pr is None else int(pr.shape[0]),
                                            loop_out.ctypes.data))
             return float(loop_out[0]), float(loop_out[1]), float(loop_out[2])
@@ -267,9 +267,9 @@ class Engine:
                            scrub_bytes: int = 0) -> Tuple[float, float]:
         """(median, mean) device µs of `iters` back-to-back tallies on the
         engine stream, timed by events on the dispatches themselves
-        (jsp_tally_device_timed); with a scrub buffer, each one cold."""
+        (jspb_tally_device_timed); with a scrub buffer, each one cold."""
         out = np.zeros(2, dtype=np.float64)
-        check(self._lib.jsp_tally_device_timed(self._h, d_cap, d_occ, ld, iters, scrub or None, scrub_bytes,
+        check(self._lib.jspb_tally_device_timed(self._h, d_cap, d_occ, ld, iters, scrub or None, scrub_bytes,
                                                _p(out)))
         return float(out[0]), float(out[1])
 
@@ -277,31 +277,31 @@ class Engine:
                            iters: int, scrub: int = 0, scrub_bytes: int = 0) -> Tuple[float, float]:
         """(median, mean) device µs of `iters` back-to-back device-path
         placements (first dispatch start -> last dispatch end each;
-        jsp_place_device_timed); with a scrub buffer, each one cold."""
+        jspb_place_device_timed); with a scrub buffer, each one cold."""
         out = np.zeros(2, dtype=np.float64)
-        check(self._lib.jsp_place_device_timed(self._h, d_run_class, d_run_len, n_runs, n_jobs, d_assign, iters,
+        check(self._lib.jspb_place_device_timed(self._h, d_run_class, d_run_len, n_runs, n_jobs, d_assign, iters,
                                                scrub or None, scrub_bytes, _p(out)))
         return float(out[0]), float(out[1])
 
     def tally_device_spans(self, d_cap: int, d_occ: int, ld: int,
                            iters: int) -> Tuple[float, float, float, float]:
         """In-kernel span of the one-tile wave tally (first wave start -> last
-        wave end, device clock; jsp_tally_device_spans): (median, mean) us,
+        wave end, device clock; jspb_tally_device_spans): (median, mean) us,
         the dispatch-event time of an empty one-workgroup launch, and the
         back-to-back launches' period by the kernels' own clock."""
         out = np.zeros(4, dtype=np.float64)
-        check(self._lib.jsp_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
+        check(self._lib.jspb_tally_device_spans(self._h, d_cap, d_occ, ld, int(iters), _p(out)))
         return float(out[0]), float(out[1]), float(out[2]), float(out[3])
 
     def link_floor(self, iters: int = 2000) -> Tuple[float, float, float]:
         """Host -> device -> host round trip through pinned memory with the
-        resident service's polling (jsp_engine_link_floor): (p50, p99, mean) us."""
+        resident service's polling (jspb_link_floor): (p50, p99, mean) us."""
         out = np.zeros(3, dtype=np.float64)
-        check(self._lib.jsp_engine_link_floor(self._h, int(iters), _p(out)))
+        check(self._lib.jspb_link_floor(self._h, int(iters), _p(out)))
         return float(out[0]), float(out[1]), float(out[2])
 
     def set_fused(self, enable: bool) -> None:
-        check(self._lib.jsp_engine_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
+        check(self._lib.jspb_set_fused(self._h, native.JSP_FUSED_AUTO if enable else native.JSP_FUSED_OFF))
 
     def set_service(self, enable: bool, parked: bool = False) -> None:
         """Resident placement service for host-API placements
@@ -316,7 +316,7 @@ class Engine:
 
     def service_clock(self) -> np.ndarray:
         """The last timed service request's per-tile 100 MHz stamps [tiles, 8]
-        (jsp_engine_service_clock); empty when none is held."""
+        (jspb_service_clock); empty when none is held."""
         return self.service_clock_rows()[0]
 
     def service_clock_rows(self) -> Tuple[np.ndarray, np.ndarray]:
@@ -324,7 +324,7 @@ class Engine:
         seen in the mailbox, 1 bell rung) of the last timed service request."""
         out = np.zeros(257 * 8, dtype=np.uint32)
         n = ctypes.c_uint32(0)
-        check(self._lib.jsp_engine_service_clock(self._h, _p(out), out.shape[0], ctypes.byref(n)))
+        check(self._lib.jspb_service_clock(self._h, _p(out), out.shape[0], ctypes.byref(n)))
         k = n.value
         return out[:k * 8].reshape(k, 8), out[k * 8:(k + 1) * 8]
 
@@ -347,13 +347,20 @@ class Engine:
                                              rows.shape[0], _p(out)))
         return out[:rows.shape[0]]
 
-    # ---------------------------------------------------------------- instrumentation
+    # ---------------------------------------------------------------- metrics (jsp_engine_get_metrics)
+    def metrics(self, reset: bool = False) -> native.JspMetrics:
+        """The engine's histograms and counters (jsplace.h jsp_metrics)."""
+        m = native.JspMetrics()
+        check(self._lib.jsp_engine_get_metrics(self._h, ctypes.byref(m), 1 if reset else 0))
+        return m
+
+    # ---------------------------------------------------------------- instrumentation (jsplace_bench.h)
     def set_timing(self, enable: bool) -> None:
-        check(self._lib.jsp_engine_set_timing(self._h, 1 if enable else 0))
+        check(self._lib.jspb_set_timing(self._h, 1 if enable else 0))
 
     def timing(self, reset: bool = True) -> JspTiming:
         t = JspTiming()
-        check(self._lib.jsp_engine_get_timing(self._h, ctypes.byref(t), 1 if reset else 0))
+        check(self._lib.jspb_get_timing(self._h, ctypes.byref(t), 1 if reset else 0))
         return t
 
     @property

@@ -54,11 +54,43 @@ class JspTiming(ctypes.Structure):
                 ("wake_us", ctypes.c_double)]
 
 
+HIST_BUCKETS = 32
+HIST_LO_US, HIST_LO_JOBS = 0.5, 1.0
+
+
+class JspHist(ctypes.Structure):
+    _fields_ = [("count", ctypes.c_uint64), ("sum", ctypes.c_double), ("max", ctypes.c_double),
+                ("bucket", ctypes.c_uint64 * HIST_BUCKETS)]
+
+    def upper_bounds(self, lo: float):
+        """`le` of each bucket (the last one +inf), as a Prometheus exporter
+        would publish them."""
+        return [lo * 2.0 ** i for i in range(HIST_BUCKETS - 1)] + [float("inf")]
+
+    def quantile(self, q: float, lo: float) -> float:
+        """Upper bound of the bucket holding the q-quantile."""
+        target, acc = q * self.count, 0
+        for ub, n in zip(self.upper_bounds(lo), self.bucket):
+            acc += n
+            if acc >= target and acc > 0:
+                return ub
+        return float("inf")
+
+
+class JspMetrics(ctypes.Structure):
+    _fields_ = [("place_us", JspHist), ("patch_us", JspHist), ("batch_jobs", JspHist), ("device_us", JspHist),
+                ("placed", ctypes.c_uint64), ("unplaceable", ctypes.c_uint64), ("place_errors", ctypes.c_uint64),
+                ("patch_errors", ctypes.c_uint64), ("svc_calls", ctypes.c_uint64), ("svc_starts", ctypes.c_uint64),
+                ("svc_fallbacks", ctypes.c_uint64)]
+
+
 JSP_FUSED_OFF, JSP_FUSED_AUTO = 0, 1
 JSP_SERVICE_OFF, JSP_SERVICE_AUTO, JSP_SERVICE_PARKED = 0, 1, 2
 
 
 # (name, restype, argtypes) — every entry point declared in include/jsplace.h
+# (the product boundary) and, after it, include/jsplace_bench.h (jspb_*: the
+# bench's and probes' symbol set)
 SIGNATURES = [
     ("jsp_abi_version", ctypes.c_int, []),
     ("jsp_last_error", ctypes.c_char_p, []),
@@ -73,27 +105,29 @@ SIGNATURES = [
     ("jsp_classes_upload", ctypes.c_int, [vp, ctypes.POINTER(JspJobClass), u32]),
     ("jsp_place", ctypes.c_int, [vp, vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
     ("jsp_place_jobs", ctypes.c_int, [vp, vp, u32, vp, vp, vp, ctypes.POINTER(JspStats)]),
-    ("jsp_place_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, u32, vp]),
-    ("jsp_recovery_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, ctypes.c_double, ctypes.c_double, ctypes.c_int,
-                                         vp, vp, u32, vp]),
     ("jsp_tally_device", ctypes.c_int, [vp, vp, vp, u32, vp]),
     ("jsp_assign_device", ctypes.c_int, [vp, vp, vp, u32, vp, vp, u32, u32, vp, vp]),
     ("jsp_place_device", ctypes.c_int, [vp, vp, vp, u32, u32, vp, vp]),
     ("jsp_resolve_leader_domains", ctypes.c_int, [vp, vp, vp, u32, vp]),
     ("jsp_audit_placements", ctypes.c_int, [vp, vp, vp, vp, vp, u32, vp]),
-    ("jsp_engine_set_fused", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_set_service", ctypes.c_int, [vp, ctypes.c_int]),
     ("jsp_engine_service_stop", ctypes.c_int, [vp]),
-    ("jsp_engine_service_clock", ctypes.c_int, [vp, vp, u32, vp]),
-    ("jsp_tally_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, ctypes.c_size_t, vp]),
-    ("jsp_place_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, u32, vp, ctypes.c_size_t, vp]),
-    ("jsp_engine_link_floor", ctypes.c_int, [vp, u32, vp]),
-    ("jsp_tally_device_spans", ctypes.c_int, [vp, vp, vp, u32, u32, vp]),
-    ("jsp_engine_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
-    ("jsp_engine_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
+    ("jsp_engine_get_metrics", ctypes.c_int, [vp, ctypes.POINTER(JspMetrics), ctypes.c_int]),
     ("jsp_engine_stream", vp, [vp]),
     ("jsp_engine_sync", ctypes.c_int, [vp]),
     ("jsp_engine_check", ctypes.c_int, [vp]),
+    # jsplace_bench.h
+    ("jspb_place_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, vp, vp, u32, vp]),
+    ("jspb_recovery_loop", ctypes.c_int, [vp, vp, vp, u32, vp, u32, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                         vp, vp, u32, vp]),
+    ("jspb_set_fused", ctypes.c_int, [vp, ctypes.c_int]),
+    ("jspb_service_clock", ctypes.c_int, [vp, vp, u32, vp]),
+    ("jspb_tally_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, ctypes.c_size_t, vp]),
+    ("jspb_place_device_timed", ctypes.c_int, [vp, vp, vp, u32, u32, vp, u32, vp, ctypes.c_size_t, vp]),
+    ("jspb_link_floor", ctypes.c_int, [vp, u32, vp]),
+    ("jspb_tally_device_spans", ctypes.c_int, [vp, vp, vp, u32, u32, vp]),
+    ("jspb_set_timing", ctypes.c_int, [vp, ctypes.c_int]),
+    ("jspb_get_timing", ctypes.c_int, [vp, ctypes.POINTER(JspTiming), ctypes.c_int]),
 ]
 
 _lib = None

@@ -11,12 +11,13 @@ from jobset_amd import native
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "jsplace.h")
+BENCH_HEADER = os.path.join(ROOT, "include", "jsplace_bench.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(path=HEADER):
+    src = open(path).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(jsp_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(jspb?_[a-z_0-9]+)\s*\(", src, flags=re.M)
     return sorted(set(names))
 
 
@@ -27,15 +28,30 @@ def test_header_declares_entry_points():
 
 def test_library_exports_every_declared_symbol():
     lib = native.lib()
-    for name in declared_functions():
+    both = declared_functions() + declared_functions(BENCH_HEADER)
+    for name in both:
         assert hasattr(lib, name), f"libjsplace.so does not export {name}"
     bound = {n for n, _, _ in native.SIGNATURES}
-    assert bound == set(declared_functions()), "native.SIGNATURES out of sync with include/jsplace.h"
+    assert bound == set(both), "native.SIGNATURES out of sync with include/jsplace.h + jsplace_bench.h"
+
+
+def test_product_header_is_what_the_go_binding_calls():
+    """include/jsplace.h lists only the product -- every
+    entry point in it is called by INTEGRATION.md's cgo binding, and every
+    measurement / tuning entry point is in the separate jspb_ symbol set."""
+    prod, bench = declared_functions(), declared_functions(BENCH_HEADER)
+    assert all(n.startswith("jsp_") for n in prod), prod
+    assert bench and all(n.startswith("jspb_") for n in bench), bench
+    go = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    called = set(re.findall(r"C\.(jspb?_[a-z_0-9]+)\(", go))
+    assert called == set(prod), (sorted(set(prod) - called), sorted(called - set(prod)))
 
 
 def test_abi_version_and_struct_layout():
     lib = native.lib()
-    assert lib.jsp_abi_version() == 6
+    assert lib.jsp_abi_version() == 7
+    assert ctypes.sizeof(native.JspHist) == 8 * 3 + 8 * native.HIST_BUCKETS
+    assert ctypes.sizeof(native.JspMetrics) == 4 * ctypes.sizeof(native.JspHist) + 7 * 8
     # layouts the Go cgo wrapper relies on (INTEGRATION.md)
     assert ctypes.sizeof(native.JspJobClass) == 8 * 4 * 2 + 4 * 3 + 4 * 4 + 4  # 100 B + 4 pad
     assert ctypes.sizeof(native.JspTopology) == 4 + 4 * 4 + 4 + 8 * 4

@@ -708,7 +708,7 @@ def test_caller_stream_destroyed_between_calls(engine):
 
 @pytest.mark.parametrize("cfg", [2, 4, 5])
 def test_device_timed_entry_points(engine, cfg):
-    """jsp_tally_device_timed / jsp_place_device_timed (the bench's kernel-time
+    """jspb_tally_device_timed / jspb_place_device_timed (the bench's kernel-time
     legs): back-to-back steps timed by events on their own dispatches, warm
     and behind the library's cache scrub; the buffers they leave hold the
     oracle's answer."""

@@ -29,12 +29,13 @@ def test_host_and_oracle_suites_under_asan_ubsan():
                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1",
                JSP_LIB_PATH=os.path.join(ROOT, "build/asan/libjsplace.so"),
                JSPO_LIB_PATH=os.path.join(ROOT, "oracle/sanitize/libjsp_oracle.so"),
-               JSPF_LIB_PATH=os.path.join(ROOT, "oracle/sanitize/libjsp_cpufast.so"))
+               JSPF_LIB_PATH=os.path.join(ROOT, "oracle/sanitize/libjsp_cpufast.so"), JSP_UNDER_SANITIZER="1")
     probe = ("import jobset_amd.native as n, oracle.oracle as o; n.lib(); o.fast_lib(); m=open('/proc/self/maps').read();"
              "print(int('asan/libjsplace.so' in m and 'sanitize/libjsp_cpufast.so' in m and 'libasan' in m))")
     r = subprocess.run([sys.executable, "-c", probe], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.stdout.strip().endswith("1"), r.stdout + r.stderr[-2000:]
     r = subprocess.run([sys.executable, "-m", "pytest", "-x", "-q", "-m", "not gpu", "-p", "no:cacheprovider",
-                        "tests/test_host_parity.py", "tests/test_ingest.py", "tests/test_oracle.py"],
+                        "tests/test_host_parity.py", "tests/test_ingest.py", "tests/test_oracle.py",
+                        "tests/test_concurrency.py"],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]

@@ -752,6 +752,75 @@ def test_micro_patch_rows_from_the_microbox(svc_engine, cols):
     np.testing.assert_array_equal(got.occ, occ)
 
 
+@pytest.mark.parametrize("pair", [(0, -1), (-1, -2), (0, 1)])
+def test_micro_patch_two_rows_at_the_ends(svc_engine, pair):
+    """Two rows in one micro-patch (the most a request line carries at W=1,
+    R=3): the snapshot's first and last rows, the last two, the first two --
+    as one patch call, and as two calls that merge into one held
+    micro-patch. Row 0 and row N-1 are where the round-5 aperture fault's
+    row-id word (k == 0) sat; bit-exact after each place."""
+    p = synth.config2()
+    svc_engine.load(p)
+    assert warm(svc_engine, p.job_class).fused == 3
+    N = p.nodes.n_nodes
+    rows = np.array([r % N for r in pair], dtype=np.uint32)
+    for k, how in enumerate(("one call", "two calls", "one call")):
+        lab = p.nodes.labels[:, [(7 * k + 5) % N, (11 * k + 3) % N]].copy()
+        t = np.array([k & 1, (k + 1) & 1], dtype=np.uint32)
+        if how == "one call":
+            svc_engine.patch_rows(rows, labels=lab, taints=t)
+        else:
+            svc_engine.patch_rows(rows[:1], labels=lab[:, :1], taints=t[:1])
+            svc_engine.patch_rows(rows[1:], labels=lab[:, 1:], taints=t[1:])
+        p.nodes.labels[:, rows] = lab
+        p.nodes.taints[rows] = t
+        got = svc_engine.place(p.job_class)
+        assert got.fused == 3
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0], err_msg=f"{how} {pair}")
+    a, cap, occ = O.place_c(p)
+    got = svc_engine.place(p.job_class, want_tally=True)
+    np.testing.assert_array_equal(got.assign, a)
+    np.testing.assert_array_equal(got.cap, cap)
+
+
+def test_microbox_wait_that_gives_up_is_reported(svc_engine, monkeypatch):
+    """a resident tile whose wait for the request's
+    micro-patch rows gives up must not answer from the registers it holds.
+    micro_spins=0 makes every microbox wait give up: the tiles write no answer
+    line but the service's error word, the host stops the service and answers
+    the call on the launch path from the rows in memory (the dispatcher wrote
+    the patch through before its completion word) -- the right answer,
+    counted as a service fallback, never a stale one. The next request starts
+    a fresh service; bit-exact throughout."""
+    p = synth.config2()
+    monkeypatch.setenv("JSP_TEST_HOOKS", "micro_spins=0")
+    try:
+        svc_engine.load(p)  # hooks are read at upload
+        assert warm(svc_engine, p.job_class).fused == 3
+        a0 = O.place_c(p)[0]
+        np.testing.assert_array_equal(svc_engine.place(p.job_class).assign, a0)
+        for k in range(3):
+            # a row of a placed rack made infeasible (an untolerated taint)
+            r = int(p.nodes.leaf_start[int(a0[3 + 5 * k])])
+            t = np.array([p.nodes.taints[r] | (1 << 31)], dtype=np.uint32)
+            svc_engine.metrics(reset=True)
+            svc_engine.patch_rows(np.array([r], dtype=np.uint32), taints=t)
+            p.nodes.taints[r] = t[0]
+            want = O.place_c(p)[0]
+            got = svc_engine.place(p.job_class)
+            np.testing.assert_array_equal(got.assign, want)
+            assert got.fused not in (3, 5)  # the launch path answered it
+            m = svc_engine.metrics()
+            assert m.svc_fallbacks == 1 and m.place_errors == 0
+            got = warm(svc_engine, p.job_class)  # a fresh service, rows from memory
+            assert got.fused == 3
+            np.testing.assert_array_equal(got.assign, want)
+            a0 = want
+    finally:
+        monkeypatch.delenv("JSP_TEST_HOOKS")
+        svc_engine.load(p)
+
+
 @pytest.mark.parametrize("cfg", [2, 5])
 def test_parked_service_survives_idle_gaps(svc_engine, cfg):
     """JSP_SERVICE_PARKED: no idle exit. Gaps of several idle limits, a
@@ -795,7 +864,7 @@ def test_parked_service_survives_idle_gaps(svc_engine, cfg):
 
 @pytest.mark.parametrize("parked", [False, True])
 def test_recovery_loop_answers_exactly(svc_engine, parked):
-    """jsp_recovery_loop (the bench's C-timed cold recovery): idle sleeps past
+    """jspb_recovery_loop (the bench's C-timed cold recovery): idle sleeps past
     the idle limit, one-row patches with the rows' own values, gaps; every
     call succeeds, the last answer is the oracle's, and each trial's three
     times are sane."""

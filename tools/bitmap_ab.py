@@ -1,7 +1,7 @@
 """Compaction service answer forms, interleaved A/B in one process
 (diagnostic): tile bitmaps expanded on the host (default) vs per-job entries
 after the tiles' look-back (test hook svc_entries=1). Host-API calls timed in
-C (jsp_place_loop); the host's post -> first / last answer split from
+C (jspb_place_loop); the host's post -> first / last answer split from
 jsp_timing (svc_first_us / svc_answer_us)."""
 import os
 import sys

@@ -1,5 +1,5 @@
 """Back-to-back host-API placements against placements with a gap (test
-hook loop_gap_ns: jsp_place_loop spins between calls), cfg2 (diagnostic):
+hook loop_gap_ns: jspb_place_loop spins between calls), cfg2 (diagnostic):
 per-call time without the gap, and the library's request post -> first /
 last answer line. A post -> first that shrinks as the gap grows means the
 service was not ready for a request right behind the previous answer."""

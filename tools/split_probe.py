@@ -1,4 +1,4 @@
-"""Split-service host-API calls (cfg3, cfg5) timed in C (jsp_place_loop), with
+"""Split-service host-API calls (cfg3, cfg5) timed in C (jspb_place_loop), with
 the library's phase clocks per call: entry -> request post (svc_pre), post ->
 answer complete incl. the host walk (svc_answer), the walk's share
 (host_post), and the host-link floor. Diagnostic."""

@@ -21,7 +21,7 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
     eng = Engine(0)
     fl = eng.link_floor(2000)
-    print(f"host-link floor (jsp_engine_link_floor): p50 {fl[0]:.2f} us p99 {fl[1]:.2f}", flush=True)
+    print(f"host-link floor (jspb_link_floor): p50 {fl[0]:.2f} us p99 {fl[1]:.2f}", flush=True)
     cfgs = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 2]
     for cfg in cfgs:
         p = synth.CONFIGS[cfg]()

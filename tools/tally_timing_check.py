@@ -1,6 +1,6 @@
 """The cfg4 tally's device time two ways in one process (diagnostic, DESIGN.md
 §9): events on the dispatch packets of K back-to-back launches inside the
-library (jsp_tally_device_timed, what bench.py reports) -- run it under
+library (jspb_tally_device_timed, what bench.py reports) -- run it under
 rocprofv3 --kernel-trace --stats and compare with the trace's own durations
 of the same launches. Also the folded-feasibility step's tally (the host API
 and jsp_place_device path) for its grid size."""

@@ -2,7 +2,7 @@
 """A/B of the call-entry prefetch of the engine's lines (jsp_engine.cc
 warm_engine; test hook warm=0 turns it off) on the realistic cold recovery
 of cfg2: sleep 60 ms, one-row patch, gap, jsp_place, timed in C
-(jsp_recovery_loop), default and parked service. Alternating blocks per
+(jspb_recovery_loop), default and parked service. Alternating blocks per
 variant; p50 / p95 / p99 of patch + place, and the patch and place p50.
 Diagnostic only."""
 import os
