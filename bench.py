@@ -66,11 +66,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md "Chip-level
 METRIC = "exclusive-topology placements/sec at 15k nodes; p99 recovery placement latency"
 LINE_MAX_BYTES = 6144  # the driver keeps the last 8 KB of stdout+stderr; leave room for stderr
 SHAPES = {0: "three launches", 1: "fused single launch", 2: "one-class compaction, one launch",
-          3: "compaction service (resident)", 5: "split service (resident tiles, host walk)"}
-# the launch shape the device path (jsp_place_device) takes for a host-API shape
-DEVICE_SHAPE = {3: 2, 4: 1, 5: 1}
+          3: "compaction service (resident)", 5: "split service (resident tiles, host walk)",
+          7: "tally + feasibility launches, host walk", 8: "split tiles launched once, host walk"}
 KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel", 3: "place_compact_kernel",
-          4: "place_fused_kernel", 5: "place_fused_kernel"}
+          4: "place_fused_kernel", 5: "place_fused_kernel", 7: "tally_kernel", 8: "place_split_service_kernel"}
 # cold recovery: the gap between the patch and the place (ms) -> share of --cold-trials
 COLD_GAPS = {1.0: 1.0, 0.0: 0.1, 10.0: 0.1}
 COLD_SLEEP_EXTRA_MS = 5.0  # a trial sleeps the idle limit plus this (the service has left)
@@ -850,12 +849,17 @@ def main() -> None:
                 st()
             us = event_loop_us(st, 200, stream)
             eng.check()
-            dev_shape = DEVICE_SHAPE.get(r.fused, r.fused)  # the device path's launch shape (no service there)
-            kb = compact_bytes(pc) if dev_shape == 2 else (tally_bytes(pc) + placement_tail_bytes(pc) if dev_shape == 1
-                                                           else tally_bytes(pc))
+            # the device path's launch shape (no service there): what the launch path reports
+            eng.set_service(False)
+            dev_shape = eng.place(pc.job_class).fused
+            eng.set_service(True)
+            r = settled_place(eng, pc.job_class)
+            kb = compact_bytes(pc) if dev_shape == 2 else tally_bytes(pc) if dev_shape == 8 else \
+                tally_bytes(pc) + placement_tail_bytes(pc)
             line = {"nodes": pc.nodes.n_nodes, "jobs": pc.n_jobs, "classes": len(pc.classes),
                     "levels": pc.topology.n_levels, "placed": r.placed, "shape": SHAPES.get(r.fused, str(r.fused)),
-                    "kernel_us": round(us, 2), "kernel_kernel": KERNEL[dev_shape], "kernel_bytes": kb,
+                    "kernel_us": round(us, 2), "kernel_shape": SHAPES.get(dev_shape, str(dev_shape)),
+                    "kernel_kernel": KERNEL.get(dev_shape), "kernel_bytes": kb,
                     "kernel_frac": round(kb / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 5),
                     "host_api_resident": host_api_latency(eng, pc, 200)}
             if r.fused in (3, 5):

@@ -138,7 +138,14 @@ typedef struct jsp_stats {
                                   3 one-class compaction answered by the resident service,
                                   4 (unused since ABI v6: the fused resident kernel was retired),
                                   5 split service: resident tiles + the walk on the host,
-                                  6 device set: shard tallies combined (RCCL / on-device add), then assign */
+                                  6 device set: shard tallies combined (RCCL / on-device add), then assign,
+                                  7 (ABI v7) tally + feasibility on the GPU, the walk on the host: every
+                                    shape the GPU level walker does not take (several levels, or more
+                                    than 32 runs), up to 65536 jobs -- launch path and device paths
+                                    (jspb_set_fused OFF keeps the GPU walkers: shape 0),
+                                  8 (ABI v7) the split service's tiles launched for this one request, the
+                                    walk on the host: the launch path and the device paths of every shape
+                                    the split service takes, when no tallies are requested */
     double wall_us;            /* host wall time of the call */
 } jsp_stats;
 

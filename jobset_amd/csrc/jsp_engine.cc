@@ -174,6 +174,7 @@ struct TestHooks {
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
     bool warm = true;               // warm=0: no call-entry prefetch of the engine's lines (A/B)
     uint32_t micro_spins = 1u << 22;  // micro_spins=N: a resident tile's passes over the microbox (kErrMicro)
+    bool level_done = true;         // level_done=0: the host API syncs the stream after a level walk (A/B)
 };
 
 TestHooks read_hooks() {
@@ -205,6 +206,7 @@ TestHooks read_hooks() {
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
         else if (k == "warm") h.warm = v != 0;
         else if (k == "micro_spins") h.micro_spins = (uint32_t)v;
+        else if (k == "level_done") h.level_done = v != 0;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -280,7 +282,22 @@ struct jsp_engine {
     unsigned long long patch_target = 0;
     uint32_t patch_seq = 0;
     bool patch_pending = false;
+    // the device paths' host walk (host_walk_impl): feasibility words and,
+    // for device-resident run lists, the runs and assign[] through pinned
+    // staging; ev_hw marks the staged inputs, ev_hw_copy the assign[] copy
+    // that still reads the staging (the next walk waits for it)
+    HostBuf hw_feas, hw_io;
+    hipEvent_t ev_hw = nullptr, ev_hw_copy = nullptr;
+    bool hw_pending = false;
+    // the split tiles launched for one request (split_oneshot): their answer
+    // lines (pinned), the geometry the host walk's tile table was set for,
+    // and the request numbers of these launches
+    HostBuf os_split;
+    unsigned long long os_key = ~0ull;
+    uint32_t os_seq = 0;
     DevBuf lvl_ready;                   // the one-launch level walk's published record count
+    DevBuf lvl_fin;                     // its workgroups' completion count (host API completion word)
+    unsigned long long lvl_fin_draws = 0;
     uint32_t lvl_epoch = 0;
     uint32_t err_tag = 0;               // launches that may report a timed-out wait (kernel error words)
     bool patch_svc = false;             // the pending patch goes to the service's dispatcher
@@ -404,6 +421,8 @@ struct jsp_engine {
                 if (p.b) (void)hipEventDestroy(p.b);
             }
         if (ev_switch) (void)hipEventDestroy(ev_switch);
+        if (ev_hw) (void)hipEventDestroy(ev_hw);
+        if (ev_hw_copy) (void)hipEventDestroy(ev_hw_copy);
         if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.ev_exit) (void)hipEventDestroy(svc.ev_exit);
@@ -702,9 +721,89 @@ bool level_walk_ok(jsp_engine* e, uint32_t n_runs) {
     return nw >= 1 && nw <= jsp::kLevelMaxWords && jsp::level_walk_lds_bytes(e->C, nw) <= 128u * 1024u;
 }
 
+// The walk on the host (ABI v7) for every shape the level walker does not
+// take -- several levels, or many runs -- up to kHostWalkMaxJobs jobs: there
+// the GPU walk is one wave's dependent scalar chain at ~100 shader cycles per
+// job visit (cfg5: 49.6 us, SQ_WAIT_ANY 82 % of its wave cycles, DESIGN.md
+// §4.2), while the host walks the same bitmaps in ~2.5 us (jsp_walk.cc, the
+// split service's walk; SURVEY.md §7 step 5 allows the sequential part of A7
+// on the host). The GPU computes the feasibility words; the host reads them,
+// walks, and writes assign[].
+constexpr uint32_t kHostWalkMaxJobs = 1u << 16;
+
+// (JSP_FUSED_OFF keeps every walk on the GPU: the three-launch shape, which
+// the tests use to exercise the GPU walkers on the shapes AUTO walks here)
+bool host_walk_ok(jsp_engine* e, uint32_t n_runs, uint32_t J) {
+    return e->fused_mode == JSP_FUSED_AUTO && e->C >= 1 && n_runs > 0 && J > 0 && J <= kHostWalkMaxJobs &&
+           !level_walk_ok(e, n_runs);
+}
+
+// Feasibility (feas_kernel into pinned memory, or the folded words copied
+// there), the run list staged when it is device-resident, one wait, the walk,
+// and assign[] copied back when it is device-resident. host_io: run_class,
+// run_len and d_assign are pinned host memory (the host API's staging) -- no
+// copies, the walk writes assign[] in place and the stats too. The call's
+// stop event (a caller stream's end-of-call marker) rides on its last launch,
+// the assign[] copy.
+int host_walk_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
+                   const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign,
+                   hipStream_t s, bool folded, bool host_io) {
+    if (e->hw_pending) {  // the previous walk's assign[] copy still reads the staging
+        HIP_TRY(hipEventSynchronize(e->ev_hw_copy));
+        e->hw_pending = false;
+    }
+    if (!e->ev_hw) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw, hipEventDisableTiming));
+    if (!e->ev_hw_copy) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw_copy, hipEventDisableTiming));
+    const uint32_t fw = std::max<uint32_t>(e->feas_words, 1);
+    HIP_TRY(e->hw_feas.reserve((size_t)fw * 8, grave(e)));
+    if (!host_io) HIP_TRY(e->hw_io.reserve((size_t)n_runs * 8 + (size_t)J * 4, grave(e)));
+    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : e->hw_io.as<uint32_t>();
+    uint32_t* hrl = host_io ? const_cast<uint32_t*>(run_len) : hrc + n_runs;
+    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(e->hw_io.as<uint32_t>() + 2 * (size_t)n_runs);
+    EvPair* p = ev_begin(e, 1, s);
+    if (folded)
+        HIP_TRY(jsp::launch_copy_u32(e->feas.as<uint32_t>(), e->hw_feas.as<uint32_t>(), 2 * e->feas_words, s));
+    else
+        HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
+                                 e->feas_words, e->topo, e->hw_feas.as<uint64_t>(), s));
+    ev_end(p, s);
+    if (!host_io) {
+        HIP_TRY(jsp::launch_copy_u32(run_class, hrc, n_runs, s));
+        HIP_TRY(jsp::launch_copy_u32(run_len, hrl, n_runs, s));
+    }
+    HIP_TRY(hipEventRecord(e->ev_hw, s));
+    e->walk.prefetch_state();  // while the device works
+    {
+        const auto t0 = std::chrono::steady_clock::now();
+        hipError_t q;
+        for (uint64_t spins = 1; (q = hipEventQuery(e->ev_hw)) == hipErrorNotReady; ++spins) {
+            if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return set_err(JSP_EHIP, "host walk: the device feasibility did not complete within 10 s");
+            _mm_pause();
+        }
+        if (q != hipSuccess) return set_err(JSP_EHIP, "host walk: feasibility failed: %s", hipGetErrorString(q));
+    }
+    p = ev_begin(e, 2, s);
+    const uint32_t placed = e->walk.walk(e->hw_feas.as<uint64_t>(), hrc, hrl, n_runs, out);
+    if (e->stats_override) {  // the host API reads them (pinned)
+        e->stats_override[0] = n_runs;
+        e->stats_override[1] = placed;
+    }
+    if (!host_io) {
+        HIP_TRY(jsp::launch_copy_u32(reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(assign), J, s));
+        HIP_TRY(hipEventRecord(e->ev_hw_copy, s));
+        e->hw_pending = true;
+    }
+    ev_end(p, s);
+    return JSP_OK;
+}
+
 int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
                 const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
-                int32_t* d_assign, hipStream_t s, bool folded = false) {
+                int32_t* d_assign, hipStream_t s, bool folded = false, bool host_io = false,
+                bool signal = false, uint32_t* n_signals = nullptr) {
+    if (host_walk_ok(e, n_runs, J))
+        return host_walk_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, J, d_assign, s, folded, host_io);
     EvPair* p = ev_begin(e, 1, s);
     if (!folded)
         HIP_TRY(jsp::launch_feas(d_cap, d_occ, ld, e->cls.as<jsp::DevClass>(), e->C, e->word_off.as<uint32_t>(),
@@ -725,9 +824,24 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
         }
         e->lvl_epoch = e->lvl_epoch % 0x7FFFFFFFu + 1u;
         we.tag = next_err_tag(e, jsp::kErrExpand);
+        // the host API waits for a completion word the launch's last
+        // workgroup writes, not for the stream (a synchronize reports a
+        // kernel's end microseconds after it)
+        jsp::LevelDone fin{nullptr, nullptr, 0ull, 0u};
+        if (signal && e->hooks.level_done) {
+            if (!e->lvl_fin.p) {
+                HIP_TRY(e->lvl_fin.reserve(64));
+                HIP_TRY(hipMemsetAsync(e->lvl_fin.p, 0, 64, s));
+                e->lvl_fin_draws = 0;
+            }
+            e->lvl_fin_draws += jsp::level_walk_grid(e->C, nw, n_runs, J);
+            fin = jsp::LevelDone{e->h_done.as<uint32_t>(), e->lvl_fin.as<unsigned long long>(), e->lvl_fin_draws,
+                                 e->epoch};
+            if (n_signals) *n_signals = 1;
+        }
         HIP_TRY(jsp::launch_assign_level(e->feas.as<uint64_t>(), e->C, nw, d_run_class, d_run_len, n_runs, J, d_assign,
                                          stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(), s,
-                                         e->lvl_ready.as<unsigned long long>(), e->lvl_epoch, we));
+                                         e->lvl_ready.as<unsigned long long>(), e->lvl_epoch, we, fin));
         ev_end(p, s);
         return JSP_OK;
     }
@@ -804,13 +918,115 @@ jsp::FusedArgs fused_args(jsp_engine* e, jsp::TallyArgs& a, const uint32_t* d_ru
     return f;
 }
 
+bool split_ok(jsp_engine* e);
+uint32_t split_groups(jsp_engine* e);
+uint32_t next_seq(uint32_t q);
+
+// The split shape launched for one request (ABI v7, shape 8): the resident
+// split service's tiles (tally, per-leaf feasibility ballots, upper-domain
+// partial sums, tagged lines into pinned memory) as one launch of tiles only
+// -- no dispatcher, no residency -- and the host walk over their lines, as
+// the service's answer is walked. The launch path and the device paths of
+// every multi-class / multi-level shape the split service takes, up to
+// kHostWalkMaxJobs jobs. host_io: the run list and assign[] are pinned host
+// memory (the host API's staging); otherwise they are device buffers, staged
+// through pinned memory by copy launches on the same stream.
+bool split_oneshot_ok(jsp_engine* e, uint32_t n_runs, uint32_t J) {
+    return e->fused_mode == JSP_FUSED_AUTO && n_runs > 0 && J > 0 && J <= kHostWalkMaxJobs && split_ok(e);
+}
+
+int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
+                  int32_t* assign, hipStream_t s, bool host_io) {
+    const uint32_t g = split_groups(e), cpg = (e->C + g - 1) / g, nb = e->n_blocks, n_tiles = nb * g;
+    const uint32_t nw = jsp::split_waves(e->blk_l0, e->blk_l1);
+    const size_t sb = (size_t)n_tiles * jsp::split_tile_words(cpg, nw) * 8;
+    if (e->hw_pending) {  // a previous device-path walk's assign[] copy still reads the staging
+        HIP_TRY(hipEventSynchronize(e->ev_hw_copy));
+        e->hw_pending = false;
+    }
+    if (!e->ev_hw) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw, hipEventDisableTiming));
+    if (!e->ev_hw_copy) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw_copy, hipEventDisableTiming));
+    if (sb > e->os_split.bytes || !e->os_split.p) {
+        HIP_TRY(e->os_split.reserve(sb, grave(e)));
+        std::memset(e->os_split.p, 0, e->os_split.bytes);  // tags: request 0 is never posted
+    }
+    const unsigned long long key = ((unsigned long long)nb << 40) | ((unsigned long long)g << 32) | cpg;
+    if (e->os_key != key) {
+        e->walk.set_tiles(e->blk_l0, e->blk_l1, g, cpg);
+        e->os_key = key;
+        e->svc.layout_key = ~0ull;  // the service re-lays its own slots (and the walk's tiles) at its next start
+    }
+    if (!host_io) HIP_TRY(e->hw_io.reserve((size_t)n_runs * 8 + (size_t)J * 4, grave(e)));
+    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : e->hw_io.as<uint32_t>();
+    uint32_t* hrl = host_io ? const_cast<uint32_t*>(run_len) : hrc + n_runs;
+    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(e->hw_io.as<uint32_t>() + 2 * (size_t)n_runs);
+    if (!host_io) {
+        HIP_TRY(jsp::launch_copy_u32(run_class, hrc, n_runs, s));
+        HIP_TRY(jsp::launch_copy_u32(run_len, hrl, n_runs, s));
+    }
+    e->os_seq = next_seq(e->os_seq);
+    const uint32_t seq = e->os_seq;
+    const jsp::TallyArgs ta = tally_args(e, nullptr, nullptr, e->L_total);
+    jsp::SplitArgs sp{};
+    sp.groups = g;
+    sp.cpg = cpg;
+    sp.nw = nw;
+    sp.C = e->C;
+    sp.out = e->os_split.as<uint64_t>();
+    sp.topo = e->topo;
+    jsp::ServiceArgs a{};
+    a.oneshot = seq;
+    EvPair* p = ev_begin(e, 3, s);
+    HIP_TRY(jsp::launch_split_oneshot(ta, sp, a, s));
+    ev_end(p, s);
+    if (!host_io) HIP_TRY(hipEventRecord(e->ev_hw, s));
+    e->walk.prefetch_state();
+    // every tile's tagged lines (the answer), bounded; a failed stream is an error
+    const uint64_t* slots = e->os_split.as<uint64_t>();
+    uint32_t t = 0;
+    QueryPacer qp;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t spins = 1;; ++spins) {
+        while (t < n_tiles && e->walk.tile_ready(slots, t, seq)) ++t;
+        if (t == n_tiles) break;
+        if ((spins & 7) == 1)
+            for (uint32_t u = t + 1; u < n_tiles; ++u) e->walk.prefetch_tile(slots, u);
+        if ((spins & 255) == 0 && qp.due()) {
+            const hipError_t q = hipStreamQuery(s);
+            if (q == hipSuccess) {
+                while (t < n_tiles && e->walk.tile_ready(slots, t, seq)) ++t;
+                if (t == n_tiles) break;
+                return set_err(JSP_EHIP, "split launch ended without the answer of tile %u", t);
+            }
+            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "split launch failed: %s", hipGetErrorString(q));
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return set_err(JSP_EHIP, "split launch: no answer within 10 s");
+        }
+    }
+    if (!host_io) {  // the staged run list (launched before the tiles: complete by now)
+        const hipError_t q = hipEventSynchronize(e->ev_hw);
+        if (q != hipSuccess) return set_err(JSP_EHIP, "split launch: run staging failed: %s", hipGetErrorString(q));
+    }
+    const uint32_t placed = e->walk.place(slots, hrc, hrl, n_runs, out);
+    if (e->stats_override) {
+        e->stats_override[0] = n_runs;
+        e->stats_override[1] = placed;
+    }
+    if (!host_io) {
+        HIP_TRY(jsp::launch_copy_u32(reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(assign), J, s));
+        HIP_TRY(hipEventRecord(e->ev_hw_copy, s));
+        e->hw_pending = true;
+    }
+    return JSP_OK;
+}
+
 // Whole placement on the engine's own tally buffers: one compaction launch for
 // a single leaf-level class, one fused launch when the snapshot is small, else
 // tally -> feas -> assign. `signal`: the single-launch shapes write host
 // completion words (e->h_done) tagged e->epoch; *n_signals says how many.
 int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
                int32_t* d_assign, hipStream_t s, bool signal = false, uint32_t* n_signals = nullptr,
-               bool want_tally = false) {
+               bool want_tally = false, bool host_io = false) {
     e->epoch = e->epoch % 0x3FFFFFFFu + 1u;
     if (n_signals) *n_signals = 0;
     if (compact_ok(e)) {
@@ -838,14 +1054,23 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
         e->tile_draws += e->n_blocks + jsp::kSpareBlocks;
         return JSP_OK;
     }
-    e->last_shape = fused_ok(e) ? 1 : 0;
-    if (e->last_shape == 0) {
+    // the split tiles launched for this request, the walk on the host (shape
+    // 8: no tallies wanted -- they stay in the tiles' LDS)
+    if (!want_tally && split_oneshot_ok(e, n_runs, J)) {
+        e->last_shape = 8;
+        return split_oneshot(e, d_run_class, d_run_len, n_runs, J, d_assign, s, host_io);
+    }
+    // the walk on the host after the GPU's tally and feasibility (shape 7), or
+    // on the GPU: one fused launch (shape 1), three launches (shape 0)
+    const bool hw = host_walk_ok(e, n_runs, J);
+    e->last_shape = hw ? 7 : fused_ok(e) ? 1 : 0;
+    if (e->last_shape != 1) {
         const bool fold = fold_ok(e);
         if (int rc = tally_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, s,
                                 fold ? e->feas.as<uint64_t>() : nullptr))
             return rc;
         return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_run_class, d_run_len,
-                           n_runs, J, d_assign, s, fold);
+                           n_runs, J, d_assign, s, fold, host_io, signal, n_signals);
     }
     jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
     jsp::FusedArgs f = fused_args(e, a, d_run_class, d_run_len, n_runs, J, d_assign, stats_ptr(e));
@@ -2389,6 +2614,9 @@ static void warm_engine(const jsp_engine* e, bool place) {
         warm_lines(e->svc.words.p, std::min<size_t>(e->svc.words.bytes, 4096));
         warm_lines(e->svc.bits.p, std::min<size_t>(e->svc.bits.bytes, 8192));
         warm_lines(e->blk_l0.data(), 4 * e->blk_l0.size());
+        // the split service's host walk: its bitmaps, sums, taken words and
+        // hierarchy tables (a cold core's walk was ~2 us slower, cfg5)
+        if (e->svc.shape == 3) e->walk.prefetch_state();
     } else {
         warm_lines(e->h_patch.p, std::min<size_t>(e->h_patch.bytes, 1024));
         warm_lines(e->svc.pstage.p, 256);
@@ -2866,7 +3094,7 @@ launch_path:
     uint32_t n_sig = 0;
     const auto t1 = std::chrono::steady_clock::now();
     const int prc = place_impl(e, h_rc, h_rl, n_runs, J, e->h_assign.as<int32_t>(), s, !want_tally, &n_sig,
-                               want_tally);
+                               want_tally, true);
     e->stats_override = nullptr;
     if (prc) return prc;
     const auto t2 = std::chrono::steady_clock::now();
@@ -2875,7 +3103,10 @@ launch_path:
             HIP_TRY(hipMemcpyAsync(tally_out, e->cap.p, (size_t)e->C * e->L_total * 4, hipMemcpyDeviceToHost, s));
         if (occ_out) HIP_TRY(hipMemcpyAsync(occ_out, e->occ.p, (size_t)e->L_total * 4, hipMemcpyDeviceToHost, s));
     }
-    if (n_sig > 0) {
+    if (!want_tally && (e->last_shape == 7 || e->last_shape == 8)) {
+        // the host walked: assign[] is complete, and nothing the stream still
+        // runs writes what the caller reads
+    } else if (n_sig > 0) {
         if (int rc = wait_done(e, s, n_sig, e->epoch)) return rc;
     } else {
         HIP_TRY(hipStreamSynchronize(s));
@@ -3170,7 +3401,7 @@ int jspi_assign(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
     if (int rc = ready(e, true)) return rc;
     if (int rc = check_launch_error(e)) return rc;
     if (int rc = enter_stream(e, e->stream)) return rc;
-    const int rc = assign_impl(e, d_cap, d_occ, ld, run_class, run_len, n_runs, J, assign, e->stream, folded);
+    const int rc = assign_impl(e, d_cap, d_occ, ld, run_class, run_len, n_runs, J, assign, e->stream, folded, true);
     if (int lr = leave_stream(e, e->stream)) return lr;
     return rc;
 }

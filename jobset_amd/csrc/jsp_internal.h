@@ -285,6 +285,9 @@ struct ServiceArgs {
     // the m rows of micro_row_words; or null
     unsigned long long* mbox;
     uint32_t micro_spins;               // passes over the microbox before a tile gives up (kErrMicro)
+    // split shape launched for one request (launch_split_oneshot): the
+    // request's seq, tiles only (no dispatcher), rows from memory; 0 = service
+    uint32_t oneshot;
 };
 
 // Split service (place_split_service_kernel): the fused shape's tiles stay
@@ -386,6 +389,8 @@ uint32_t service_row_cache_words(uint32_t la);
 size_t service_lds_bytes(uint32_t la, int W, int R, bool row_cache);
 size_t compact_lds_bytes(uint32_t la);
 hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);
+// the split tiles for one request (ServiceArgs::oneshot): grid = tiles
+hipError_t launch_split_oneshot(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s);
 size_t split_lds_bytes(uint32_t cpg, uint32_t la);
 // the split service's LDS: split_lds_bytes, then (row_cache) the tile's rows
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la);
@@ -400,6 +405,7 @@ size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint3
 // every level above the leaves; 0 when there is no such class or it exceeds
 // kFusedScrMax (the tail then builds those words one wave per word).
 uint32_t fused_scratch_words(uint32_t K, const uint32_t* D, const uint32_t* class_level, uint32_t C);
+hipError_t launch_copy_u32(const uint32_t* src, uint32_t* dst, uint32_t n, hipStream_t s);
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s);
@@ -421,10 +427,23 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
 // count) there once its records are written, and the launch's other
 // workgroups expand them (epoch: new per launch, != 0); an expander that
 // waits longer than we.wait_ticks writes we.tag to the error word.
+// The level walk's completion word for the host API (level_done): the
+// launch's workgroups count themselves in ctr (monotone across launches); the
+// one that makes it `target` writes `tag` to the host-mapped word `done`.
+// done == null: no completion word (the device paths).
+struct LevelDone {
+    uint32_t* done;
+    unsigned long long* ctr;
+    unsigned long long target;
+    uint32_t tag;
+};
+// workgroups of launch_assign_level's launch (the completion count)
+uint32_t level_walk_grid(uint32_t C, uint32_t nw, uint32_t n_runs, uint32_t J);
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
-                               uint32_t epoch, const WaitErr& we);
+                               uint32_t epoch, const WaitErr& we,
+                               const LevelDone& fin);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

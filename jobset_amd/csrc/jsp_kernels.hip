@@ -2171,6 +2171,24 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
 // their jobs' domains as expand_kernel does. A wave that gives up (the
 // walker, dispatched first, never published within wait.wait_ticks) writes
 // the launch's tag to the error word: the call fails, never a stale assign[].
+// The host API's completion word for the one-launch level walk (fin.done !=
+// null): every workgroup's assign[] stores go out (system-scope release),
+// then it counts itself in; the last one -- the launch's fin.target-th since
+// the engine was created -- writes fin.tag to the host word the caller spins
+// on, instead of a stream synchronize after the kernel's end.
+__device__ __forceinline__ void level_done(const LevelDone& fin) {
+    if (fin.done == nullptr) return;
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long old = __hip_atomic_fetch_add(fin.ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (old + 1ull == fin.target) {
+            __threadfence_system();
+            __hip_atomic_store(fin.done, fin.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+}
+
 __device__ void level_expand(const AssignRec* recs, const unsigned long long* ready, uint32_t epoch, uint32_t bound,
                              uint32_t rpw, int32_t* assign, const WaitErr& wait) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2238,13 +2256,14 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
                                                                      AssignRec* __restrict__ recs,
                                                                      unsigned long long* __restrict__ ready,
                                                                      uint32_t epoch, uint32_t bound, uint32_t rpw,
-                                                                     WaitErr wait) {
+                                                                     WaitErr wait, LevelDone fin) {
     // Expansion in the same launch (ready != null): workgroups 1.. wait for
     // the walker (workgroup 0, dispatched first, never waits for them) to
     // publish its record count, then expand the records as expand_kernel
     // does -- no second launch and no launch gap between walk and expansion.
     if (ready != nullptr && blockIdx.x > 0) {
         level_expand(recs, ready, epoch, bound, rpw, assign, wait);
+        level_done(fin);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][NT]
@@ -2371,6 +2390,7 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
         for (uint32_t j = a1 + tid; j < j1; j += (uint32_t)NT) assign[j] = -1;
     }
     JSP_STAMP(4050u, 7);
+    level_done(fin);
 }
 
 // ---- fused tail: leaf pass of the feasibility build (see place_fused_kernel)
@@ -3709,6 +3729,14 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     ag.cap_out = nullptr;  // the sums stay in LDS
     const uint4 bt = a.blk[ft.blk];
     uint64_t* out = sp.out + (size_t)tile * split_tile_words(sp.cpg, sp.nw);
+    if (v.oneshot != 0u) {
+        // one launch, one request (the launch path and the device paths of the
+        // split shape, ABI v7): no dispatcher, no bell, rows from memory; the
+        // tile answers request v.oneshot through its tagged lines and leaves
+        tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, nullptr, false);
+        split_emit(ag, sp, bt, out, v.oneshot, lds, s_x);
+        return;
+    }
     uint32_t seq = v.seq0;
     // the tile's rows stay in LDS between requests (as the compaction
     // service's; bit 63 of the bell: the snapshot was patched since the
@@ -4080,6 +4108,19 @@ hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const S
 }
 
 template <int W, int R>
+static hipError_t launch_split_oneshot_wr(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v,
+                                          hipStream_t s) {
+    jsp_launch((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups), dim3(kTallyThreads),
+               split_service_lds_bytes(sp.cpg, a.la, a.W, a.R, false), s, a, sp, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_split_oneshot(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v, hipStream_t s) {
+    if (v.oneshot == 0u || v.row_cache_words != 0u) return hipErrorInvalidValue;
+    JSP_DISPATCH_WR(launch_split_oneshot_wr, a, sp, v, s)
+}
+
+template <int W, int R>
 static hipError_t service_occupancy_wr(const TallyArgs&, int shape, size_t lds_bytes, int* blocks) {
     const void* fn = shape == 2 ? reinterpret_cast<const void*>(&place_service_kernel<W, R>)
                                 : reinterpret_cast<const void*>(&place_split_service_kernel<W, R>);
@@ -4141,6 +4182,21 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
     return p;
 }
 
+// u32 copy between device and host-mapped memory (the device path's host
+// walk: runs and feasibility out, assign[] back), through jsp_launch so the
+// call's stop event rides on it like on every other launch.
+__global__ __launch_bounds__(256) void copy_u32_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                       uint32_t n) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = src[i];
+}
+
+hipError_t launch_copy_u32(const uint32_t* src, uint32_t* dst, uint32_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 255) / 256 < 512u ? (n + 255) / 256 : 512u;
+    jsp_launch(copy_u32_kernel, dim3(blocks), dim3(256), 0, s, src, dst, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s) {
@@ -4190,10 +4246,21 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
     return wpt ? (size_t)C * nt * wpt * 8u : 0u;
 }
 
+uint32_t level_walk_grid(uint32_t C, uint32_t nw, uint32_t n_runs, uint32_t J) {
+    uint32_t wpt, nt;
+    level_shape(nw, &wpt, &nt);
+    if (J == 0) return 1u;
+    const uint64_t wb = (uint64_t)C * nw + n_runs;
+    const uint32_t bound = wb < J ? (uint32_t)wb : J;
+    const uint32_t waves = (bound + kExpandRpw - 1) / kExpandRpw;
+    const uint32_t wpb = nt / 64;
+    return 1u + (waves + wpb - 1) / wpb;
+}
+
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
-                               uint32_t epoch, const WaitErr& we) {
+                               uint32_t epoch, const WaitErr& we, const LevelDone& fin) {
     uint32_t wpt, nt;
     level_shape(nw, &wpt, &nt);
     const size_t lds = level_walk_lds_bytes(C, nw);
@@ -4209,9 +4276,10 @@ hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, co
     unsigned long long* rd = J > 0 ? ready : nullptr;
     const uint32_t wpb = nt / 64;  // expander waves per workgroup
     const dim3 g(rd ? 1u + (waves + wpb - 1) / wpb : 1u), b(nt);
+    if (g.x != level_walk_grid(C, nw, n_runs, J)) return hipErrorInvalidValue;  // the completion count's grid
 #define JSP_LEVEL_LAUNCH(W_, N_) \
     jsp_launch((assign_level_kernel<W_, N_>), g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, \
-               stats, rec_count, recs, rd, epoch, bound, rpw, we)
+               stats, rec_count, recs, rd, epoch, bound, rpw, we, fin)
     if (nt == 1024) {
         if (wpt == 1) JSP_LEVEL_LAUNCH(1, 1024);
         else JSP_LEVEL_LAUNCH(2, 1024);

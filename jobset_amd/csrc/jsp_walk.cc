@@ -238,13 +238,42 @@ void HostWalk::take_marks(uint32_t d, uint32_t k) {
 uint32_t HostWalk::place(const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                          int32_t* assign) {
     build_feasibility(slots);
+    return walk(feas_.data(), run_class, run_len, n_runs, assign);
+}
+
+static inline void prefetch_vec(const void* p, size_t bytes) {
+    const char* c = static_cast<const char*>(p);
+    for (size_t i = 0; c && i < bytes; i += 64) __builtin_prefetch(c + i, 0, 3);
+}
+
+void HostWalk::prefetch_state() const {
+    prefetch_vec(taken_.data(), taken_.size() * 8);
+    prefetch_vec(feas_.data(), feas_.size() * 8);
+    prefetch_vec(occ_.data(), occ_.size() * 8);
+    prefetch_vec(sums_.data(), std::min<size_t>(sums_.size() * 8, 65536));
+    prefetch_vec(cw_.data(), cw_.size() * sizeof(ClassWalk));
+    prefetch_vec(level_.data(), level_.size() * 4);
+    prefetch_vec(pods_.data(), pods_.size() * 4);
+    prefetch_vec(woff_.data(), woff_.size() * 4);
+    prefetch_vec(uoff_.data(), uoff_.size() * 4);
+    prefetch_vec(l0_.data(), l0_.size() * 4);
+    prefetch_vec(l1_.data(), l1_.size() * 4);
+    for (uint32_t k = 0; k < K_; ++k) {
+        prefetch_vec(fl_[k].data(), std::min<size_t>(fl_[k].size() * 4, 65536));
+        prefetch_vec(cs_[k].data(), std::min<size_t>(cs_[k].size() * 4, 65536));
+        prefetch_vec(par_[k].data(), std::min<size_t>(par_[k].size() * 4, 65536));
+    }
+}
+
+uint32_t HostWalk::walk(const uint64_t* feas, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                        int32_t* assign) {
     std::fill(taken_.begin(), taken_.end(), 0ull);
     // per class, everything a run needs in one record (cfg5: ~500 runs of one
     // job each, so the per-run set-up is most of the walk)
     cw_.resize(C_);
     for (uint32_t c = 0; c < C_; ++c) {
         const uint32_t k = level_[c];
-        cw_[c] = ClassWalk{feas_.data() + woff_[c], taken_.data() + toff_[k], D_[k], (D_[k] + 63) / 64, k, 0u};
+        cw_[c] = ClassWalk{feas + woff_[c], taken_.data() + toff_[k], D_[k], (D_[k] + 63) / 64, k, 0u};
     }
     uint32_t placed = 0;
     size_t j = 0;

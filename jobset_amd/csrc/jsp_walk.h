@@ -37,6 +37,16 @@ public:
     uint32_t place(const uint64_t* slots, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                    int32_t* assign);
 
+    // The walk alone over feasibility bitmaps the GPU built (feas_kernel's
+    // layout: class c's words at the cumulative offset of (D[level] + 63) / 64
+    // words per class -- the engine's word_off). The device paths' walk for
+    // the shapes whose GPU walk is a one-wave dependent chain.
+    uint32_t walk(const uint64_t* feas, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
+                  int32_t* assign);
+    // start loading the walk's own state (cold host core: the call after a
+    // sleep), while the device works
+    void prefetch_state() const;
+
     // Tile t (= row block t / groups, class group t % groups) has answered:
     // start loading its slot lines into the host cache while the other tiles
     // finish (pinned memory the device just wrote misses every cache level;

@@ -889,3 +889,94 @@ def test_pipe_walk_timeout_is_reported(monkeypatch):
         finally:
             e.close()
     assert errors >= 1
+
+
+def _device_runs(p):
+    import torch
+    from jobset_amd.snapshot import job_runs
+    rc, rl = job_runs(p.job_class)
+    return (torch.from_numpy(rc.astype(np.int32)).cuda(), torch.from_numpy(rl.astype(np.int32)).cuda(),
+            int(rc.shape[0]))
+
+
+@pytest.mark.parametrize("cfg", [3, 5])
+def test_host_walk_device_paths(engine, cfg):
+    """ABI v7 shapes 7 and 8: every shape the GPU level walker does not take
+    walks on the host -- after the GPU's tally and feasibility (shape 7: the
+    launch path with tallies requested, jsp_tally_device + jsp_assign_device,
+    the sharded harness's halves), or over the split tiles' lines of a
+    one-request launch (shape 8: the launch path without tallies and
+    jsp_place_device on a caller's stream, device run list in and device
+    assign[] out through pinned staging). Repeated calls reuse the staging;
+    bit-exact against the oracle each time."""
+    import torch
+    p = synth.CONFIGS[cfg]()
+    engine.load(p)
+    a, cap, occ = O.place_c(p)
+    got = engine.place(p.job_class, want_tally=True)
+    assert_same(got, a, cap, occ)
+    if cfg == 5:
+        assert got.fused == 7
+    # no tallies wanted, service off: the split tiles launched once (shape 8)
+    engine.set_service(False)
+    try:
+        for _ in range(3):
+            got = engine.place(p.job_class)
+            assert got.fused == 8
+            np.testing.assert_array_equal(got.assign, a)
+    finally:
+        engine.set_service(True)
+    rct, rlt, nr = _device_runs(p)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = [torch.full((p.n_jobs,), -7, dtype=torch.int32, device="cuda") for _ in range(3)]
+    for i in range(9):  # back to back, three output buffers in turn
+        engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, outs[i % 3].data_ptr(), s)
+    engine.check()
+    for o in outs:
+        np.testing.assert_array_equal(o.cpu().numpy(), a)
+    L = p.topology.n_leaves
+    capd = torch.zeros((len(p.classes) + 1, L), dtype=torch.int32, device="cuda")
+    out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+    engine.tally_device(capd.data_ptr(), capd[-1].data_ptr(), L, s)
+    engine.assign_device(capd.data_ptr(), capd[-1].data_ptr(), L, rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs,
+                         out.data_ptr(), s)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out.cpu().numpy(), a)
+    np.testing.assert_array_equal(capd[:-1].cpu().numpy().astype(np.uint32), cap)
+    # a patch after a device-path call is ordered after it (the walk's staging included)
+    r = np.array([int(p.nodes.leaf_start[int(a[0])])], dtype=np.uint32) if a[0] >= 0 else np.array([0], np.uint32)
+    t = np.array([p.nodes.taints[r[0]] | (1 << 31)], dtype=np.uint32)
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, out.data_ptr(), s)
+    engine.patch_rows(r, taints=t)
+    p.nodes.taints[r] = t
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, outs[0].data_ptr(), s)
+    engine.check()
+    np.testing.assert_array_equal(out.cpu().numpy(), a)
+    np.testing.assert_array_equal(outs[0].cpu().numpy(), O.place_c(p)[0])
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_host_walk_random_multilevel(engine, seed):
+    """Random 1-4 level snapshots with many short runs (interleaved classes
+    at several levels): the host walk after the GPU feasibility, through the
+    host API and the device path, equals the oracle and the GPU walkers
+    (JSP_FUSED_OFF keeps the walk on the GPU)."""
+    import torch
+    p = synth.random_problem(9100 + seed, max_nodes=30_000, max_levels=4, max_leaves=2000, max_jobs=2500)
+    engine.load(p)
+    a, cap, occ = O.place_c(p)
+    got = engine.place(p.job_class, want_tally=True)
+    assert_same(got, a, cap, occ)
+    rct, rlt, nr = _device_runs(p)
+    out = torch.empty(max(p.n_jobs, 1), dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, out.data_ptr(), s)
+    engine.check()
+    np.testing.assert_array_equal(out[:p.n_jobs].cpu().numpy(), a)
+    engine.set_fused(False)
+    try:
+        got0 = engine.place(p.job_class, want_tally=True)
+        assert got0.fused == 0
+        assert_same(got0, a, cap, occ)
+    finally:
+        engine.set_fused(True)

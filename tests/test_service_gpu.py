@@ -381,7 +381,7 @@ def test_service_that_cannot_fit_falls_back(monkeypatch):
             e.timing(reset=True)
             for _ in range(5):
                 got = e.place(p.job_class)
-                assert got.fused in (1, 2)  # launch shapes only
+                assert got.fused in (1, 2, 7, 8)  # launch shapes only
                 np.testing.assert_array_equal(got.assign, a)
             assert e.timing(reset=True).svc_fallbacks == 1
     finally:

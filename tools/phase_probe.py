@@ -47,8 +47,43 @@ def main():
             pa, pl = np.median(res[:, 0]), np.median(res[:, 1])
             print(f"cfg{cfg} cold gap {gap:g} ms: patch p50 {pa:.2f} place p50 {pl:.2f} "
                   f"(p90 {np.percentile(res[:, 1], 90):.2f}) | {per_call(t, t.host_calls)}", flush=True)
+        if cfg == 2:
+            # raw per-trial (patch, place) at gap 1 ms: default service, parked,
+            # and the gap spun instead of slept (a caller whose core stays awake)
+            out_dir = os.environ.get("PHASE_OUT", ".")
+            for label, parked, spin in (("default", False, False), ("default_spun_gap", False, True),
+                                        ("parked", True, False)):
+                if parked:
+                    eng.set_service(True, parked=True)
+                    call()
+                    call()
+                rows = np.array([(i * 7919) % p.nodes.n_nodes for i in range(300)], dtype=np.uint32)
+                vals = np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)
+                res = call.recovery(300, (idle + 5) * 1e3, 1e3, rows, vals, spin=spin)
+                np.savetxt(os.path.join(out_dir, f"cold_cfg2_{label}.csv"), res, delimiter=",", fmt="%.3f",
+                           header="patch_us,place_us,gap_us")
+                tot = res[:, 0] + res[:, 1]
+                q = lambda a, x: np.percentile(a, x)  # noqa: E731
+                print(f"cfg2 cold gap 1 ms {label}: total p50/p95/p99 {q(tot, 50):.2f}/{q(tot, 95):.2f}/"
+                      f"{q(tot, 99):.2f} | patch {q(res[:, 0], 50):.2f}/{q(res[:, 0], 95):.2f}/{q(res[:, 0], 99):.2f}"
+                      f" | place {q(res[:, 1], 50):.2f}/{q(res[:, 1], 95):.2f}/{q(res[:, 1], 99):.2f}", flush=True)
+                if parked:
+                    eng.service_stop()
+                    eng.set_service(True)
         eng.service_stop()
     p4 = synth.config4()
+    # A/B: the level walk's completion word vs a stream synchronize (test hook)
+    os.environ["JSP_TEST_HOOKS"] = "level_done=0"
+    eng.load(p4)
+    call = eng.host_placer(*job_runs(p4.job_class))
+    for _ in range(5):
+        call()
+    eng.timing(reset=True)
+    tot, med, _ = call.loop(50)
+    t = eng.timing(reset=True)
+    print(f"cfg4 host API, stream synchronize (level_done=0): mean {tot / 50:.2f} p50 {med:.2f} | "
+          f"{per_call(t, t.host_calls)}", flush=True)
+    del os.environ["JSP_TEST_HOOKS"]
     eng.load(p4)
     call = eng.host_placer(*job_runs(p4.job_class))
     for _ in range(5):
@@ -63,6 +98,45 @@ def main():
     dmed, _ = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p4.n_jobs, out.data_ptr(), 50)
     print(f"cfg4 host API: mean {tot / 50:.2f} p50 {med:.2f} | device step {dmed:.2f} | {per_call(t, t.host_calls)}",
           flush=True)
+    # the same device step with assign[] in pinned host memory (what the host API writes)
+    pin = torch.empty(p4.n_jobs, dtype=torch.int32, pin_memory=True)
+    pmed, _ = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p4.n_jobs, pin.data_ptr(), 50)
+    print(f"cfg4 device step with assign[] in pinned host memory: {pmed:.2f} us", flush=True)
+    # device paths of the multi-level shapes (cfg3, cfg5): host walk after the GPU feasibility
+    s = torch.cuda.current_stream().cuda_stream
+    for cfg in (3, 5):
+        p = synth.CONFIGS[cfg]()
+        eng.load(p)
+        shape = eng.place(p.job_class, want_tally=True).fused
+        rc, rl = job_runs(p.job_class)
+        rct = torch.from_numpy(rc.astype(np.int32)).cuda()
+        rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
+        out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+        for _ in range(20):
+            eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(200):
+            eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
+        b.record()
+        b.synchronize()
+        loop = a.elapsed_time(b) * 1e3 / 200
+        dmed, _ = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 100)
+        eng.set_fused(False)
+        fmed, _ = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 100)
+        eng.set_fused(True)
+        eng.timing(reset=True)
+        eng.set_timing(True)
+        for _ in range(100):
+            eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
+        eng.check()
+        t = eng.timing(reset=True)
+        eng.set_timing(False)
+        n = max(t.calls, 1)
+        print(f"cfg{cfg} device path (shape {shape}): event loop {loop:.2f} us/step, dispatch-timed {dmed:.2f} | "
+              f"GPU walk (three launches) {fmed:.2f} | events per call: tally {t.tally_ms * 1e3 / n:.2f} "
+              f"feas {t.feas_ms * 1e3 / n:.2f} walk+copy {t.assign_ms * 1e3 / n:.2f}", flush=True)
 
 
 if __name__ == "__main__":
