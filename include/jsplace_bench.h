@@ -50,6 +50,11 @@ typedef struct jsp_timing {
     uint64_t patches;          /* patch calls with at least one row */
     double patch_us;           /* their host time (a waker-thread restart is not in it) */
     double wake_us;            /* host time (re)starting the service for a coming recovery, wherever it ran */
+    /* the split tiles launched for one request (stats.fused 8, ABI v7), host wall clock */
+    uint64_t oneshot_calls;
+    double oneshot_launch_us;  /* entry to the launch's return */
+    double oneshot_wait_us;    /* ... to every tile's lines seen */
+    double oneshot_walk_us;    /* ... the host walk and (device paths) the assign[] copy launch */
 } jsp_timing;
 
 /* jspb_set_fused modes */

@@ -174,7 +174,7 @@ struct TestHooks {
     uint32_t wait_delay_ns = 0;     // wait_delay_ns=N: the split wait spins N ns after the post (diagnostic)
     bool warm = true;               // warm=0: no call-entry prefetch of the engine's lines (A/B)
     uint32_t micro_spins = 1u << 22;  // micro_spins=N: a resident tile's passes over the microbox (kErrMicro)
-    bool level_done = true;         // level_done=0: the host API syncs the stream after a level walk (A/B)
+    uint32_t waker_poll_us = 200;   // waker_poll_us=N: the armed waker's poll period; 0 = condition variable only
 };
 
 TestHooks read_hooks() {
@@ -206,7 +206,7 @@ TestHooks read_hooks() {
         else if (k == "wait_delay_ns") h.wait_delay_ns = (uint32_t)v;
         else if (k == "warm") h.warm = v != 0;
         else if (k == "micro_spins") h.micro_spins = (uint32_t)v;
-        else if (k == "level_done") h.level_done = v != 0;
+        else if (k == "waker_poll_us") h.waker_poll_us = (uint32_t)v;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -282,13 +282,21 @@ struct jsp_engine {
     unsigned long long patch_target = 0;
     uint32_t patch_seq = 0;
     bool patch_pending = false;
-    // the device paths' host walk (host_walk_impl): feasibility words and,
-    // for device-resident run lists, the runs and assign[] through pinned
-    // staging; ev_hw marks the staged inputs, ev_hw_copy the assign[] copy
-    // that still reads the staging (the next walk waits for it)
-    HostBuf hw_feas, hw_io;
-    hipEvent_t ev_hw = nullptr, ev_hw_copy = nullptr;
-    bool hw_pending = false;
+    // the device paths' host walks (host_walk_impl, split_oneshot): the
+    // feasibility words (and a completion tag) in pinned memory, and a ring
+    // of staging slots for the device paths' run list and assign[]:
+    // a back-to-back call never waits for the previous call's assign[] copy
+    // (it waited ~12 us for that copy's completion report, profiles/r06)
+    struct WalkStage {
+        HostBuf io;
+        hipEvent_t ev = nullptr;
+        bool pending = false;
+    };
+    static constexpr int kWalkStages = 4;
+    WalkStage hw_stage[kWalkStages];
+    uint32_t hw_next = 0;
+    uint32_t hw_tag = 0;
+    HostBuf hw_feas;
     // the split tiles launched for one request (split_oneshot): their answer
     // lines (pinned), the geometry the host walk's tile table was set for,
     // and the request numbers of these launches
@@ -296,8 +304,6 @@ struct jsp_engine {
     unsigned long long os_key = ~0ull;
     uint32_t os_seq = 0;
     DevBuf lvl_ready;                   // the one-launch level walk's published record count
-    DevBuf lvl_fin;                     // its workgroups' completion count (host API completion word)
-    unsigned long long lvl_fin_draws = 0;
     uint32_t lvl_epoch = 0;
     uint32_t err_tag = 0;               // launches that may report a timed-out wait (kernel error words)
     bool patch_svc = false;             // the pending patch goes to the service's dispatcher
@@ -320,9 +326,14 @@ struct jsp_engine {
     std::thread waker;
     std::mutex wake_mu;
     std::condition_variable wake_cv;
-    bool wake_ring = false, wake_quit = false;
-    // a ring is delivered after the caller releases mu (wake_notify)
+    std::atomic<bool> wake_ring{false}, wake_quit{false};
+    // a ring is delivered after the caller releases mu (wake_notify) -- only
+    // while the waker sleeps on wake_cv: while the service is armed it polls
+    // wake_ring instead (waker_poll), so a recovery's first patch call makes
+    // no system call
     std::atomic<bool> wake_notify{false};
+    std::atomic<bool> waker_poll{false};     // the service is armed: the waker polls
+    std::atomic<bool> waker_polling{false};  // the waker is in its polling loop
     jsp::PatchArgs last_patch{};        // its kernel form (the fallback when the service left without it)
     uint32_t err_ack = 0;               // last error word value reported to a caller
     uint32_t* stats_override = nullptr;  // kernels' stats go here when set (host path)
@@ -408,7 +419,7 @@ struct jsp_engine {
         if (waker.joinable()) {  // jsp_engine_destroy joins it; any other delete too
             {
                 std::lock_guard<std::mutex> l(wake_mu);
-                wake_quit = true;
+                wake_quit.store(true);
             }
             wake_cv.notify_one();
             waker.join();
@@ -421,8 +432,8 @@ struct jsp_engine {
                 if (p.b) (void)hipEventDestroy(p.b);
             }
         if (ev_switch) (void)hipEventDestroy(ev_switch);
-        if (ev_hw) (void)hipEventDestroy(ev_hw);
-        if (ev_hw_copy) (void)hipEventDestroy(ev_hw_copy);
+        for (auto& w : hw_stage)
+            if (w.ev) (void)hipEventDestroy(w.ev);
         if (ev_last) (void)hipEventDestroy(ev_last);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.ev_exit) (void)hipEventDestroy(svc.ev_exit);
@@ -517,6 +528,9 @@ int check_launch_error(jsp_engine* e) {
         if (kind == jsp::kErrPipe)
             return set_err(JSP_EHIP, "placement launch %u failed: the pipelined batch walk timed out waiting for an "
                                      "earlier batch; that launch's assign[] is invalid", n);
+        if (kind == jsp::kErrCopyWait)
+            return set_err(JSP_EHIP, "placement launch %u failed: its assign[] copy timed out waiting for the host "
+                                     "walk; that launch's assign[] is invalid", n);
         return set_err(JSP_EHIP, "placement launch %u failed: the compaction look-back timed out (a workgroup "
                                  "never published its count); that launch's assign[] is invalid", n);
     }
@@ -730,12 +744,61 @@ bool level_walk_ok(jsp_engine* e, uint32_t n_runs) {
 // on the host). The GPU computes the feasibility words; the host reads them,
 // walks, and writes assign[].
 constexpr uint32_t kHostWalkMaxJobs = 1u << 16;
+// Below this many jobs the GPU walk (~40 ns per job visit) costs less than the
+// host round trip of the walk on the host (~15 us: the answer out, the copy
+// of assign[] back): cfg3's 64 jobs take 16.6 us on the fused launch against
+// 26.8 us walked on the host; cfg5's 500 take 49.6 against 30.5 (profiles/r06).
+constexpr uint32_t kHostWalkMinJobs = 256;
 
 // (JSP_FUSED_OFF keeps every walk on the GPU: the three-launch shape, which
 // the tests use to exercise the GPU walkers on the shapes AUTO walks here)
 bool host_walk_ok(jsp_engine* e, uint32_t n_runs, uint32_t J) {
-    return e->fused_mode == JSP_FUSED_AUTO && e->C >= 1 && n_runs > 0 && J > 0 && J <= kHostWalkMaxJobs &&
-           !level_walk_ok(e, n_runs);
+    return e->fused_mode == JSP_FUSED_AUTO && e->C >= 1 && n_runs > 0 && J >= kHostWalkMinJobs &&
+           J <= kHostWalkMaxJobs && !level_walk_ok(e, n_runs);
+}
+
+// The next staging slot of the device paths' walks, `bytes` large: its last
+// copy has long finished by the time the ring comes round (a wait only then).
+int walk_stage(jsp_engine* e, size_t bytes, jsp_engine::WalkStage** out) {
+    jsp_engine::WalkStage& w = e->hw_stage[e->hw_next];
+    if (w.pending) {
+        HIP_TRY(hipEventSynchronize(w.ev));
+        w.pending = false;
+    }
+    if (!w.ev) HIP_TRY(hipEventCreateWithFlags(&w.ev, hipEventDisableTiming));
+    HIP_TRY(w.io.reserve(bytes + 64, grave(e)));  // + the host's release word of the copy (copy_wait_kernel)
+    *out = &w;
+    return JSP_OK;
+}
+
+// The assign[] copy of a device-path walk, launched before the host walks:
+// it waits for the host's release of the slot's flag (walk_release), so the
+// copy needs no launch after the walk. Carries the call's stop event.
+int walk_copy_launch(jsp_engine* e, jsp_engine::WalkStage* w, size_t flag_off, const int32_t* staged, int32_t* d_assign,
+                     uint32_t J, hipStream_t s, uint32_t* tag) {
+    uint32_t* flag = reinterpret_cast<uint32_t*>(static_cast<char*>(w->io.p) + flag_off);
+    e->hw_tag = e->hw_tag % 0x7FFFFFFFu + 1u;
+    *tag = e->hw_tag;
+    __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+    HIP_TRY(jsp::launch_copy_wait(flag, *tag, reinterpret_cast<const uint32_t*>(staged),
+                                  reinterpret_cast<uint32_t*>(d_assign), J, e->h_err.as<uint32_t>(),
+                                  next_err_tag(e, jsp::kErrCopyWait), e->hooks.wait_ticks, s));
+    return JSP_OK;
+}
+
+// The host's side of walk_copy_launch: the walk's assign[] is in the staging
+// (ok), or the call fails and nothing is copied (!ok).
+void walk_release(jsp_engine::WalkStage* w, size_t flag_off, uint32_t tag, bool ok) {
+    uint32_t* flag = reinterpret_cast<uint32_t*>(static_cast<char*>(w->io.p) + flag_off);
+    __atomic_store_n(flag, ok ? tag : (tag | 0x80000000u), __ATOMIC_RELEASE);
+}
+
+// After the assign[] copy out of slot w was launched on stream s.
+int walk_stage_done(jsp_engine* e, jsp_engine::WalkStage* w, hipStream_t s) {
+    HIP_TRY(hipEventRecord(w->ev, s));
+    w->pending = true;
+    e->hw_next = (e->hw_next + 1) % jsp_engine::kWalkStages;
+    return JSP_OK;
 }
 
 // Feasibility (feas_kernel into pinned memory, or the folded words copied
@@ -748,18 +811,17 @@ bool host_walk_ok(jsp_engine* e, uint32_t n_runs, uint32_t J) {
 int host_walk_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
                    const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign,
                    hipStream_t s, bool folded, bool host_io) {
-    if (e->hw_pending) {  // the previous walk's assign[] copy still reads the staging
-        HIP_TRY(hipEventSynchronize(e->ev_hw_copy));
-        e->hw_pending = false;
-    }
-    if (!e->ev_hw) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw, hipEventDisableTiming));
-    if (!e->ev_hw_copy) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw_copy, hipEventDisableTiming));
     const uint32_t fw = std::max<uint32_t>(e->feas_words, 1);
-    HIP_TRY(e->hw_feas.reserve((size_t)fw * 8, grave(e)));
-    if (!host_io) HIP_TRY(e->hw_io.reserve((size_t)n_runs * 8 + (size_t)J * 4, grave(e)));
-    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : e->hw_io.as<uint32_t>();
+    HIP_TRY(e->hw_feas.reserve((size_t)fw * 8 + 64, grave(e)));  // + the tag word
+    jsp_engine::WalkStage* st = nullptr;
+    if (!host_io)
+        if (int rc = walk_stage(e, (size_t)n_runs * 8 + (size_t)J * 4, &st)) return rc;
+    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : st->io.as<uint32_t>();
     uint32_t* hrl = host_io ? const_cast<uint32_t*>(run_len) : hrc + n_runs;
-    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(e->hw_io.as<uint32_t>() + 2 * (size_t)n_runs);
+    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(hrc + 2 * (size_t)n_runs);
+    // a caller stream's end-of-call event rides on the last launch only (each
+    // launch that carries one costs its dispatch an event write)
+    const hipEvent_t stop = jsp::take_launch_stop();
     EvPair* p = ev_begin(e, 1, s);
     if (folded)
         HIP_TRY(jsp::launch_copy_u32(e->feas.as<uint32_t>(), e->hw_feas.as<uint32_t>(), 2 * e->feas_words, s));
@@ -771,17 +833,45 @@ int host_walk_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, 
         HIP_TRY(jsp::launch_copy_u32(run_class, hrc, n_runs, s));
         HIP_TRY(jsp::launch_copy_u32(run_len, hrl, n_runs, s));
     }
-    HIP_TRY(hipEventRecord(e->ev_hw, s));
+    // a tag written behind them on the stream tells the host they are done
+    // (an event's completion reaches the host microseconds later)
+    uint32_t* tag = e->hw_feas.as<uint32_t>() + 2 * (size_t)fw;
+    e->hw_tag = e->hw_tag % 0x7FFFFFFFu + 1u;
+    const uint32_t want = e->hw_tag;
+    HIP_TRY(jsp::launch_tag(tag, want, s));
+    // the assign[] copy is queued now (it waits for the walk's release): no
+    // launch between the walk and the copy
+    const size_t flag_off = (size_t)n_runs * 8 + (size_t)J * 4;
+    uint32_t ctag = 0;
+    if (!host_io) {
+        jsp::set_launch_stop(stop);
+        if (int rc = walk_copy_launch(e, st, flag_off, out, assign, J, s, &ctag)) return rc;
+        if (int rc = walk_stage_done(e, st, s)) {
+            walk_release(st, flag_off, ctag, false);
+            return rc;
+        }
+    }
     e->walk.prefetch_state();  // while the device works
     {
         const auto t0 = std::chrono::steady_clock::now();
-        hipError_t q;
-        for (uint64_t spins = 1; (q = hipEventQuery(e->ev_hw)) == hipErrorNotReady; ++spins) {
-            if ((spins & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                return set_err(JSP_EHIP, "host walk: the device feasibility did not complete within 10 s");
+        QueryPacer qp;
+        int rc = JSP_OK;
+        for (uint64_t spins = 1; __atomic_load_n(tag, __ATOMIC_ACQUIRE) != want; ++spins) {
+            if ((spins & 255) == 0 && qp.due()) {
+                const hipError_t q = hipStreamQuery(s);
+                if (q == hipSuccess && __atomic_load_n(tag, __ATOMIC_ACQUIRE) == want) break;
+                if (q == hipSuccess) rc = set_err(JSP_EHIP, "host walk: the feasibility ended without its tag");
+                else if (q != hipErrorNotReady) rc = set_err(JSP_EHIP, "host walk: feasibility failed: %s", hipGetErrorString(q));
+                else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                    rc = set_err(JSP_EHIP, "host walk: the device feasibility did not complete within 10 s");
+                if (rc) break;
+            }
             _mm_pause();
         }
-        if (q != hipSuccess) return set_err(JSP_EHIP, "host walk: feasibility failed: %s", hipGetErrorString(q));
+        if (rc) {
+            if (!host_io) walk_release(st, flag_off, ctag, false);
+            return rc;
+        }
     }
     p = ev_begin(e, 2, s);
     const uint32_t placed = e->walk.walk(e->hw_feas.as<uint64_t>(), hrc, hrl, n_runs, out);
@@ -789,19 +879,15 @@ int host_walk_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, 
         e->stats_override[0] = n_runs;
         e->stats_override[1] = placed;
     }
-    if (!host_io) {
-        HIP_TRY(jsp::launch_copy_u32(reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(assign), J, s));
-        HIP_TRY(hipEventRecord(e->ev_hw_copy, s));
-        e->hw_pending = true;
-    }
+    if (!host_io) walk_release(st, flag_off, ctag, true);
+    else jsp::set_launch_stop(stop);
     ev_end(p, s);
     return JSP_OK;
 }
 
 int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uint32_t ld,
                 const uint32_t* d_run_class, const uint32_t* d_run_len, uint32_t n_runs, uint32_t J,
-                int32_t* d_assign, hipStream_t s, bool folded = false, bool host_io = false,
-                bool signal = false, uint32_t* n_signals = nullptr) {
+                int32_t* d_assign, hipStream_t s, bool folded = false, bool host_io = false) {
     if (host_walk_ok(e, n_runs, J))
         return host_walk_impl(e, d_cap, d_occ, ld, d_run_class, d_run_len, n_runs, J, d_assign, s, folded, host_io);
     EvPair* p = ev_begin(e, 1, s);
@@ -824,24 +910,9 @@ int assign_impl(jsp_engine* e, const uint32_t* d_cap, const uint32_t* d_occ, uin
         }
         e->lvl_epoch = e->lvl_epoch % 0x7FFFFFFFu + 1u;
         we.tag = next_err_tag(e, jsp::kErrExpand);
-        // the host API waits for a completion word the launch's last
-        // workgroup writes, not for the stream (a synchronize reports a
-        // kernel's end microseconds after it)
-        jsp::LevelDone fin{nullptr, nullptr, 0ull, 0u};
-        if (signal && e->hooks.level_done) {
-            if (!e->lvl_fin.p) {
-                HIP_TRY(e->lvl_fin.reserve(64));
-                HIP_TRY(hipMemsetAsync(e->lvl_fin.p, 0, 64, s));
-                e->lvl_fin_draws = 0;
-            }
-            e->lvl_fin_draws += jsp::level_walk_grid(e->C, nw, n_runs, J);
-            fin = jsp::LevelDone{e->h_done.as<uint32_t>(), e->lvl_fin.as<unsigned long long>(), e->lvl_fin_draws,
-                                 e->epoch};
-            if (n_signals) *n_signals = 1;
-        }
         HIP_TRY(jsp::launch_assign_level(e->feas.as<uint64_t>(), e->C, nw, d_run_class, d_run_len, n_runs, J, d_assign,
                                          stats_ptr(e), e->stats.as<uint32_t>() + 3, e->recs.as<jsp::AssignRec>(), s,
-                                         e->lvl_ready.as<unsigned long long>(), e->lvl_epoch, we, fin));
+                                         e->lvl_ready.as<unsigned long long>(), e->lvl_epoch, we));
         ev_end(p, s);
         return JSP_OK;
     }
@@ -932,20 +1003,17 @@ uint32_t next_seq(uint32_t q);
 // memory (the host API's staging); otherwise they are device buffers, staged
 // through pinned memory by copy launches on the same stream.
 bool split_oneshot_ok(jsp_engine* e, uint32_t n_runs, uint32_t J) {
-    return e->fused_mode == JSP_FUSED_AUTO && n_runs > 0 && J > 0 && J <= kHostWalkMaxJobs && split_ok(e);
+    return e->fused_mode == JSP_FUSED_AUTO && n_runs > 0 && J >= kHostWalkMinJobs && J <= kHostWalkMaxJobs &&
+           split_ok(e);
 }
 
 int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs, uint32_t J,
                   int32_t* assign, hipStream_t s, bool host_io) {
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
     const uint32_t g = split_groups(e), cpg = (e->C + g - 1) / g, nb = e->n_blocks, n_tiles = nb * g;
     const uint32_t nw = jsp::split_waves(e->blk_l0, e->blk_l1);
     const size_t sb = (size_t)n_tiles * jsp::split_tile_words(cpg, nw) * 8;
-    if (e->hw_pending) {  // a previous device-path walk's assign[] copy still reads the staging
-        HIP_TRY(hipEventSynchronize(e->ev_hw_copy));
-        e->hw_pending = false;
-    }
-    if (!e->ev_hw) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw, hipEventDisableTiming));
-    if (!e->ev_hw_copy) HIP_TRY(hipEventCreateWithFlags(&e->ev_hw_copy, hipEventDisableTiming));
     if (sb > e->os_split.bytes || !e->os_split.p) {
         HIP_TRY(e->os_split.reserve(sb, grave(e)));
         std::memset(e->os_split.p, 0, e->os_split.bytes);  // tags: request 0 is never posted
@@ -956,14 +1024,12 @@ int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_
         e->os_key = key;
         e->svc.layout_key = ~0ull;  // the service re-lays its own slots (and the walk's tiles) at its next start
     }
-    if (!host_io) HIP_TRY(e->hw_io.reserve((size_t)n_runs * 8 + (size_t)J * 4, grave(e)));
-    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : e->hw_io.as<uint32_t>();
+    jsp_engine::WalkStage* st = nullptr;
+    if (!host_io)
+        if (int rc = walk_stage(e, (size_t)n_runs * 8 + (size_t)J * 4, &st)) return rc;
+    uint32_t* hrc = host_io ? const_cast<uint32_t*>(run_class) : st->io.as<uint32_t>();
     uint32_t* hrl = host_io ? const_cast<uint32_t*>(run_len) : hrc + n_runs;
-    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(e->hw_io.as<uint32_t>() + 2 * (size_t)n_runs);
-    if (!host_io) {
-        HIP_TRY(jsp::launch_copy_u32(run_class, hrc, n_runs, s));
-        HIP_TRY(jsp::launch_copy_u32(run_len, hrl, n_runs, s));
-    }
+    int32_t* out = host_io ? assign : reinterpret_cast<int32_t*>(hrc + 2 * (size_t)n_runs);
     e->os_seq = next_seq(e->os_seq);
     const uint32_t seq = e->os_seq;
     const jsp::TallyArgs ta = tally_args(e, nullptr, nullptr, e->L_total);
@@ -974,49 +1040,88 @@ int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_
     sp.C = e->C;
     sp.out = e->os_split.as<uint64_t>();
     sp.topo = e->topo;
+    if (!host_io) {  // the device-resident run list comes out with tile 0's answer
+        sp.run_class = run_class;
+        sp.run_len = run_len;
+        sp.run_dst = hrc;
+        sp.n_runs = n_runs;
+    }
     jsp::ServiceArgs a{};
     a.oneshot = seq;
+    // the assign[] copy rides in the same launch: one extra workgroup waits
+    // for the walk's release and copies (no launch between walk and copy)
+    const size_t flag_off = (size_t)n_runs * 8 + (size_t)J * 4;
+    uint32_t ctag = 0;
+    if (!host_io) {
+        uint32_t* flag = reinterpret_cast<uint32_t*>(static_cast<char*>(st->io.p) + flag_off);
+        e->hw_tag = e->hw_tag % 0x7FFFFFFFu + 1u;
+        ctag = e->hw_tag;
+        __atomic_store_n(flag, 0u, __ATOMIC_RELEASE);
+        sp.cw_flag = flag;
+        sp.cw_tag = ctag;
+        sp.cw_src = reinterpret_cast<const uint32_t*>(out);
+        sp.cw_dst = reinterpret_cast<uint32_t*>(assign);
+        sp.cw_n = J;
+        sp.cw_err = e->h_err.as<uint32_t>();
+        sp.cw_err_tag = next_err_tag(e, jsp::kErrCopyWait);
+        sp.cw_ticks = e->hooks.wait_ticks;
+    }
     EvPair* p = ev_begin(e, 3, s);
-    HIP_TRY(jsp::launch_split_oneshot(ta, sp, a, s));
+    HIP_TRY(jsp::launch_split_oneshot(ta, sp, a, s));  // carries the call's stop event, if any
     ev_end(p, s);
-    if (!host_io) HIP_TRY(hipEventRecord(e->ev_hw, s));
+    if (!host_io)
+        if (int rc = walk_stage_done(e, st, s)) {
+            walk_release(st, flag_off, ctag, false);
+            return rc;
+        }
+    const auto t1 = clk::now();
     e->walk.prefetch_state();
     // every tile's tagged lines (the answer), bounded; a failed stream is an error
     const uint64_t* slots = e->os_split.as<uint64_t>();
     uint32_t t = 0;
     QueryPacer qp;
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint64_t spins = 1;; ++spins) {
+    int wrc = JSP_OK;
+    for (uint64_t spins = 1; wrc == JSP_OK; ++spins) {
         while (t < n_tiles && e->walk.tile_ready(slots, t, seq)) ++t;
         if (t == n_tiles) break;
         if ((spins & 7) == 1)
             for (uint32_t u = t + 1; u < n_tiles; ++u) e->walk.prefetch_tile(slots, u);
         if ((spins & 255) == 0 && qp.due()) {
+            // (the stream also holds the queued copy, which waits for this
+            // walk: a query reports the split launch's failure, never success)
             const hipError_t q = hipStreamQuery(s);
             if (q == hipSuccess) {
                 while (t < n_tiles && e->walk.tile_ready(slots, t, seq)) ++t;
                 if (t == n_tiles) break;
-                return set_err(JSP_EHIP, "split launch ended without the answer of tile %u", t);
+                wrc = set_err(JSP_EHIP, "split launch ended without the answer of tile %u", t);
+            } else if (q != hipErrorNotReady) {
+                wrc = set_err(JSP_EHIP, "split launch failed: %s", hipGetErrorString(q));
+            } else if (clk::now() - t1 > std::chrono::seconds(10)) {
+                wrc = set_err(JSP_EHIP, "split launch: no answer within 10 s");
             }
-            if (q != hipErrorNotReady) return set_err(JSP_EHIP, "split launch failed: %s", hipGetErrorString(q));
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                return set_err(JSP_EHIP, "split launch: no answer within 10 s");
         }
     }
-    if (!host_io) {  // the staged run list (launched before the tiles: complete by now)
-        const hipError_t q = hipEventSynchronize(e->ev_hw);
-        if (q != hipSuccess) return set_err(JSP_EHIP, "split launch: run staging failed: %s", hipGetErrorString(q));
+    if (wrc) {
+        if (!host_io) walk_release(st, flag_off, ctag, false);
+        return wrc;
     }
+    // (a device-resident run list came out with tile 0's lines: its stores
+    // were released before them)
+    const auto t2 = clk::now();
     const uint32_t placed = e->walk.place(slots, hrc, hrl, n_runs, out);
     if (e->stats_override) {
         e->stats_override[0] = n_runs;
         e->stats_override[1] = placed;
     }
-    if (!host_io) {
-        HIP_TRY(jsp::launch_copy_u32(reinterpret_cast<const uint32_t*>(out), reinterpret_cast<uint32_t*>(assign), J, s));
-        HIP_TRY(hipEventRecord(e->ev_hw_copy, s));
-        e->hw_pending = true;
-    }
+    if (!host_io) walk_release(st, flag_off, ctag, true);
+    // the phases (jspb_get_timing): set-up and launch, the wait for the
+    // tiles' lines, the walk and the copy launch
+    using us = std::chrono::duration<double, std::micro>;
+    const auto t3 = clk::now();
+    e->acc.oneshot_calls += 1;
+    e->acc.oneshot_launch_us += us(t1 - t0).count();
+    e->acc.oneshot_wait_us += us(t2 - t1).count();
+    e->acc.oneshot_walk_us += us(t3 - t2).count();
     return JSP_OK;
 }
 
@@ -1070,7 +1175,7 @@ int place_impl(jsp_engine* e, const uint32_t* d_run_class, const uint32_t* d_run
                                 fold ? e->feas.as<uint64_t>() : nullptr))
             return rc;
         return assign_impl(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total, d_run_class, d_run_len,
-                           n_runs, J, d_assign, s, fold, host_io, signal, n_signals);
+                           n_runs, J, d_assign, s, fold, host_io);
     }
     jsp::TallyArgs a = tally_args(e, e->cap.as<uint32_t>(), e->occ.as<uint32_t>(), e->L_total);
     jsp::FusedArgs f = fused_args(e, a, d_run_class, d_run_len, n_runs, J, d_assign, stats_ptr(e));
@@ -1261,6 +1366,7 @@ void svc_resume(jsp_engine* e) {
 }
 
 void start_waker(jsp_engine* e);
+void notify_waker_poll(jsp_engine* e);
 
 int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
     auto& v = e->svc;
@@ -1893,20 +1999,37 @@ void run_wake(jsp_engine* e) {
     e->acc.wake_us += std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// The waker's loop. While the service is armed (a placement it answered may
+// be followed by a recovery's first patch, hours later) the waker polls the
+// ring every waker_poll_us (200 us: ~5k sleeps a second, ~1 % of one core),
+// so the patch call that rings it only stores a flag -- a futex wake from a
+// core that slept was the default service's cold-recovery tail (patch call
+// p95 9.9 us against 4.7 us with no wake, profiles/r06/g2). Otherwise it
+// sleeps on wake_cv. The ring is consumed whichever way it arrives; a ring
+// the waker has not taken yet is run by the next placement itself (run_wake).
 void waker_main(jsp_engine* e) {
     // Normal priority: at SCHED_IDLE (measured, profiles/r05) a waker
     // preempted while it held the engine lock stalled the next placement by
     // milliseconds (a 5.2 ms cold-recovery p99 on a shared host).
     (void)hipSetDevice(e->device);
+    const auto period = std::chrono::microseconds(e->hooks.waker_poll_us);
     for (;;) {
-        {
-            std::unique_lock<std::mutex> l(e->wake_mu);
-            e->wake_cv.wait(l, [e] { return e->wake_ring || e->wake_quit; });
-            if (e->wake_quit) return;
-            e->wake_ring = false;
+        if (e->wake_quit.load(std::memory_order_acquire)) return;
+        if (e->wake_ring.exchange(false, std::memory_order_acq_rel)) {
+            std::lock_guard<std::mutex> g(e->mu);
+            run_wake(e);
+            continue;
         }
-        std::lock_guard<std::mutex> g(e->mu);
-        run_wake(e);
+        if (period.count() > 0 && e->waker_poll.load(std::memory_order_acquire)) {
+            e->waker_polling.store(true, std::memory_order_release);
+            std::this_thread::sleep_for(period);
+            continue;
+        }
+        e->waker_polling.store(false, std::memory_order_release);
+        std::unique_lock<std::mutex> l(e->wake_mu);
+        e->wake_cv.wait_for(l, std::chrono::milliseconds(50), [e, period] {
+            return e->wake_ring.load() || e->wake_quit.load() || (period.count() > 0 && e->waker_poll.load());
+        });
     }
 }
 
@@ -1927,12 +2050,17 @@ void ring_waker(jsp_engine* e) {
     return;
 #endif
     start_waker(e);
+    e->wake_ring.store(true, std::memory_order_release);
+    if (e->waker_polling.load(std::memory_order_acquire)) return;  // it polls: no notify
     {
-        std::lock_guard<std::mutex> l(e->wake_mu);
-        e->wake_ring = true;
+        std::lock_guard<std::mutex> l(e->wake_mu);  // no lost wake-up between its predicate and its wait
     }
     e->wake_notify.store(true, std::memory_order_relaxed);
 }
+
+// The service became armed: the waker leaves its condition variable for its
+// polling loop (once per arming; a waiter that misses it polls within 50 ms).
+void notify_waker_poll(jsp_engine* e) { e->wake_cv.notify_one(); }
 
 // Deliver a ring (mu not held). Keeping the waker off the ringing thread's
 // CPU (an affinity change when the caller's CPU changed) was measured and
@@ -2355,7 +2483,7 @@ void jsp_engine_destroy(jsp_engine* e) {
     if (e->waker.joinable()) {  // not under mu: the waker may be waiting for it
         {
             std::lock_guard<std::mutex> l(e->wake_mu);
-            e->wake_quit = true;
+            e->wake_quit.store(true);
         }
         e->wake_cv.notify_one();
         e->waker.join();
@@ -3058,6 +3186,10 @@ static int place_call(jsp_engine* e, const uint32_t* run_class, const uint32_t* 
         {
         const auto t2 = std::chrono::steady_clock::now();
         e->svc.armed = true;
+        if (!e->waker_poll.load(std::memory_order_relaxed)) {
+            e->waker_poll.store(true, std::memory_order_release);
+            notify_waker_poll(e);
+        }
         e->last_shape = e->svc.shape == 3 ? 5 : 3;
         if (stats) {
             stats->jobs = J;
@@ -3333,6 +3465,7 @@ int jsp_engine_set_service(jsp_engine* e, int mode) {
     if (mode != e->svc_mode) {  // the running service's shape may change
         e->svc.resume = false;
         e->svc.armed = false;
+        e->waker_poll.store(false, std::memory_order_release);
         if (int rc = svc_stop(e)) return rc;
         e->svc.zero_key = ~0ull;
     }
@@ -3363,6 +3496,7 @@ int jsp_engine_service_stop(jsp_engine* e) {
     std::lock_guard<std::mutex> g(e->mu);
     e->svc.resume = false;
     e->svc.armed = false;  // no patch restarts it until a jsp_place is answered by it again
+    e->waker_poll.store(false, std::memory_order_release);
     e->wake_job = false;   // nor a wake still queued (its patch lands through patch_wait)
     return svc_stop(e);
 }

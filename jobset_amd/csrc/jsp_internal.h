@@ -323,6 +323,24 @@ struct SplitArgs {
     uint32_t nw;    // waves of the largest tile that hold leaves (1..4)
     uint64_t* out;  // host-mapped [n_tiles][split_tile_words(cpg, nw)]
     TopoDev topo;
+    // one-request launch of a device-resident run list (ServiceArgs::oneshot):
+    // tile 0 copies it to run_dst (host-mapped, class then length) before its
+    // lines, so the host has it once every tile's lines are in; null: none
+    const uint32_t* run_class;
+    const uint32_t* run_len;
+    uint32_t* run_dst;
+    uint32_t n_runs;
+    // ... and its assign[] copy in one extra workgroup (null flag: none):
+    // after the host walk's release of cw_tag in cw_flag, cw_n words from the
+    // host-mapped cw_src to the device buffer cw_dst (copy_after_release)
+    const uint32_t* cw_flag;
+    uint32_t cw_tag;
+    const uint32_t* cw_src;
+    uint32_t* cw_dst;
+    uint32_t cw_n;
+    uint32_t* cw_err;
+    uint32_t cw_err_tag;
+    unsigned long long cw_ticks;
 };
 
 constexpr int assign_small_words(int nt) { return 2 * (nt / 64) + 8 + 3 * kMaxClasses + (kMaxClasses + 1) + 4 * 8 + 3 * nt + 64; }
@@ -364,6 +382,9 @@ AssignPlan plan_assign(uint32_t t_words, uint32_t feas_words, uint32_t topo_word
 void set_launch_stop(hipEvent_t ev);
 void set_launch_start(hipEvent_t ev);  // the next launch's start event (then cleared)
 bool launch_stop_used();
+// the stop event set for the coming launches, cleared (a call whose last
+// launch alone should carry it sets it back with set_launch_stop)
+hipEvent_t take_launch_stop();
 // host-link floor probe (instrumentation): four polling waves answer request
 // numbers 1..n of *req in ack[16 w] (pinned host memory)
 hipError_t launch_link_probe(const uint32_t* req, uint32_t* ack, uint32_t n, uint64_t wait_ticks, hipStream_t s);
@@ -406,6 +427,11 @@ size_t fused_lds_bytes(uint32_t t_words, uint32_t feas_words, uint32_t nc, uint3
 // kFusedScrMax (the tail then builds those words one wave per word).
 uint32_t fused_scratch_words(uint32_t K, const uint32_t* D, const uint32_t* class_level, uint32_t C);
 hipError_t launch_copy_u32(const uint32_t* src, uint32_t* dst, uint32_t n, hipStream_t s);
+hipError_t launch_tag(uint32_t* dst, uint32_t v, hipStream_t s);
+hipError_t launch_copy_wait(const uint32_t* flag, uint32_t tag, const uint32_t* src, uint32_t* dst, uint32_t n,
+                            uint32_t* err, uint32_t err_tag, unsigned long long ticks, hipStream_t s);
+// kind of a timed-out device-path copy wait in the engine's error word
+constexpr uint32_t kErrCopyWait = 3u << 30;
 hipError_t launch_feas(const uint32_t* cap, const uint32_t* occ, uint32_t ld, const DevClass* cls, uint32_t C,
                        const uint32_t* word_off, uint32_t total_words, const TopoDev& topo, uint64_t* feas,
                        hipStream_t s);
@@ -427,23 +453,10 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw);
 // count) there once its records are written, and the launch's other
 // workgroups expand them (epoch: new per launch, != 0); an expander that
 // waits longer than we.wait_ticks writes we.tag to the error word.
-// The level walk's completion word for the host API (level_done): the
-// launch's workgroups count themselves in ctr (monotone across launches); the
-// one that makes it `target` writes `tag` to the host-mapped word `done`.
-// done == null: no completion word (the device paths).
-struct LevelDone {
-    uint32_t* done;
-    unsigned long long* ctr;
-    unsigned long long target;
-    uint32_t tag;
-};
-// workgroups of launch_assign_level's launch (the completion count)
-uint32_t level_walk_grid(uint32_t C, uint32_t nw, uint32_t n_runs, uint32_t J);
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
-                               uint32_t epoch, const WaitErr& we,
-                               const LevelDone& fin);
+                               uint32_t epoch, const WaitErr& we);
 hipError_t launch_resolve(const int32_t* rows, const uint32_t* levels, uint32_t n, uint32_t n_rows,
                           const uint32_t* leaf_start, uint32_t n_leaves, uint32_t leaf_base, const TopoDev& topo,
                           int32_t* out, hipStream_t s);

@@ -2171,24 +2171,6 @@ __global__ __launch_bounds__(256) void expand_kernel(const AssignRec* __restrict
 // their jobs' domains as expand_kernel does. A wave that gives up (the
 // walker, dispatched first, never published within wait.wait_ticks) writes
 // the launch's tag to the error word: the call fails, never a stale assign[].
-// The host API's completion word for the one-launch level walk (fin.done !=
-// null): every workgroup's assign[] stores go out (system-scope release),
-// then it counts itself in; the last one -- the launch's fin.target-th since
-// the engine was created -- writes fin.tag to the host word the caller spins
-// on, instead of a stream synchronize after the kernel's end.
-__device__ __forceinline__ void level_done(const LevelDone& fin) {
-    if (fin.done == nullptr) return;
-    __threadfence_system();
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const unsigned long long old = __hip_atomic_fetch_add(fin.ctr, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (old + 1ull == fin.target) {
-            __threadfence_system();
-            __hip_atomic_store(fin.done, fin.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
 __device__ void level_expand(const AssignRec* recs, const unsigned long long* ready, uint32_t epoch, uint32_t bound,
                              uint32_t rpw, int32_t* assign, const WaitErr& wait) {
     const uint32_t lane = threadIdx.x & 63;
@@ -2256,14 +2238,13 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
                                                                      AssignRec* __restrict__ recs,
                                                                      unsigned long long* __restrict__ ready,
                                                                      uint32_t epoch, uint32_t bound, uint32_t rpw,
-                                                                     WaitErr wait, LevelDone fin) {
+                                                                     WaitErr wait) {
     // Expansion in the same launch (ready != null): workgroups 1.. wait for
     // the walker (workgroup 0, dispatched first, never waits for them) to
     // publish its record count, then expand the records as expand_kernel
     // does -- no second launch and no launch gap between walk and expansion.
     if (ready != nullptr && blockIdx.x > 0) {
         level_expand(recs, ready, epoch, bound, rpw, assign, wait);
-        level_done(fin);
         return;
     }
     extern __shared__ __attribute__((aligned(16))) uint64_t s_f[];  // [C][WPT][NT]
@@ -2390,7 +2371,6 @@ __global__ __launch_bounds__(NT) void assign_level_kernel(const uint64_t* __rest
         for (uint32_t j = a1 + tid; j < j1; j += (uint32_t)NT) assign[j] = -1;
     }
     JSP_STAMP(4050u, 7);
-    level_done(fin);
 }
 
 // ---- fused tail: leaf pass of the feasibility build (see place_fused_kernel)
@@ -3651,6 +3631,45 @@ __device__ __forceinline__ uint32_t leaf_ancestor(uint32_t leaf, uint32_t level,
     return d;
 }
 
+// The device paths' assign[] copy, launched before the host walks (so no
+// launch sits between the walk and the copy): each workgroup waits (bounded)
+// for the host's release of `tag` in the host-mapped word `flag`, then copies
+// n words from the host-mapped staging into the device buffer. The host
+// writes tag | 0x80000000 when it cannot deliver (the call fails): nothing is
+// copied. A wait that times out writes err_tag to err (the engine reports it).
+__device__ __forceinline__ void copy_after_release(const uint32_t* flag, uint32_t tag, const uint32_t* __restrict__ src,
+                                                   uint32_t* __restrict__ dst, uint32_t n, uint32_t* err,
+                                                   uint32_t err_tag, unsigned long long ticks, uint32_t wg,
+                                                   uint32_t n_wg) {
+    __shared__ uint32_t s_go;
+    if (threadIdx.x == 0) {
+        const uint64_t t0 = wall_clock64();
+        uint32_t f = 0;
+        while (true) {
+            f = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+            if ((f & 0x7FFFFFFFu) == tag) break;
+            if (wall_clock64() - t0 > ticks) {
+                if (err != nullptr) __hip_atomic_store(err, err_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                f = 0x80000000u;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        s_go = (f & 0x80000000u) ? 0u : 1u;
+    }
+    __syncthreads();
+    if (s_go == 0u) return;
+    for (uint32_t i = wg * blockDim.x + threadIdx.x; i < n; i += n_wg * blockDim.x)
+        dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(256) void copy_wait_kernel(const uint32_t* flag, uint32_t tag,
+                                                        const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                        uint32_t n, uint32_t* err, uint32_t err_tag,
+                                                        unsigned long long ticks) {
+    copy_after_release(flag, tag, src, dst, n, err, err_tag, ticks, blockIdx.x, gridDim.x);
+}
+
 __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
                                            uint32_t seq, uint32_t* lds, uint32_t* s_x) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -3717,6 +3736,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     const uint32_t tile = blockIdx.x;
     const uint32_t n_tiles = a.n_blocks * sp.groups;
     uint32_t* s_x = lds + tally_lds_words((int)sp.cpg, (int)sp.cpg + 1, (int)a.la);  // [0] seq [4..16) scan [16..) prefixes
+    if (v.oneshot != 0u && tile == n_tiles) {
+        // the one-request launch's assign[] copy: waits for the host walk's
+        // release, then copies (split_oneshot; no launch after the walk)
+        copy_after_release(sp.cw_flag, sp.cw_tag, sp.cw_src, sp.cw_dst, sp.cw_n, sp.cw_err, sp.cw_err_tag, sp.cw_ticks, 0u,
+                           1u);
+        return;
+    }
     if (tile == n_tiles) {
         service_dispatch(v, a, s_x);
         return;
@@ -3733,6 +3759,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         // one launch, one request (the launch path and the device paths of the
         // split shape, ABI v7): no dispatcher, no bell, rows from memory; the
         // tile answers request v.oneshot through its tagged lines and leaves
+        if (tile == 0 && sp.run_dst != nullptr) {
+            for (uint32_t i = threadIdx.x; i < sp.n_runs; i += kTallyThreads) {
+                sp.run_dst[i] = sp.run_class[i];
+                sp.run_dst[sp.n_runs + i] = sp.run_len[i];
+            }
+            __threadfence_system();  // before this tile's lines, which the host waits for
+        }
         tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, nullptr, false);
         split_emit(ag, sp, bt, out, v.oneshot, lds, s_x);
         return;
@@ -3972,6 +4005,11 @@ void set_launch_stop(hipEvent_t ev) {
     t_stop_used = false;
 }
 void set_launch_start(hipEvent_t ev) { t_start = ev; }
+hipEvent_t take_launch_stop() {
+    hipEvent_t ev = t_stop;
+    t_stop = nullptr;
+    return ev;
+}
 bool launch_stop_used() { return t_stop_used; }
 
 template <typename F, typename... Args>
@@ -4110,7 +4148,8 @@ hipError_t launch_split_service(const TallyArgs& a, const SplitArgs& sp, const S
 template <int W, int R>
 static hipError_t launch_split_oneshot_wr(const TallyArgs& a, const SplitArgs& sp, const ServiceArgs& v,
                                           hipStream_t s) {
-    jsp_launch((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups), dim3(kTallyThreads),
+    jsp_launch((place_split_service_kernel<W, R>), dim3(a.n_blocks * sp.groups + (sp.cw_flag != nullptr ? 1u : 0u)),
+               dim3(kTallyThreads),
                split_service_lds_bytes(sp.cpg, a.la, a.W, a.R, false), s, a, sp, v);
     return hipGetLastError();
 }
@@ -4190,6 +4229,25 @@ __global__ __launch_bounds__(256) void copy_u32_kernel(const uint32_t* __restric
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) dst[i] = src[i];
 }
 
+hipError_t launch_copy_wait(const uint32_t* flag, uint32_t tag, const uint32_t* src, uint32_t* dst, uint32_t n,
+                            uint32_t* err, uint32_t err_tag, unsigned long long ticks, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    const uint32_t blocks = (n + 255) / 256 < 64u ? (n + 255) / 256 : 64u;
+    jsp_launch(copy_wait_kernel, dim3(blocks), dim3(256), 0, s, flag, tag, src, dst, n, err, err_tag, ticks);
+    return hipGetLastError();
+}
+
+// one word to host-mapped memory, system scope: a completion tag behind the
+// stream's earlier kernels
+__global__ void tag_kernel(uint32_t* __restrict__ dst, uint32_t v) {
+    if (threadIdx.x == 0) __hip_atomic_store(dst, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_tag(uint32_t* dst, uint32_t v, hipStream_t s) {
+    jsp_launch(tag_kernel, dim3(1), dim3(64), 0, s, dst, v);
+    return hipGetLastError();
+}
+
 hipError_t launch_copy_u32(const uint32_t* src, uint32_t* dst, uint32_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     const uint32_t blocks = (n + 255) / 256 < 512u ? (n + 255) / 256 : 512u;
@@ -4246,21 +4304,10 @@ size_t level_walk_lds_bytes(uint32_t C, uint32_t nw) {
     return wpt ? (size_t)C * nt * wpt * 8u : 0u;
 }
 
-uint32_t level_walk_grid(uint32_t C, uint32_t nw, uint32_t n_runs, uint32_t J) {
-    uint32_t wpt, nt;
-    level_shape(nw, &wpt, &nt);
-    if (J == 0) return 1u;
-    const uint64_t wb = (uint64_t)C * nw + n_runs;
-    const uint32_t bound = wb < J ? (uint32_t)wb : J;
-    const uint32_t waves = (bound + kExpandRpw - 1) / kExpandRpw;
-    const uint32_t wpb = nt / 64;
-    return 1u + (waves + wpb - 1) / wpb;
-}
-
 hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, const uint32_t* run_class,
                                const uint32_t* run_len, uint32_t n_runs, uint32_t J, int32_t* assign, uint32_t* stats,
                                uint32_t* rec_count, AssignRec* recs, hipStream_t s, unsigned long long* ready,
-                               uint32_t epoch, const WaitErr& we, const LevelDone& fin) {
+                               uint32_t epoch, const WaitErr& we) {
     uint32_t wpt, nt;
     level_shape(nw, &wpt, &nt);
     const size_t lds = level_walk_lds_bytes(C, nw);
@@ -4276,10 +4323,9 @@ hipError_t launch_assign_level(const uint64_t* feas, uint32_t C, uint32_t nw, co
     unsigned long long* rd = J > 0 ? ready : nullptr;
     const uint32_t wpb = nt / 64;  // expander waves per workgroup
     const dim3 g(rd ? 1u + (waves + wpb - 1) / wpb : 1u), b(nt);
-    if (g.x != level_walk_grid(C, nw, n_runs, J)) return hipErrorInvalidValue;  // the completion count's grid
 #define JSP_LEVEL_LAUNCH(W_, N_) \
     jsp_launch((assign_level_kernel<W_, N_>), g, b, (uint32_t)lds, s, feas, C, nw, run_class, run_len, n_runs, assign, \
-               stats, rec_count, recs, rd, epoch, bound, rpw, we, fin)
+               stats, rec_count, recs, rd, epoch, bound, rpw, we)
     if (nt == 1024) {
         if (wpt == 1) JSP_LEVEL_LAUNCH(1, 1024);
         else JSP_LEVEL_LAUNCH(2, 1024);

@@ -44,7 +44,8 @@ def stub_detail(b):
                             "bit-exact with the engine)"},
           "warm_trials": _pc(200), "patched": {"mean_us": X, "p50_us": X, "p99_us": X}, "cpu_patched_best_us": X,
           "link_floor_p50_us": X, "service_request_us_device": X}
-    cfg = {"nodes": 40960, "jobs": 64, "placed": 64, "kernel_us": X, "kernel_frac": X, "service_frac": X,
+    cfg = {"nodes": 40960, "jobs": 64, "placed": 64, "kernel_us": X, "kernel_loop_us": X, "kernel_frac": X,
+           "service_frac": X,
            "host_api_resident": _pc(200), "cpu_us": {"1t": X, "16t": X},
            "cold_vs_cpu": {g: _vs(100) for g in gaps}}
     c4 = {k: X for k in ("placements_per_s", "host_api_us", "kernel_only_us", "kernel_only_placements_per_s",

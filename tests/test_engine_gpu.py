@@ -922,7 +922,8 @@ def test_host_walk_device_paths(engine, cfg):
     try:
         for _ in range(3):
             got = engine.place(p.job_class)
-            assert got.fused == 8
+            # (below 256 jobs the GPU walk costs less: cfg3's 64 stay on the fused launch)
+            assert got.fused == (8 if p.n_jobs >= 256 else 1)
             np.testing.assert_array_equal(got.assign, a)
     finally:
         engine.set_service(True)
@@ -964,6 +965,12 @@ def test_host_walk_random_multilevel(engine, seed):
     import torch
     p = synth.random_problem(9100 + seed, max_nodes=30_000, max_levels=4, max_leaves=2000, max_jobs=2500)
     engine.load(p)
+    engine.set_service(False)  # the launch path: shape 8 (>= 256 jobs, split geometry), 7, 1 or 0
+    try:
+        got = engine.place(p.job_class)
+        np.testing.assert_array_equal(got.assign, O.place_c(p)[0])
+    finally:
+        engine.set_service(True)
     a, cap, occ = O.place_c(p)
     got = engine.place(p.job_class, want_tally=True)
     assert_same(got, a, cap, occ)
@@ -980,3 +987,29 @@ def test_host_walk_random_multilevel(engine, seed):
         assert_same(got0, a, cap, occ)
     finally:
         engine.set_fused(True)
+
+
+def test_walk_copy_timeout_is_reported(engine, monkeypatch):
+    """The device paths' assign[] copy is queued before the host walks and
+    waits (bounded) for the walk's release; with the hook wait_us=0 every
+    such wait gives up: the device path reports JSP_EHIP (engine check or the
+    next call), never a silent stale assign[]. Without the hook, bit-exact."""
+    import torch
+    from jobset_amd.native import JSP_EHIP
+    p = synth.config5()
+    monkeypatch.setenv("JSP_TEST_HOOKS", "wait_us=0")
+    engine.load(p)
+    rct, rlt, nr = _device_runs(p)
+    out = torch.empty(p.n_jobs, dtype=torch.int32, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    with pytest.raises(JspError) as ei:
+        for _ in range(5):
+            engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, out.data_ptr(), s)
+            engine.check()
+    assert ei.value.code == JSP_EHIP and "copy timed out" in str(ei.value)
+    monkeypatch.delenv("JSP_TEST_HOOKS")
+    engine.check()
+    engine.load(p)
+    engine.place_device(rct.data_ptr(), rlt.data_ptr(), nr, p.n_jobs, out.data_ptr(), s)
+    engine.check()
+    np.testing.assert_array_equal(out.cpu().numpy(), O.place_c(p)[0])

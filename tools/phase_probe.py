@@ -51,8 +51,30 @@ def main():
             # raw per-trial (patch, place) at gap 1 ms: default service, parked,
             # and the gap spun instead of slept (a caller whose core stays awake)
             out_dir = os.environ.get("PHASE_OUT", ".")
-            for label, parked, spin in (("default", False, False), ("default_spun_gap", False, True),
+            for label, parked, spin in (("default", False, False), ("default_condvar_waker", False, False),
                                         ("parked", True, False)):
+                if label == "default_condvar_waker":  # A/B: the waker on its condition variable only
+                    os.environ["JSP_TEST_HOOKS"] = "waker_poll_us=0"
+                    e2 = Engine(0)
+                    del os.environ["JSP_TEST_HOOKS"]
+                    e2.load(p)
+                    c2 = e2.host_placer(*job_runs(p.job_class))
+                    for _ in range(5):
+                        c2()
+                    rows = np.array([(i * 7919) % p.nodes.n_nodes for i in range(300)], dtype=np.uint32)
+                    vals = np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)
+                    res = c2.recovery(300, (idle + 5) * 1e3, 1e3, rows, vals)
+                    e2.service_stop()
+                    e2.close()
+                    tot = res[:, 0] + res[:, 1]
+                    q = lambda a, x: np.percentile(a, x)  # noqa: E731
+                    print(f"cfg2 cold gap 1 ms {label}: total p50/p95/p99 {q(tot, 50):.2f}/{q(tot, 95):.2f}/"
+                          f"{q(tot, 99):.2f} | patch {q(res[:, 0], 50):.2f}/{q(res[:, 0], 95):.2f}/"
+                          f"{q(res[:, 0], 99):.2f} | place {q(res[:, 1], 50):.2f}/{q(res[:, 1], 95):.2f}/"
+                          f"{q(res[:, 1], 99):.2f}", flush=True)
+                    np.savetxt(os.path.join(out_dir, f"cold_cfg2_{label}.csv"), res, delimiter=",", fmt="%.3f",
+                               header="patch_us,place_us,gap_us")
+                    continue
                 if parked:
                     eng.set_service(True, parked=True)
                     call()
@@ -72,18 +94,6 @@ def main():
                     eng.set_service(True)
         eng.service_stop()
     p4 = synth.config4()
-    # A/B: the level walk's completion word vs a stream synchronize (test hook)
-    os.environ["JSP_TEST_HOOKS"] = "level_done=0"
-    eng.load(p4)
-    call = eng.host_placer(*job_runs(p4.job_class))
-    for _ in range(5):
-        call()
-    eng.timing(reset=True)
-    tot, med, _ = call.loop(50)
-    t = eng.timing(reset=True)
-    print(f"cfg4 host API, stream synchronize (level_done=0): mean {tot / 50:.2f} p50 {med:.2f} | "
-          f"{per_call(t, t.host_calls)}", flush=True)
-    del os.environ["JSP_TEST_HOOKS"]
     eng.load(p4)
     call = eng.host_placer(*job_runs(p4.job_class))
     for _ in range(5):
@@ -107,7 +117,9 @@ def main():
     for cfg in (3, 5):
         p = synth.CONFIGS[cfg]()
         eng.load(p)
-        shape = eng.place(p.job_class, want_tally=True).fused
+        eng.set_service(False)
+        shape = eng.place(p.job_class).fused
+        eng.set_service(True)
         rc, rl = job_runs(p.job_class)
         rct = torch.from_numpy(rc.astype(np.int32)).cuda()
         rlt = torch.from_numpy(rl.astype(np.int32)).cuda()
@@ -127,16 +139,17 @@ def main():
         fmed, _ = eng.place_device_timed(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), 100)
         eng.set_fused(True)
         eng.timing(reset=True)
-        eng.set_timing(True)
         for _ in range(100):
             eng.place_device(rct.data_ptr(), rlt.data_ptr(), rc.shape[0], p.n_jobs, out.data_ptr(), s)
         eng.check()
         t = eng.timing(reset=True)
-        eng.set_timing(False)
         n = max(t.calls, 1)
+        o = max(t.oneshot_calls, 1)
         print(f"cfg{cfg} device path (shape {shape}): event loop {loop:.2f} us/step, dispatch-timed {dmed:.2f} | "
               f"GPU walk (three launches) {fmed:.2f} | events per call: tally {t.tally_ms * 1e3 / n:.2f} "
-              f"feas {t.feas_ms * 1e3 / n:.2f} walk+copy {t.assign_ms * 1e3 / n:.2f}", flush=True)
+              f"feas {t.feas_ms * 1e3 / n:.2f} walk+copy {t.assign_ms * 1e3 / n:.2f} | split launch host phases: "
+              f"launch {t.oneshot_launch_us / o:.2f} wait {t.oneshot_wait_us / o:.2f} walk+copy "
+              f"{t.oneshot_walk_us / o:.2f} (calls {t.oneshot_calls})", flush=True)
 
 
 if __name__ == "__main__":
