@@ -43,7 +43,13 @@
  *
  * Stream ordering: uploads, patches, jsp_place and the webhook batches run on
  * the engine's own stream and return after it has finished; the *_device
- * entry points enqueue on the caller's stream and return at once. Every call
+ * entry points enqueue on the caller's stream and return at once -- except
+ * where the walk runs on the host (ABI v7, jsp_stats.fused 7 and 8: the
+ * multi-class / multi-level shapes the GPU level walker does not take, 256 to
+ * 65536 jobs): there the call waits for its own kernels' answer (the stream's
+ * earlier work first), walks, and returns with the assign[] copy enqueued on
+ * the stream behind them (it waits for the walk's release, so no launch
+ * separates the walk from the copy). Every call
  * is ordered after all work the engine enqueued earlier, on whatever stream
  * (the first call on a different stream waits on an event of the previous
  * one), so a patch after a jsp_place_device never races its tally.

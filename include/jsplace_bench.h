@@ -55,6 +55,7 @@ typedef struct jsp_timing {
     double oneshot_launch_us;  /* entry to the launch's return */
     double oneshot_wait_us;    /* ... to every tile's lines seen */
     double oneshot_walk_us;    /* ... the host walk and (device paths) the assign[] copy launch */
+    double oneshot_stage_us;   /* the part of oneshot_launch_us before the launch call (staging slot, set-up) */
 } jsp_timing;
 
 /* jspb_set_fused modes */

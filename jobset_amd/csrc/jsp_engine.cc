@@ -357,6 +357,11 @@ struct jsp_engine {
     bool last_foreign = false;          // the last call enqueued on a caller's stream
     hipEvent_t ev_switch = nullptr;     // recorded on the engine stream
     hipEvent_t ev_last = nullptr;       // recorded on the last caller stream, at the end of its call
+    // ev_last alternates between two events: a launch that carries an event
+    // still pending from the previous call (its kernel running) waits in the
+    // runtime for it -- ~7 us of host time per device-path call (profiles/r06)
+    hipEvent_t ev_ring[2] = {nullptr, nullptr};
+    int ev_i = 0;
 
     // resident placement service: the compaction shape kept on the GPU
     // between host-API placements (place_service_kernel), fed by a host-mapped
@@ -434,7 +439,8 @@ struct jsp_engine {
         if (ev_switch) (void)hipEventDestroy(ev_switch);
         for (auto& w : hw_stage)
             if (w.ev) (void)hipEventDestroy(w.ev);
-        if (ev_last) (void)hipEventDestroy(ev_last);
+        for (hipEvent_t x : ev_ring)
+            if (x) (void)hipEventDestroy(x);
         if (stream) (void)hipStreamDestroy(stream);
         if (svc.ev_exit) (void)hipEventDestroy(svc.ev_exit);
         if (svc.stream) (void)hipStreamDestroy(svc.stream);
@@ -482,7 +488,7 @@ int enter_stream(jsp_engine* e, hipStream_t s) {
     if (int rc = patch_fence(e)) return rc;
     if (e->have_last && e->last_stream != s)
         if (int rc = wait_prior(e, s)) return rc;
-    if (s != e->stream) jsp::set_launch_stop(e->ev_last);
+    if (s != e->stream) jsp::set_launch_stop(e->ev_ring[e->ev_i ^ 1]);  // this call's end (ev_last after it)
     return JSP_OK;
 }
 
@@ -496,7 +502,11 @@ int leave_stream(jsp_engine* e, hipStream_t s) {
     e->have_last = true;
     e->last_foreign = s != e->stream;
     e->foreign_pending = e->last_foreign;
-    if (e->last_foreign && !launched) HIP_TRY(hipEventRecord(e->ev_last, s));
+    if (e->last_foreign) {
+        e->ev_i ^= 1;
+        e->ev_last = e->ev_ring[e->ev_i];
+        if (!launched) HIP_TRY(hipEventRecord(e->ev_last, s));
+    }
     return JSP_OK;
 }
 
@@ -1067,7 +1077,11 @@ int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_
         sp.cw_ticks = e->hooks.wait_ticks;
     }
     EvPair* p = ev_begin(e, 3, s);
+    const auto tl = clk::now();
+    // one launch (the copy as a kernel of its own behind the tiles measured the
+    // same: 20.9 against 21.7 us per back-to-back call, profiles/r06/g2)
     HIP_TRY(jsp::launch_split_oneshot(ta, sp, a, s));  // carries the call's stop event, if any
+    e->acc.oneshot_stage_us += std::chrono::duration<double, std::micro>(tl - t0).count();
     ev_end(p, s);
     if (!host_io)
         if (int rc = walk_stage_done(e, st, s)) {
@@ -2423,7 +2437,8 @@ int jsp_engine_create(int device_id, jsp_engine** out) {
         delete e;
         return set_err(JSP_EHIP, "hipStreamCreate: %s", hipGetErrorString(err));
     }
-    if (hipEventCreateWithFlags(&e->ev_last, hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
+    if (hipEventCreateWithFlags(&e->ev_ring[0], hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess ||
+        hipEventCreateWithFlags(&e->ev_ring[1], hipEventDisableTiming | hipEventReleaseToDevice) != hipSuccess) {
         delete e;
         return set_err(JSP_EHIP, "hipEventCreate failed");
     }

@@ -52,7 +52,8 @@ class JspTiming(ctypes.Structure):
                 ("svc_ready_us", ctypes.c_double), ("svc_pre_us", ctypes.c_double),
                 ("svc_answer_us", ctypes.c_double), ("svc_first_us", ctypes.c_double), ("patches", ctypes.c_uint64), ("patch_us", ctypes.c_double),
                 ("wake_us", ctypes.c_double), ("oneshot_calls", ctypes.c_uint64), ("oneshot_launch_us", ctypes.c_double),
-                ("oneshot_wait_us", ctypes.c_double), ("oneshot_walk_us", ctypes.c_double)]
+                ("oneshot_wait_us", ctypes.c_double), ("oneshot_walk_us", ctypes.c_double),
+                ("oneshot_stage_us", ctypes.c_double)]
 
 
 HIST_BUCKETS = 32

@@ -148,8 +148,9 @@ def main():
         print(f"cfg{cfg} device path (shape {shape}): event loop {loop:.2f} us/step, dispatch-timed {dmed:.2f} | "
               f"GPU walk (three launches) {fmed:.2f} | events per call: tally {t.tally_ms * 1e3 / n:.2f} "
               f"feas {t.feas_ms * 1e3 / n:.2f} walk+copy {t.assign_ms * 1e3 / n:.2f} | split launch host phases: "
-              f"launch {t.oneshot_launch_us / o:.2f} wait {t.oneshot_wait_us / o:.2f} walk+copy "
-              f"{t.oneshot_walk_us / o:.2f} (calls {t.oneshot_calls})", flush=True)
+              f"launch {t.oneshot_launch_us / o:.2f} (stage {t.oneshot_stage_us / o:.2f}) wait "
+              f"{t.oneshot_wait_us / o:.2f} walk+copy {t.oneshot_walk_us / o:.2f} (calls {t.oneshot_calls})",
+              flush=True)
 
 
 if __name__ == "__main__":
