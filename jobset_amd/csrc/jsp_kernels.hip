@@ -530,14 +530,13 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         const auto& fr = cur.fr;
         const auto& ex = cur.ex;
 
-        // ---- row pass: per value, evaluate 4 rows, scan, store row prefixes
-        for (int c = 0; c < nv; ++c) {
-            uint32_t v[4];
+        // ---- row pass: per value, evaluate 4 rows, scan, store row prefixes.
+        // Two values per step: their evaluations and their DPP scans are
+        // independent, so the two dependent chains interleave (cfg3's split
+        // tiles: 2 classes + occupancy, row pass 1.6 us one value at a time).
+        auto eval = [&](int c, uint32_t (&v)[4]) {
             if (c < nc) {
                 const ClassRegs<W, R> k = class_regs<W, R>(s_cls[c]);
-#ifdef JSP_AB_FINESTAMP
-                if (c == 0) svc_stamp(clk, 3);
-#endif
                 uint32_t cap[4];
                 row_caps<W, R>(k, fr, cap);
 #pragma unroll
@@ -551,14 +550,30 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
 #pragma unroll
                 for (int i = 0; i < 4; ++i) v[i] = (valid[i] && ex[i] != -1) ? 1u : 0u;
             }
+        };
+#ifdef JSP_AB_FINESTAMP
+        svc_stamp(clk, 3);
+#endif
+        for (int c = 0; c < nv; c += 2) {
+            const bool two = c + 1 < nv;  // workgroup-uniform
+            uint32_t v[4], u[4] = {0u, 0u, 0u, 0u};
+            eval(c, v);
+            if (two) eval(c + 1, u);
             const uint32_t p0 = v[0], p1 = p0 + v[1], p2 = p1 + v[2], p3 = p2 + v[3];
-            const uint32_t incl = wave_incl_scan(p3, lane);
+            const uint32_t q0 = u[0], q1 = q0 + u[1], q2 = q1 + u[2], q3 = q2 + u[3];
+            const uint32_t incl = wave_incl_scan(p3, lane), incl2 = wave_incl_scan(q3, lane);
 #ifdef JSP_AB_FINESTAMP
             if (c == 0 && incl != 0xFFFFFFFFu) svc_stamp(clk, 4);
 #endif
             const uint32_t wex = incl - p3;
             reinterpret_cast<uint4*>(s_pre + c * kChunkRows)[tid] = make_uint4(wex + p0, wex + p1, wex + p2, incl);
             if (lane == 63) s_wsum[c * kTallyWaves + wid] = incl;
+            if (two) {
+                const uint32_t wex2 = incl2 - q3;
+                reinterpret_cast<uint4*>(s_pre + (c + 1) * kChunkRows)[tid] =
+                    make_uint4(wex2 + q0, wex2 + q1, wex2 + q2, incl2);
+                if (lane == 63) s_wsum[(c + 1) * kTallyWaves + wid] = incl2;
+            }
         }
         __syncthreads();
         JSP_STAMP(blk, 6);
@@ -568,8 +583,13 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         // Chunk prefix at row x = wave-local prefix + the totals of the waves
         // before x's wave; every LDS read of a value is independent (one
         // round trip), the wave offsets come from one 16-B read.
+        // One thread per (value, leaf): a tile of few large leaves (cfg3: 2
+        // leaves, 3 values) reads its prefixes in one LDS round trip instead
+        // of a chain of nv per leaf thread (leaf pass 0.52 us on cfg3's split
+        // tiles, profiles/r06/probes). Each (value, leaf) sum has one owner.
         static_assert(kTallyWaves == 4, "wave-offset select assumes 4 waves");
-        for (uint32_t li = tid; li < nl; li += kTallyThreads) {
+        for (uint32_t q = tid; q < nl * (uint32_t)nv; q += kTallyThreads) {
+            const uint32_t c = q / nl, li = q - c * nl;
             const uint32_t s = s_ls[li], e = s_ls[li + 1];
             const uint32_t lo = s > base ? s : base;
             const uint32_t hi = e < base + kChunkRows ? e : base + kChunkRows;
@@ -578,14 +598,14 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
             const uint32_t xb = lo > base ? lo - 1 - base : 0u;      // row before the first (if any)
             const bool has_lo = lo > base;
             const uint32_t wh = xh >> 8, wb = xb >> 8;               // their waves (256 rows per wave)
-            for (int c = 0; c < nv; ++c) {
-                const uint32_t* pre = s_pre + c * kChunkRows;
-                const uint4 ws = reinterpret_cast<const uint4*>(s_wsum)[c];
-                const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
-                const uint32_t hi_p = pre[xh] + (wh == 0 ? 0u : wh == 1 ? e1 : wh == 2 ? e2 : e3);
-                const uint32_t lo_p = has_lo ? pre[xb] + (wb == 0 ? 0u : wb == 1 ? e1 : wb == 2 ? e2 : e3) : 0u;
-                s_acc[c * la + li] += hi_p - lo_p;
-            }
+            const uint32_t* pre = s_pre + c * kChunkRows;
+            const uint4 ws = reinterpret_cast<const uint4*>(s_wsum)[c];
+            const uint32_t e1 = ws.x, e2 = e1 + ws.y, e3 = e2 + ws.z;
+            // all four reads unconditional (xb = 0 when the leaf starts the chunk), then selects
+            const uint32_t ph = pre[xh], pb = pre[xb];
+            const uint32_t hi_p = ph + (wh == 0 ? 0u : wh == 1 ? e1 : wh == 2 ? e2 : e3);
+            const uint32_t lo_p = has_lo ? pb + (wb == 0 ? 0u : wb == 1 ? e1 : wb == 2 ? e2 : e3) : 0u;
+            s_acc[c * la + li] += hi_p - lo_p;
         }
         if (more) cur = nxt;
     }
