@@ -1520,6 +1520,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
         sp.out = v.split.as<uint64_t>();
         sp.topo = e->topo;
         a.row_cache_words = one_chunk ? jsp::split_row_cache_words(v.cpg, e->blk_leaves) : 0u;
+        a.anc_words = one_chunk ? jsp::split_anc_words(v.cpg, e->blk_leaves, (int)e->W, (int)e->R) : 0u;
         lds = jsp::split_service_lds_bytes(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, one_chunk);
         grid = n_tiles + 1;
     }

@@ -459,10 +459,18 @@ __device__ __forceinline__ ClassRegs<W, R> class_regs(const DevClass& d) {
 // row_cache (resident compaction service, single-chunk tiles only): the
 // tile's rows are read from this LDS copy when use_cache, else loaded and
 // copied into it.
+// staged_rt (the resident split service after its first request): the same
+// as STAGED at run time -- the class records and leaf starts an earlier
+// request staged are still in LDS (nothing else writes those words; an
+// upload restarts the service), and bt_staged is the tile's geometry. A
+// request answered from the row copy then issues no global load before its
+// row pass (cfg3: 0.52 us from the broadcast to the first chunk, one memory
+// round trip for words that never change).
 template <int W, int R, bool STAGED = false, bool SC1 = STAGED>
 __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, uint32_t* lds,
                                             uint4 bt_staged = make_uint4(0, 0, 0, 0), JSP_LDS uint32_t* clk = nullptr,
-                                            JSP_LDS u32x4* row_cache = nullptr, bool use_cache = false) {
+                                            JSP_LDS u32x4* row_cache = nullptr, bool use_cache = false,
+                                            bool staged_rt = false) {
     const int nc = (int)a.nc;
     const int nv = nc + a.do_occ;
     DevClass* s_cls = reinterpret_cast<DevClass*>(lds);
@@ -473,7 +481,8 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     uint32_t* s_pre = lds + tally_pre_off(nc, nv, la);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint4 bt = STAGED ? bt_staged : a.blk[blk];  // {first leaf, end leaf, first row, end row}
+    const bool staged = STAGED || staged_rt;
+    const uint4 bt = staged ? bt_staged : a.blk[blk];  // {first leaf, end leaf, first row, end row}
     const uint32_t l0 = bt.x, nl = bt.y - bt.x, r0 = bt.z, r1 = bt.w;
 
     // Every global load a workgroup needs before its first barrier is issued
@@ -484,8 +493,8 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     constexpr int kClsVec = (int)(sizeof(DevClass) / 16);
     static_assert(kTallyClasses * kClsVec <= kTallyThreads, "one class vector per thread");
     static_assert(kMaxBlkLeaves + 1 <= 2 * kTallyThreads, "two leaf starts per thread");
-    const bool st_cls = !STAGED && tid < nc * kClsVec;
-    const bool st_ls0 = !STAGED && (uint32_t)tid <= nl, st_ls1 = !STAGED && (uint32_t)tid + kTallyThreads <= nl;
+    const bool st_cls = !staged && tid < nc * kClsVec;
+    const bool st_ls0 = !staged && (uint32_t)tid <= nl, st_ls1 = !staged && (uint32_t)tid + kTallyThreads <= nl;
     uint4 cls_v = make_uint4(0, 0, 0, 0);
     uint32_t ls0 = 0, ls1 = 0;
     if (st_cls) cls_v = reinterpret_cast<const uint4*>(a.cls + a.c0)[tid];
@@ -3690,8 +3699,16 @@ __global__ __launch_bounds__(256) void copy_wait_kernel(const uint32_t* flag, ui
     copy_after_release(flag, tag, src, dst, n, err, err_tag, ticks, blockIdx.x, gridDim.x);
 }
 
+// anc (the resident service with a row copy): per (class slot, leaf thread)
+// one LDS word d | first << 20 | last << 28 -- the leaf's level-k domain, the
+// tile-local index of that domain's first leaf, whether the leaf ends it --
+// computed by the service's first request and read by the later ones, in
+// place of the dependent global loads of the ancestor chain and the domain's
+// leaf range (topology only: an upload restarts the service). d < 2^20 as in
+// the records; first < 256 (a split tile's leaves fit its four waves).
 __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
-                                           uint32_t seq, uint32_t* lds, uint32_t* s_x) {
+                                           uint32_t seq, uint32_t* lds, uint32_t* s_x,
+                                           JSP_LDS uint32_t* anc = nullptr, bool anc_ready = false) {
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int nc = (int)ag.nc;
     JSP_LDS const DevClass* cls_l = lds_ptr(reinterpret_cast<const DevClass*>(lds));
@@ -3723,11 +3740,20 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
             bool last = false;
             unsigned long long rec = 0;
             if (in) {
-                const uint32_t l = l0 + (uint32_t)tid;
-                const uint32_t d = leaf_ancestor(l, level, sp.topo);
-                const uint32_t beg = sp.topo.fl[level][d], end = sp.topo.fl[level][d + 1];
-                last = (uint32_t)tid + 1 == nl || l + 1 == end;
-                const uint32_t first = (beg > l0 ? beg : l0) - l0;
+                uint32_t d, first;
+                if (anc != nullptr && anc_ready) {
+                    const uint32_t w = anc[c * kTallyThreads + tid];
+                    d = w & 0xFFFFFu;
+                    first = (w >> 20) & 0xFFu;
+                    last = (w >> 28) != 0u;
+                } else {
+                    const uint32_t l = l0 + (uint32_t)tid;
+                    d = leaf_ancestor(l, level, sp.topo);
+                    const uint32_t beg = sp.topo.fl[level][d], end = sp.topo.fl[level][d + 1];
+                    last = (uint32_t)tid + 1 == nl || l + 1 == end;
+                    first = (beg > l0 ? beg : l0) - l0;
+                    if (anc != nullptr) anc[c * kTallyThreads + tid] = d | (first << 20) | ((last ? 1u : 0u) << 28);
+                }
                 const uint32_t partial = incl - (first > 0 ? s_pre[first - 1] : 0u);
                 rec = rtag | ((unsigned long long)d << 30) | partial;
             }
@@ -3796,6 +3822,10 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
     // previous request)
     JSP_LDS u32x4* row_cache = v.row_cache_words ? lds_ptr(reinterpret_cast<u32x4*>(lds + v.row_cache_words)) : nullptr;
     bool cached = false;
+    // the first request stages the class records, leaf starts and ancestor
+    // words in LDS; the later ones reuse them (tally_block staged_rt, split_emit anc)
+    bool staged = false;
+    JSP_LDS uint32_t* anc = v.anc_words ? lds_ptr(lds + v.anc_words) : nullptr;
     // this request's phase stamps (timing on). One word in: the array sits at
     // LDS address 0, which compares equal to a null LDS pointer
     __shared__ uint32_t s_clk[kSvcClkSlots + 1];
@@ -3835,12 +3865,13 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         const bool use_cache = cached && s_x[1] == 0u;
         const bool job_less = s_x[2] == 0u;  // a request without jobs: this tile writes its done word
         svc_stamp(clk, 1);
-        tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), clk, row_cache, use_cache);
+        tally_block<W, R, false, true>(ag, ft.blk, lds, bt, clk, row_cache, use_cache, staged);
         cached = row_cache != nullptr;
 #ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 2);
 #endif
-        split_emit(ag, sp, bt, out, next, lds, s_x);
+        split_emit(ag, sp, bt, out, next, lds, s_x, anc, staged);
+        staged = true;
 #ifndef JSP_AB_FINESTAMP
     svc_stamp(clk, 4);
 #endif
@@ -4148,9 +4179,14 @@ size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
 
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la) { return (uint32_t)((split_lds_bytes(cpg, la) + 15) / 16 * 4); }
 
+// the split service's ancestor words (split_emit anc), past the row copy: cpg x 256 words
+uint32_t split_anc_words(uint32_t cpg, uint32_t la, int W, int R) {
+    return split_row_cache_words(cpg, la) + (uint32_t)(2 * W + 2 + R) * 4u * kTallyThreads;
+}
+
 size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache) {
     if (!row_cache) return split_lds_bytes(cpg, la);
-    return sizeof(uint32_t) * split_row_cache_words(cpg, la) + (size_t)(2 * W + 2 + R) * 16 * kTallyThreads;
+    return sizeof(uint32_t) * ((size_t)split_anc_words(cpg, la, W, R) + (size_t)cpg * kTallyThreads);
 }
 
 template <int W, int R>
