@@ -123,6 +123,13 @@ tools/bin/ab_fine/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engin
 	@mkdir -p build/ab_fine tools/bin/ab_fine
 	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_FINESTAMP -c -o build/ab_fine/k.o jobset_amd/csrc/jsp_kernels.hip
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_fine/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+# A/B build: split-service stamps 2-4 at tally_block's entry, after its row copy, after its first barrier
+tools/bin/ab_entry/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
+	@mkdir -p build/ab_entry tools/bin/ab_entry
+	$(HIPCC) $(HIPFLAGS) $(KFLAGS) -DJSP_AB_ENTRYSTAMP -c -o build/ab_entry/k.o jobset_amd/csrc/jsp_kernels.hip
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ build/ab_entry/k.o build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) -ldl
+AB_FLAGS_noinv = -DJSP_AB_NOINV
+AB_FLAGS_entrynoinv = -DJSP_AB_NOINV -DJSP_AB_ENTRYSTAMP
 # diagnostic stamp build shipped to the GPU box (tools/bin is not gpurun-ignored)
 tools/bin/diag/libjsplace.so: jobset_amd/csrc/jsp_kernels.hip build/jsp_engine.o build/jsp_walk.o build/jsp_multi.o $(HOST_OBJ) $(HDR)
 	@mkdir -p build/diag2 tools/bin/diag

@@ -1058,6 +1058,7 @@ int split_oneshot(jsp_engine* e, const uint32_t* run_class, const uint32_t* run_
     }
     jsp::ServiceArgs a{};
     a.oneshot = seq;
+    a.anc_words = jsp::split_anc_words(cpg, e->blk_leaves, (int)e->W, (int)e->R, false);
     // the assign[] copy rides in the same launch: one extra workgroup waits
     // for the walk's release and copies (no launch between walk and copy)
     const size_t flag_off = (size_t)n_runs * 8 + (size_t)J * 4;
@@ -1520,7 +1521,7 @@ int svc_start(jsp_engine* e, uint32_t J, bool wait_ready) {
         sp.out = v.split.as<uint64_t>();
         sp.topo = e->topo;
         a.row_cache_words = one_chunk ? jsp::split_row_cache_words(v.cpg, e->blk_leaves) : 0u;
-        a.anc_words = one_chunk ? jsp::split_anc_words(v.cpg, e->blk_leaves, (int)e->W, (int)e->R) : 0u;
+        a.anc_words = jsp::split_anc_words(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, one_chunk);
         lds = jsp::split_service_lds_bytes(v.cpg, e->blk_leaves, (int)e->W, (int)e->R, one_chunk);
         grid = n_tiles + 1;
     }

@@ -257,8 +257,8 @@ struct ServiceArgs {
     uint32_t* ready;                    // host-mapped: the dispatcher writes gen once it polls
     uint32_t gen;                       // service launch number
     uint32_t row_cache_words;           // split shape: LDS word offset of the tiles' row copy, 0 = none
-    uint32_t anc_words;                 // split shape with a row copy: LDS word offset of the tiles'
-                                        //   ancestor words (split_anc_words), 0 = none
+    uint32_t anc_words;                 // split shape: LDS word offset of the tiles' ancestor words
+                                        //   (split_anc_words), 0 = none
     // XCD co-location (compaction shape): the grid is spread x (tiles + 1)
     // workgroups and only those with blockIdx % spread == 0 stay -- one XCD
     // under the round-robin dealing of workgroups to XCDs. Each survivor
@@ -417,7 +417,7 @@ hipError_t launch_split_oneshot(const TallyArgs& a, const SplitArgs& sp, const S
 size_t split_lds_bytes(uint32_t cpg, uint32_t la);
 // the split service's LDS: split_lds_bytes, then (row_cache) the tile's rows
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la);
-uint32_t split_anc_words(uint32_t cpg, uint32_t la, int W, int R);
+uint32_t split_anc_words(uint32_t cpg, uint32_t la, int W, int R, bool row_cache);
 size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache);
 // Workgroups of the resident service kernel (shape 2 compaction, 3 split) of
 // this W/R that one CU holds at once with lds_bytes each (occupancy API).

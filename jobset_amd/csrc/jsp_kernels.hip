@@ -481,6 +481,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     uint32_t* s_pre = lds + tally_pre_off(nc, nv, la);
 
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+#ifdef JSP_AB_ENTRYSTAMP
+    svc_stamp(clk, 2);  // A/B build: slots 2-4 at the block's entry, after its row copy, after the first barrier
+#endif
     const bool staged = STAGED || staged_rt;
     const uint4 bt = staged ? bt_staged : a.blk[blk];  // {first leaf, end leaf, first row, end row}
     const uint32_t l0 = bt.x, nl = bt.y - bt.x, r0 = bt.z, r1 = bt.w;
@@ -508,6 +511,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
     RowRegs<W, R> cur;
     if (row_cache != nullptr && use_cache) {
         rows_from_lds<W, R>(row_cache, tid, cur);
+#ifdef JSP_AB_ENTRYSTAMP
+        svc_stamp(clk, 3);
+#endif
     } else {
         const uint32_t row = base0 + 4u * tid;
         load_rows<W, R, SC1>(a, row, (row < r1) && (row + 3 >= r0), cur);
@@ -525,6 +531,9 @@ __device__ __forceinline__ void tally_block(const TallyArgs& a, uint32_t blk, ui
         for (int i = 0; i < 4; ++i) valid[i] = any && (row + i >= r0) && (row + i < r1);
         __syncthreads();  // s_cls / s_ls / s_acc ready (first chunk); previous leaf pass done (later ones)
         JSP_STAMP(blk, 1);
+#ifdef JSP_AB_ENTRYSTAMP
+        if (base == base0) svc_stamp(clk, 4);
+#endif
 #ifdef JSP_AB_FINESTAMP
         svc_stamp(clk, 2);  // A/B build: slots 2-4 inside the row pass (compact_tile's are dropped)
 #endif
@@ -3699,13 +3708,17 @@ __global__ __launch_bounds__(256) void copy_wait_kernel(const uint32_t* flag, ui
     copy_after_release(flag, tag, src, dst, n, err, err_tag, ticks, blockIdx.x, gridDim.x);
 }
 
-// anc (the resident service with a row copy): per (class slot, leaf thread)
-// one LDS word d | first << 20 | last << 28 -- the leaf's level-k domain, the
-// tile-local index of that domain's first leaf, whether the leaf ends it --
-// computed by the service's first request and read by the later ones, in
-// place of the dependent global loads of the ancestor chain and the domain's
-// leaf range (topology only: an upload restarts the service). d < 2^20 as in
-// the records; first < 256 (a split tile's leaves fit its four waves).
+// anc: per (upper level k, leaf thread) one LDS word d | first << 20 |
+// last << 28 -- the leaf's level-k domain, the block-local index of that
+// domain's first leaf, whether the leaf ends it. The first upper class of a
+// level walks the hierarchy tables (dependent global loads) and leaves the
+// words there; the level's other classes, and a resident tile's later
+// requests (anc_ready: topology only, an upload restarts the service), read
+// them. On gfx9 vmcnt counts stores, so each of those global loads also
+// waited for the previous class's system-scope record stores (a link round
+// trip): cfg5's resident request 4.99 -> 3.89 us on the device.
+// d < 2^20 as in the records; first < 256 (a split tile's leaves fit its
+// four waves).
 __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
                                            uint32_t seq, uint32_t* lds, uint32_t* s_x,
                                            JSP_LDS uint32_t* anc = nullptr, bool anc_ready = false) {
@@ -3717,12 +3730,13 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
     // the tile's lines, gathered here and written by one pass of stores
     JSP_LDS uint32_t* s_line = lds_ptr(s_x + 16 + kTallyThreads);
     const uint32_t nw = sp.nw, n_line = split_line_words(sp.cpg, nw);
-    if ((uint32_t)tid < n_line) s_line[tid] = 0u;
-    __syncthreads();
     const uint32_t la = ag.la;
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
     const bool in = (uint32_t)tid < nl;
+    if ((uint32_t)tid < n_line) s_line[tid] = 0u;
+    __syncthreads();
     const uint32_t K = sp.topo.K;
+    uint32_t anc_lv = anc_ready ? 0xFu : 0u;  // bit k: level k's words are in anc
     const unsigned long long rtag = (unsigned long long)split_rec_tag(seq) << 50;
     for (int c = 0; c < nc; ++c) {
         const uint32_t level = to_sgpr(cls_l[c].level), pods = to_sgpr(cls_l[c].pods);
@@ -3741,8 +3755,8 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
             unsigned long long rec = 0;
             if (in) {
                 uint32_t d, first;
-                if (anc != nullptr && anc_ready) {
-                    const uint32_t w = anc[c * kTallyThreads + tid];
+                if (anc != nullptr && ((anc_lv >> level) & 1u)) {
+                    const uint32_t w = anc[level * kTallyThreads + tid];
                     d = w & 0xFFFFFu;
                     first = (w >> 20) & 0xFFu;
                     last = (w >> 28) != 0u;
@@ -3752,11 +3766,12 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
                     const uint32_t beg = sp.topo.fl[level][d], end = sp.topo.fl[level][d + 1];
                     last = (uint32_t)tid + 1 == nl || l + 1 == end;
                     first = (beg > l0 ? beg : l0) - l0;
-                    if (anc != nullptr) anc[c * kTallyThreads + tid] = d | (first << 20) | ((last ? 1u : 0u) << 28);
+                    if (anc != nullptr) anc[level * kTallyThreads + tid] = d | (first << 20) | ((last ? 1u : 0u) << 28);
                 }
                 const uint32_t partial = incl - (first > 0 ? s_pre[first - 1] : 0u);
                 rec = rtag | ((unsigned long long)d << 30) | partial;
             }
+            if (anc != nullptr) anc_lv |= 1u << level;  // each thread reads back only its own words
             const uint64_t m = __ballot(last);
             uint64_t* recs = out + n_line + ((size_t)c * nw + wid) * kSplitRecs;
             if (last) __hip_atomic_store(recs + mbcnt64(m), rec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3813,7 +3828,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
             __threadfence_system();  // before this tile's lines, which the host waits for
         }
         tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, nullptr, false);
-        split_emit(ag, sp, bt, out, v.oneshot, lds, s_x);
+        split_emit(ag, sp, bt, out, v.oneshot, lds, s_x, v.anc_words ? lds_ptr(lds + v.anc_words) : nullptr, false);
         return;
     }
     uint32_t seq = v.seq0;
@@ -3867,12 +3882,12 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         svc_stamp(clk, 1);
         tally_block<W, R, false, true>(ag, ft.blk, lds, bt, clk, row_cache, use_cache, staged);
         cached = row_cache != nullptr;
-#ifndef JSP_AB_FINESTAMP
+#if !defined(JSP_AB_FINESTAMP) && !defined(JSP_AB_ENTRYSTAMP)
     svc_stamp(clk, 2);
 #endif
         split_emit(ag, sp, bt, out, next, lds, s_x, anc, staged);
         staged = true;
-#ifndef JSP_AB_FINESTAMP
+#if !defined(JSP_AB_FINESTAMP) && !defined(JSP_AB_ENTRYSTAMP)
     svc_stamp(clk, 4);
 #endif
         if (!clk_out) {
@@ -3888,7 +3903,9 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         }
         // drop this CU's L1 lines before the next request (patches come from
         // other launches), off the request path
+#ifndef JSP_AB_NOINV
         if (threadIdx.x == 0) asm volatile("buffer_inv sc1" ::: "memory");  // no wait for the done word's store
+#endif
         seq = next;
         __syncthreads();  // s_x and the tally carve are rewritten by the next request
     }
@@ -4179,14 +4196,14 @@ size_t split_lds_bytes(uint32_t cpg, uint32_t la) {
 
 uint32_t split_row_cache_words(uint32_t cpg, uint32_t la) { return (uint32_t)((split_lds_bytes(cpg, la) + 15) / 16 * 4); }
 
-// the split service's ancestor words (split_emit anc), past the row copy: cpg x 256 words
-uint32_t split_anc_words(uint32_t cpg, uint32_t la, int W, int R) {
-    return split_row_cache_words(cpg, la) + (uint32_t)(2 * W + 2 + R) * 4u * kTallyThreads;
+// the split tiles' ancestor words (split_emit anc): (kMaxLevels - 1) x 256
+// words past the row copy, or past the tally carve without one
+uint32_t split_anc_words(uint32_t cpg, uint32_t la, int W, int R, bool row_cache) {
+    return split_row_cache_words(cpg, la) + (row_cache ? (uint32_t)(2 * W + 2 + R) * 4u * kTallyThreads : 0u);
 }
 
 size_t split_service_lds_bytes(uint32_t cpg, uint32_t la, int W, int R, bool row_cache) {
-    if (!row_cache) return split_lds_bytes(cpg, la);
-    return sizeof(uint32_t) * ((size_t)split_anc_words(cpg, la, W, R) + (size_t)cpg * kTallyThreads);
+    return sizeof(uint32_t) * ((size_t)split_anc_words(cpg, la, W, R, row_cache) + (kMaxLevels - 1) * kTallyThreads);
 }
 
 template <int W, int R>
