@@ -1,4 +1,6 @@
-# same-box A/B: the product library against tools/bin/ab_prev (the previous kernels), alternating
+# Same-box A/B: the product library against tools/bin/ab_prev/libjsplace.so (a build of the previous kernels),
+# alternating, on configs $CFGS (default 5,3): tools/devpath_loop.py twice each, then tools/svc_probe.py.
+#   TAG=name CFGS=5,3 bash scripts/ab_same_box.sh
 set -u
 cd "$GRAFT_REPO_ROOT"; OUT=gpurun_out/r6/${TAG:-ab}; mkdir -p $OUT
 for v in new prev new2 prev2; do

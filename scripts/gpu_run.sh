@@ -9,6 +9,7 @@
 #   ceiling   tools/bin/stream_ceiling (read / copy ceilings at the kernels' byte counts)
 #   bin:NAME  tools/bin/NAME (a compiled probe) -> NAME.json
 #   probes    tools/svc_probe.py + tools/host_api_probe.py
+#   devloop   tools/devpath_loop.py (device paths and host API of cfg5, cfg3)
 #   trace     rocprofv3 --kernel-trace --stats of the bench (no CPU legs)
 #   pmc       separate rocprofv3 --pmc passes (FETCH_SIZE / WRITE_SIZE / SQ) on configs 2, 4, 5
 #   py:FILE[:ARG]  python FILE ARG (a probe under tools/) -> FILE_ARG.txt
@@ -40,6 +41,7 @@ for step in "$@"; do
     bin:*)   b="${step#bin:}"; run 120 "$OUT/$b.json" "tools/bin/$b"; cat "$OUT/$b.json" ;;
     probes)  run 200 "$OUT/svc_probe.txt" python3 tools/svc_probe.py 2000
              run 240 "$OUT/host_api_phases.txt" python3 tools/host_api_probe.py ;;
+    devloop) run 300 "$OUT/devpath_loop.txt" python3 tools/devpath_loop.py 5,3 3; cat "$OUT/devpath_loop.txt" ;;
     trace)   ( cd /tmp && export TMPDIR=/tmp && run 500 "$OUT/bench_trace.log" rocprofv3 --kernel-trace --stats -d "$OUT/bench_trace" -o run --output-format csv -- python3 "$R/bench.py" --trials 100 --cold-trials 0 --cpu-seconds 0 ) || exit $?
              python3 tools/summarize_prof.py "$OUT" > "$OUT/summary.txt" 2>&1 ;;
     pmc)     ( cd /tmp && export TMPDIR=/tmp
