@@ -3719,6 +3719,14 @@ __global__ __launch_bounds__(256) void copy_wait_kernel(const uint32_t* flag, ui
 // trip): cfg5's resident request 4.99 -> 3.89 us on the device.
 // d < 2^20 as in the records; first < 256 (a split tile's leaves fit its
 // four waves).
+// The tile's answer line words start at zero (split_emit writes only the
+// ballots and counts it has); zeroed before the tally, whose barriers order
+// it before split_emit's writes (no barrier of its own).
+__device__ __forceinline__ void split_zero_line(const SplitArgs& sp, uint32_t* s_x) {
+    JSP_LDS uint32_t* s_line = lds_ptr(s_x + 16 + kTallyThreads);
+    if ((uint32_t)threadIdx.x < split_line_words(sp.cpg, sp.nw)) s_line[threadIdx.x] = 0u;
+}
+
 __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs& sp, uint4 bt, uint64_t* out,
                                            uint32_t seq, uint32_t* lds, uint32_t* s_x,
                                            JSP_LDS uint32_t* anc = nullptr, bool anc_ready = false) {
@@ -3733,14 +3741,14 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
     const uint32_t la = ag.la;
     const uint32_t l0 = bt.x, nl = bt.y - bt.x;
     const bool in = (uint32_t)tid < nl;
-    if ((uint32_t)tid < n_line) s_line[tid] = 0u;
-    __syncthreads();
+    // s_line was zeroed before the tally (split_zero_line), whose barriers order it
     const uint32_t K = sp.topo.K;
     uint32_t anc_lv = anc_ready ? 0xFu : 0u;  // bit k: level k's words are in anc
     const unsigned long long rtag = (unsigned long long)split_rec_tag(seq) << 50;
     for (int c = 0; c < nc; ++c) {
         const uint32_t level = to_sgpr(cls_l[c].level), pods = to_sgpr(cls_l[c].pods);
-        const uint32_t cap = in ? s_acc[c * la + tid] : 0u;
+        const uint32_t cap_r = s_acc[c * la + tid];  // in the tally carve for every tid: read with the class words
+        const uint32_t cap = in ? cap_r : 0u;
         if (level + 1 == K) {
             const uint64_t word = __ballot(in && cap >= pods);
             if (lane < 2 && (uint32_t)wid < nw)
@@ -3780,7 +3788,8 @@ __device__ __forceinline__ void split_emit(const TallyArgs& ag, const SplitArgs&
         }
     }
     if (ag.do_occ) {
-        const uint32_t o = in ? s_acc[nc * la + tid] : 0u;
+        const uint32_t o_r = s_acc[nc * la + tid];
+        const uint32_t o = in ? o_r : 0u;
         const uint64_t word = __ballot(in && o != 0u);
         if (lane < 2 && (uint32_t)wid < nw)
             s_line[2 * (sp.cpg * nw + wid) + lane] = lane == 0 ? (uint32_t)word : (uint32_t)(word >> 32);
@@ -3827,6 +3836,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
             }
             __threadfence_system();  // before this tile's lines, which the host waits for
         }
+        split_zero_line(sp, s_x);
         tally_block<W, R, false, true>(ag, ft.blk, lds, make_uint4(0, 0, 0, 0), nullptr, nullptr, false);
         split_emit(ag, sp, bt, out, v.oneshot, lds, s_x, v.anc_words ? lds_ptr(lds + v.anc_words) : nullptr, false);
         return;
@@ -3880,6 +3890,7 @@ __global__ __launch_bounds__(kTallyThreads) void place_split_service_kernel(Tall
         const bool use_cache = cached && s_x[1] == 0u;
         const bool job_less = s_x[2] == 0u;  // a request without jobs: this tile writes its done word
         svc_stamp(clk, 1);
+        split_zero_line(sp, s_x);
         tally_block<W, R, false, true>(ag, ft.blk, lds, bt, clk, row_cache, use_cache, staged);
         cached = row_cache != nullptr;
 #if !defined(JSP_AB_FINESTAMP) && !defined(JSP_AB_ENTRYSTAMP)
