@@ -19,12 +19,6 @@ namespace jsp {
 
 namespace {
 
-inline void or_bits(uint64_t* g, uint32_t pos, uint64_t x) {
-    const uint32_t w = pos >> 6, b = pos & 63u;
-    g[w] |= x << b;
-    if (b != 0) g[w + 1] |= x >> (64u - b);
-}
-
 inline void set_range(uint64_t* t, uint32_t lo, uint32_t hi) {
     while (lo < hi) {
         const uint32_t w = lo >> 6, b = lo & 63u;
@@ -152,19 +146,51 @@ static inline uint64_t line_word(const uint64_t* lines, uint32_t nw, uint32_t j,
     return (p[0] & 0xFFFFFFFFull) | (p[1] << 32);
 }
 
+// Bitmap words built from 64-bit pieces at nondecreasing bit positions (the
+// tiles' ballots, in leaf order) into a zeroed bitmap: the two words a piece
+// touches are kept in registers and written once they are passed, instead of
+// a read-modify-write per piece (cfg3's 80 tiles: a store-to-load chain).
+struct BitAppender {
+    uint64_t* g;
+    uint32_t w = 0;
+    uint64_t a0 = 0, a1 = 0;
+    explicit BitAppender(uint64_t* g_) : g(g_) {}
+    inline void add(uint32_t pos, uint64_t x) {
+        const uint32_t pw = pos >> 6, b = pos & 63u;
+        if (pw != w) {
+            g[w] |= a0;
+            if (pw == w + 1) {
+                a0 = a1;
+            } else {
+                g[w + 1] |= a1;
+                a0 = 0;
+            }
+            a1 = 0;
+            w = pw;
+        }
+        a0 |= x << b;
+        if (b != 0) a1 |= x >> (64u - b);
+    }
+    inline void flush() {
+        g[w] |= a0;
+        g[w + 1] |= a1;
+    }
+};
+
 void HostWalk::build_feasibility(const uint64_t* slots) {
     const size_t tile_words = split_tile_words(cpg_, nw_);
     const uint32_t n_line = split_line_words(cpg_, nw_);
     const uint32_t nb = (uint32_t)l0_.size();
     // occupied leaves, from the group-0 tiles
     std::fill(occ_.begin(), occ_.end(), 0ull);
-    for (uint32_t b = 0; b < nb; ++b) {
-        const uint64_t* s = slots + (size_t)(b * groups_) * tile_words;
-        const uint32_t nl = l1_[b] - l0_[b];
-        for (uint32_t w = 0; 64 * w < nl; ++w) {
-            const uint64_t x = line_word(s, nw_, cpg_, w);
-            if (x) or_bits(occ_.data(), l0_[b] + 64 * w, x);
+    {
+        BitAppender ap(occ_.data());
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint64_t* s = slots + (size_t)(b * groups_) * tile_words;
+            const uint32_t nl = l1_[b] - l0_[b];
+            for (uint32_t w = 0; 64 * w < nl; ++w) ap.add(l0_[b] + 64 * w, line_word(s, nw_, cpg_, w));
         }
+        ap.flush();
     }
     // occupied domains above the leaves (only levels some class places at)
     if (any_upper_) {
@@ -184,14 +210,13 @@ void HostWalk::build_feasibility(const uint64_t* slots) {
         const uint32_t g = c / cpg_, j = c % cpg_, k = level_[c], pods = pods_[c];
         uint64_t* F = feas_.data() + woff_[c];
         if (k + 1 == K_) {
+            BitAppender ap(F);
             for (uint32_t b = 0; b < nb; ++b) {
                 const uint64_t* s = slots + (size_t)(b * groups_ + g) * tile_words;
                 const uint32_t nl = l1_[b] - l0_[b];
-                for (uint32_t w = 0; 64 * w < nl; ++w) {
-                    const uint64_t x = line_word(s, nw_, j, w);
-                    if (x) or_bits(F, l0_[b] + 64 * w, x);
-                }
+                for (uint32_t w = 0; 64 * w < nl; ++w) ap.add(l0_[b] + 64 * w, line_word(s, nw_, j, w));
             }
+            ap.flush();
             const uint32_t nw = woff_[c + 1] - woff_[c];
             for (uint32_t w = 0; w < nw; ++w) F[w] &= ~occ_[w];
         } else {
@@ -219,19 +244,20 @@ void HostWalk::build_feasibility(const uint64_t* slots) {
 
 // Taking domain d at level k (its own bit is set by the caller) takes its
 // ancestors and its descendants at every other level.
+// (the per-level table pointers are set up by walk(): raw pointers, not a
+// vector lookup per level and job)
 void HostWalk::take_marks(uint32_t d, uint32_t k) {
-    const uint32_t* fl = fl_[k].data();
-    if (fl[d] == fl[d + 1]) return;  // an empty domain intersects nothing (never feasible)
+    if (k + 1 < K_ && lv_fl_[k][d] == lv_fl_[k][d + 1]) return;  // an empty domain intersects nothing
     uint32_t dd = d;
     for (int kk = (int)k - 1; kk >= 0; --kk) {
-        dd = (uint32_t)par_[kk + 1][dd];
-        taken_[toff_[kk] + (dd >> 6)] |= 1ull << (dd & 63);
+        dd = (uint32_t)lv_par_[kk + 1][dd];
+        lv_t_[kk][dd >> 6] |= 1ull << (dd & 63);
     }
     uint32_t lo = d, hi = d + 1;
     for (uint32_t kk = k + 1; kk < K_; ++kk) {
-        lo = cs_[kk - 1][lo];
-        hi = cs_[kk - 1][hi];
-        set_range(taken_.data() + toff_[kk], lo, hi);
+        lo = lv_cs_[kk - 1][lo];
+        hi = lv_cs_[kk - 1][hi];
+        set_range(lv_t_[kk], lo, hi);
     }
 }
 
@@ -268,6 +294,12 @@ void HostWalk::prefetch_state() const {
 uint32_t HostWalk::walk(const uint64_t* feas, const uint32_t* run_class, const uint32_t* run_len, uint32_t n_runs,
                         int32_t* assign) {
     std::fill(taken_.begin(), taken_.end(), 0ull);
+    for (uint32_t k = 0; k < K_; ++k) {
+        lv_t_[k] = taken_.data() + toff_[k];
+        lv_fl_[k] = fl_[k].data();
+        lv_cs_[k] = cs_[k].data();
+        lv_par_[k] = par_[k].data();
+    }
     // per class, everything a run needs in one record (cfg5: ~500 runs of one
     // job each, so the per-run set-up is most of the walk)
     cw_.resize(C_);

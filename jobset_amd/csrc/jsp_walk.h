@@ -87,6 +87,11 @@ private:
     std::vector<uint64_t> sums_;             // clamped capacity sums of every upper class's domains (uoff_ layout)
     std::vector<uint64_t> taken_;            // taken domains per level (toff_ layout)
     std::vector<ClassWalk> cw_;              // per class, set up per request
+    // per level, set up per walk: taken words, first leaf, child start, parent
+    uint64_t* lv_t_[kMaxLevels] = {nullptr, nullptr, nullptr, nullptr};
+    const uint32_t* lv_fl_[kMaxLevels] = {nullptr, nullptr, nullptr, nullptr};
+    const uint32_t* lv_cs_[kMaxLevels] = {nullptr, nullptr, nullptr, nullptr};
+    const int32_t* lv_par_[kMaxLevels] = {nullptr, nullptr, nullptr, nullptr};
     bool any_upper_ = false;
 };
 
