@@ -73,6 +73,7 @@ KERNEL = {0: "tally_kernel", 1: "place_fused_kernel", 2: "place_compact_kernel",
 # cold recovery: the gap between the patch and the place (ms) -> share of --cold-trials
 COLD_GAPS = {1.0: 1.0, 0.0: 0.1, 10.0: 0.1}
 COLD_SLEEP_EXTRA_MS = 5.0  # a trial sleeps the idle limit plus this (the service has left)
+COLD_WARM = 2  # untimed trials before each cold leg, GPU and CPU alike
 
 
 def tally_bytes(p) -> int:
@@ -327,6 +328,9 @@ def cold_recovery_latency(eng, p, plan, idle_ms: float):
     out = {}
     for gap, trials in plan.items():
         rows, vals = _recovery_rows(p, trials, gap)
+        # COLD_WARM untimed trials first (as the CPU leg): the leg's first
+        # trial after a mode change or another leg is not a recovery's
+        call.recovery(COLD_WARM, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows[:COLD_WARM], vals[:COLD_WARM])
         eng.timing(reset=True)
         res = call.recovery(trials, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows, vals)
         t = eng.timing(reset=True)
@@ -356,6 +360,8 @@ def cpu_cold_recovery(p, plan, threads, idle_ms: float):
             fc.run()
             n = trials if th == max(threads) else max(20, trials // 5)
             rows, vals = _recovery_rows(p, n, gap)
+            fc.recovery_loop(COLD_WARM, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows[:COLD_WARM],
+                             vals[:COLD_WARM])  # untimed, as the GPU leg's
             res = fc.recovery_loop(n, (idle_ms + COLD_SLEEP_EXTRA_MS) * 1e3, gap * 1e3, rows, vals)
             fc.close()
             legs[f"{th}t"] = pcts((res[:, 0] + res[:, 1]).tolist())
