@@ -283,6 +283,35 @@ def test_fused_service_random_parity(svc_engine, seed):
     np.testing.assert_array_equal(ref.assign, a)
 
 
+@pytest.mark.parametrize("seed", range(12))
+def test_split_tiles_reuse_staged_words(svc_engine, seed):
+    """Round 6: a resident split tile stages its class records, leaf starts
+    and per-upper-level ancestor words in LDS at its first request and reuses
+    them. Four-level ragged snapshots with classes at every level (several per
+    level: the words are shared per level), requests with and without rows
+    patched in between (dirty rows reload, the staged words stay), every answer
+    against the oracle of the snapshot as patched."""
+    p = synth.random_problem(7300 + seed, max_nodes=12_000, max_levels=4, max_leaves=600, max_jobs=400)
+    K = p.topology.n_levels
+    for i, c in enumerate(p.classes):  # spread the classes over the levels
+        c.level = i % K
+    svc_engine.load(p)
+    rng = np.random.default_rng(seed)
+    call = svc_engine.host_placer(*job_runs(p.job_class))
+    call()
+    shapes = set()
+    for step in range(6):
+        if step in (2, 4):
+            rows = np.sort(rng.choice(p.nodes.n_nodes, size=min(3, p.nodes.n_nodes), replace=False)).astype(np.uint32)
+            taints = rng.integers(0, 4, size=rows.shape[0]).astype(np.uint32)
+            svc_engine.patch_rows(rows, taints=taints)
+            p.nodes.taints[rows] = taints
+        st = call()
+        shapes.add(st.fused)
+        np.testing.assert_array_equal(call.assign, O.place_c(p)[0], err_msg=f"seed {seed} step {step}")
+    assert shapes <= {0, 1, 2, 3, 5, 7, 8}, shapes  # (the split service when the tiles fit: fused 5)
+
+
 def test_fused_service_patch_and_device_path(svc_engine):
     """cfg5 resident while device-path launches (their own tally buffers) and
     patches interleave with its requests."""
