@@ -818,8 +818,9 @@ def main() -> None:
         d["cold2"] = cold
         # the same recovery with the service parked (JSP_SERVICE_PARKED: no
         # idle exit, a dedicated GPU -- the GPU side of the CPU pool's
-        # spinning threads), at the short gaps' sample size
-        plan_p = {g: n for g, n in cold_plan(max(20, args.cold_trials // 10), {1.0: 1.0, 0.0: 1.0}).items()}
+        # spinning threads): the 1 ms gap at the headline's sample size (its
+        # p99 beside the CPU leg's at equal n), no gap at the short gaps'
+        plan_p = {1.0: args.cold_trials, 0.0: max(20, args.cold_trials // 10)}
         eng.set_service(True, parked=True)
         settled_place(eng, p.job_class)
         gp = cold_recovery_latency(eng, p, plan_p, idle_ms)
