@@ -76,6 +76,17 @@ COLD_SLEEP_EXTRA_MS = 5.0  # a trial sleeps the idle limit plus this (the servic
 COLD_WARM = 2  # untimed trials before each cold leg, GPU and CPU alike
 
 
+_T0 = time.perf_counter()
+_PROGRESS = True  # rank 0 only (set in main)
+
+
+def progress(msg: str) -> None:
+    """One short line on stderr per phase: the run's progress (a silent run of
+    minutes reads as hung to a watchdog), before the one JSON line on stdout."""
+    if _PROGRESS:
+        print(f"bench: {msg} ({time.perf_counter() - _T0:.0f} s)", file=sys.stderr, flush=True)
+
+
 def tally_bytes(p) -> int:
     """Algorithmic bytes of one tally launch: every node row read once
     (labels 8W + taints 4 + free 4R + excl 4 B), leaf offsets read,
@@ -327,6 +338,7 @@ def cold_recovery_latency(eng, p, plan, idle_ms: float):
     call()
     out = {}
     for gap, trials in plan.items():
+        progress(f"cold recovery ({p.name}), gap {gap:g} ms, {trials} trials")
         rows, vals = _recovery_rows(p, trials, gap)
         # COLD_WARM untimed trials first (as the CPU leg): the leg's first
         # trial after a mode change or another leg is not a recovery's
@@ -355,6 +367,7 @@ def cpu_cold_recovery(p, plan, threads, idle_ms: float):
     for gap, trials in plan.items():
         legs = {}
         for th in threads:
+            progress(f"CPU cold recovery ({p.name}), gap {gap:g} ms, {th} threads")
             fc = O.FastCPU(th)
             fc.prepare(p)
             fc.run()
@@ -673,6 +686,9 @@ def main() -> None:
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    global _PROGRESS
+    _PROGRESS = rank == 0
+    progress(f"start: {world} rank(s), steps {args.steps}, warmup {args.warmup}")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1:
@@ -704,6 +720,7 @@ def main() -> None:
         return step, out
 
     # ------------------------------------------------ config 2: host-API placements/s (value)
+    progress("config 2: host-API placements/s")
     p = synth.config2()
     eng.load(p)
     J = p.n_jobs
@@ -766,6 +783,7 @@ def main() -> None:
         c2["link_floor_p50_us"], c2["link_floor_p99_us"] = round(floor[0], 2), round(floor[1], 2)
 
     # ------------------------------------------------ config 2: kernel-only (device-resident runs and assign)
+    progress("config 2: kernel-only")
     step, out = device_step(p)
     for _ in range(args.warmup):
         step()
@@ -806,6 +824,7 @@ def main() -> None:
                       "trace_median_us": tr_us, "trace_source": tr_src}
 
     # ------------------------------------------------ recovery latency (rank 0)
+    progress("config 2: recovery latency")
     if rank == 0 and args.trials > 0:
         c2["warm_trials"] = host_api_latency(eng, p, args.trials, synth.config2)
     plan2 = cold_plan(args.cold_trials) if rank == 0 else {}
@@ -832,6 +851,7 @@ def main() -> None:
         d["cold2_parked"] = parked
 
     # ------------------------------------------------ CPU baseline (rank 0, N=1 only): optimized evaluator
+    progress("config 2: CPU baseline legs")
     if do_cpu:
         legs = cpu_legs(p, call.assign, sorted({1, 2, T}), args.cpu_seconds, placed)
         best = max(legs, key=lambda x: x["placements_per_s"])  # the fastest leg is the baseline
@@ -845,9 +865,11 @@ def main() -> None:
             c2["cpu_patched_best_us"] = min(legs_p.values())
 
     # ------------------------------------------------ configs 1, 3, 5 (one GPU)
+    progress("configs 1, 3, 5")
     if rank == 0 and not args.no_configs:
         configs = {}
         for cfg in (1, 3, 5):
+            progress(f"config {cfg}")
             pc = synth.CONFIGS[cfg]()
             eng.load(pc)
             r = settled_place(eng, pc.job_class)
@@ -909,6 +931,7 @@ def main() -> None:
         eng.load(p)
 
     # ------------------------------------------------ config 4: 1M nodes, sharded over the ranks
+    progress("config 4")
     if not args.no_cfg4:
         p4 = synth.config4()
         sp = ShardedPlacement(Engine(local) if world > 1 else eng, p4, rank, world, stream)
@@ -978,6 +1001,7 @@ def main() -> None:
         del scrub
         sp.engine.check()
         if do_cpu:
+            progress("config 4: CPU legs")
             legs4 = cpu_legs(p4, a4, sorted({1, 2, T}), max(1.5, args.cpu_seconds / 2), placed4)
             best4 = max(legs4, key=lambda x: x["placements_per_s"])
             c4["cpu_baseline"] = {"value": best4["placements_per_s"], "cores": best4["threads"],
@@ -988,6 +1012,7 @@ def main() -> None:
         # (ids {0, 0} on a one-GPU box: two shards, on-device add)
         barrier(world)
         if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
+            progress("config 4: device set")
             c4["device_set"] = device_set_leg(p4, a4, max(20, args.steps))
             torch.cuda.set_device(local)  # the rank's own device for the barrier (the library restores it too)
         barrier(world)
