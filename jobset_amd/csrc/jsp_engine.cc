@@ -175,6 +175,8 @@ struct TestHooks {
     bool warm = true;               // warm=0: no call-entry prefetch of the engine's lines (A/B)
     uint32_t micro_spins = 1u << 22;  // micro_spins=N: a resident tile's passes over the microbox (kErrMicro)
     uint32_t waker_poll_us = 200;   // waker_poll_us=N: the armed waker's poll period; 0 = condition variable only
+    bool waker_spin = false;        // waker_spin=1: the armed waker spins instead of sleeping (A/B: a host core
+                                    //   kept awake, as the CPU evaluator's pool threads are)
 };
 
 TestHooks read_hooks() {
@@ -207,6 +209,7 @@ TestHooks read_hooks() {
         else if (k == "warm") h.warm = v != 0;
         else if (k == "micro_spins") h.micro_spins = (uint32_t)v;
         else if (k == "waker_poll_us") h.waker_poll_us = (uint32_t)v;
+        else if (k == "waker_spin") h.waker_spin = v != 0;
         else if (k == "seq0") {
             h.seq0 = (uint32_t)v;
             h.have_seq0 = true;
@@ -2038,7 +2041,11 @@ void waker_main(jsp_engine* e) {
         }
         if (period.count() > 0 && e->waker_poll.load(std::memory_order_acquire)) {
             e->waker_polling.store(true, std::memory_order_release);
-            std::this_thread::sleep_for(period);
+            if (e->hooks.waker_spin) {
+                for (int i = 0; i < 64; ++i) __builtin_ia32_pause();
+            } else {
+                std::this_thread::sleep_for(period);
+            }
             continue;
         }
         e->waker_polling.store(false, std::memory_order_release);
