@@ -217,7 +217,10 @@ typedef struct jsp_metrics {
                                   GPU analogue of a CPU pool whose threads spin). It leaves on
                                   jsp_engine_service_stop, an upload, a mode change or destroy;
                                   a device-wide synchronize needs the stop first. JSP_SERVICE=parked
-                                  in the environment selects it. */
+                                  in the environment selects it. Freeing device memory waits for
+                                  every kernel on the device as well: with several engines on one
+                                  GPU, stop a parked service before another engine's destroy or
+                                  re-upload (whose frees would otherwise wait for it). */
 
 /* ---- lifecycle ---- */
 int jsp_abi_version(void);
