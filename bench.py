@@ -1011,7 +1011,9 @@ def main() -> None:
         # process would drive, main.go:161-190): rank 0 opens every visible GPU
         # (ids {0, 0} on a one-GPU box: two shards, on-device add)
         barrier(world)
-        if rank == 0 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
+        # (one process only: under torchrun the ranks' own process group and
+        # engines hold the GPUs, and the device set's RCCL would sit beside it)
+        if rank == 0 and world == 1 and os.environ.get("JSP_BENCH_DEVICE_SET", "1") != "0":
             progress("config 4: device set")
             c4["device_set"] = device_set_leg(p4, a4, max(20, args.steps))
             torch.cuda.set_device(local)  # the rank's own device for the barrier (the library restores it too)
