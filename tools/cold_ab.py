@@ -31,7 +31,10 @@ def main():
     rows = np.array([(i * 7919) % p.nodes.n_nodes for i in range(trials)], dtype=np.uint32)
     vals = np.ascontiguousarray(p.nodes.taints[rows], dtype=np.uint32)
     engines = {}
-    for label, hooks in (("default", None), ("waker_spin", "waker_spin=1"), ("parked", None)):
+    variants = os.environ.get("COLD_AB_VARIANTS", "default,waker_spin,parked").split(",")
+    hooks_of = {"default": None, "waker_spin": "waker_spin=1", "poll50": "waker_poll_us=50",
+                "poll20": "waker_poll_us=20", "parked": None}
+    for label, hooks in ((v, hooks_of[v]) for v in variants):
         if hooks:
             os.environ["JSP_TEST_HOOKS"] = hooks
         e = Engine(0)
